@@ -1,0 +1,408 @@
+"""CPU ORACLE for the Fourier-basis GP residual synthesis path — TEST INFRASTRUCTURE ONLY.
+
+This module is a plain numpy restatement of the reference algorithm
+(mfalxa/fakepta @ 2025-08-08, /root/reference), used as the CHECKER for the HIP
+product path. Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline
+leg may import it. The product package (fakepta_amd) never imports it and has
+no CPU fallback.
+
+Parity pinning: every reference-semantics function below is checked against the
+committed golden vectors in tests/golden/ (generated in the build container by
+tools/gen_golden.py, which imports the real reference) — see
+tests/test_oracle_golden.py. The batch semantics (Philox draws, ORF mixing
+order, white/ECORR streams) are new in this build and are specified here; the
+Philox core is pinned by the Random123 known-answer vectors.
+
+Two restatements of the synthesis are provided:
+  * loop-faithful  — same per-mode elementwise structure as fake_pta.py:385-387
+                     and correlated_noises.py:153-160 (used for the CPU baseline)
+  * vectorised     — basis F (n_toa x 2N) times coefficients (used for checking
+                     larger cases quickly)
+"""
+import numpy as np
+
+# fakepta/constants.py:23-25 (copy of enterprise.constants): yr = Julian year, fyr = 1/yr
+JULIAN_YEAR = 365.25 * 86400.0
+FYR = 1.0 / JULIAN_YEAR
+TWO_PI = 2.0 * np.pi
+
+
+# ----------------------------------------------------------------------------- PSDs
+# fakepta/spectrum.py:12-86 (ENTERPRISE gp_priors forms)
+
+def powerlaw(f, log10_A, gamma):
+    """fakepta/spectrum.py:12-15"""
+    return (10 ** log10_A) ** 2 / (12.0 * np.pi ** 2) * FYR ** (gamma - 3) * f ** (-gamma)
+
+
+def turnover(f, log10_A=-15, gamma=4.33, lf0=-8.5, kappa=10 / 3, beta=0.5):
+    """fakepta/spectrum.py:18-20"""
+    hcf = 10 ** log10_A * (f / FYR) ** ((3 - gamma) / 2) / (1 + (10 ** lf0 / f) ** kappa) ** beta
+    return hcf ** 2 / 12 / np.pi ** 2 / f ** 3
+
+
+def t_process(f, log10_A=-15, gamma=4.33, alphas=None):
+    """fakepta/spectrum.py:23-29"""
+    alphas = np.ones_like(f) if alphas is None else alphas
+    return powerlaw(f, log10_A=log10_A, gamma=gamma) * alphas
+
+
+def t_process_adapt(f, log10_A=-15, gamma=4.33, alphas_adapt=None, nfreq=None):
+    """fakepta/spectrum.py:32-46"""
+    if alphas_adapt is None:
+        alpha_model = np.ones_like(f)
+    elif nfreq is None:
+        alpha_model = alphas_adapt
+    else:
+        alpha_model = np.ones_like(f)
+        alpha_model[int(np.rint(nfreq))] = alphas_adapt
+    return powerlaw(f, log10_A=log10_A, gamma=gamma) * alpha_model
+
+
+def turnover_knee(f, log10_A, gamma, lfb, lfk, kappa, delta):
+    """fakepta/spectrum.py:49-66"""
+    hcf = (10 ** log10_A * (f / FYR) ** ((3 - gamma) / 2) * (1.0 + (f / 10 ** lfk)) ** delta
+           / np.sqrt(1 + (10 ** lfb / f) ** kappa))
+    return hcf ** 2 / 12 / np.pi ** 2 / f ** 3
+
+
+def broken_powerlaw(f, log10_A, gamma, delta, log10_fb, kappa=0.1):
+    """fakepta/spectrum.py:69-86"""
+    hcf = (10 ** log10_A * (f / FYR) ** ((3 - gamma) / 2)
+           * (1 + (f / 10 ** log10_fb) ** (1 / kappa)) ** (kappa * (gamma - delta) / 2))
+    return hcf ** 2 / 12 / np.pi ** 2 / f ** 3
+
+
+PSDS = dict(powerlaw=powerlaw, turnover=turnover, t_process=t_process,
+            t_process_adapt=t_process_adapt, turnover_knee=turnover_knee,
+            broken_powerlaw=broken_powerlaw)
+
+
+# ----------------------------------------------------------------------------- grids
+
+def freq_grid(n_modes, tspan):
+    """fakepta/fake_pta.py:264 (per pulsar) / correlated_noises.py:120 (global span)"""
+    return np.arange(1, n_modes + 1) / tspan
+
+
+def delta_f(f):
+    """fakepta/fake_pta.py:370: df = diff([0, f]), so df_0 = f_0"""
+    return np.diff(np.append(0.0, f))
+
+
+def chromatic(freqs, idx, freqf=1400.0):
+    """fakepta/fake_pta.py:386: (freqf / nu)**idx (code, not the tutorial's prose, is authoritative)"""
+    return (freqf / freqs) ** idx
+
+
+# ----------------------------------------------------------------------------- per-pulsar GP
+
+def gp_coeffs_from_z(psd, z):
+    """fakepta/fake_pta.py:372-374: coeffs = normal(0, sqrt(repeat(psd, 2))) == sqrt(psd_rep) * z"""
+    return 0.0 + np.sqrt(np.repeat(psd, 2)) * z
+
+
+def gp_fourier(coeffs, f):
+    """fakepta/fake_pta.py:381: fourier = (c_even, c_odd) / sqrt(df)"""
+    df = delta_f(f)
+    return np.vstack((coeffs[::2] / df ** 0.5, coeffs[1::2] / df ** 0.5))
+
+
+def gp_synth_loop(toas, freqs, f, coeffs, idx, freqf=1400.0, mask=None, residuals=None):
+    """Loop-faithful restatement of fakepta/fake_pta.py:385-387 (in-place accumulate).
+
+    mask: the reference applies `mask` to toas but not to the chromatic factor
+    (defect D9: it raises for a partial mask); here the chromatic factor is masked too.
+    """
+    r = np.zeros(len(toas)) if residuals is None else residuals
+    if mask is None:
+        mask = np.ones(len(toas), dtype=bool)
+    df = delta_f(f)
+    chrom = (freqf / freqs[mask]) ** idx
+    for i in range(len(f)):
+        r[mask] += chrom * df[i] ** 0.5 * coeffs[2 * i] * np.cos(2 * np.pi * f[i] * toas[mask])
+        r[mask] += chrom * df[i] ** 0.5 * coeffs[2 * i + 1] * np.sin(2 * np.pi * f[i] * toas[mask])
+    return r
+
+
+def fourier_basis(toas, freqs, f, idx, freqf=1400.0):
+    """F[t, 2k] = chrom cos(2 pi f_k t), F[t, 2k+1] = chrom sin(...) — fake_pta.py:415-418 layout"""
+    ph = np.outer(toas, TWO_PI * np.asarray(f))
+    F = np.empty((len(toas), 2 * len(f)))
+    ch = chromatic(freqs, idx, freqf)[:, None]
+    F[:, 0::2] = ch * np.cos(ph)
+    F[:, 1::2] = ch * np.sin(ph)
+    return F
+
+
+def gp_synth_vec(toas, freqs, f, amp_cos, amp_sin, idx, freqf=1400.0):
+    """Vectorised: sum_k chrom (amp_cos_k cos + amp_sin_k sin); amp = sqrt(df) * coeff (inject)
+    or df * fourier (reconstruct). Supports amp of shape [N] or [R, N] (returns [R, n_toa])."""
+    F = fourier_basis(toas, freqs, f, idx, freqf)
+    amp_cos = np.asarray(amp_cos)
+    A = np.empty(amp_cos.shape[:-1] + (2 * amp_cos.shape[-1],))
+    A[..., 0::2] = amp_cos
+    A[..., 1::2] = amp_sin
+    return A @ F.T
+
+
+def reconstruct_loop(toas, freqs, f, fourier, idx, freqf=1400.0):
+    """fakepta/fake_pta.py:538-545 (GP branch of reconstruct_signal)"""
+    sig = np.zeros(len(toas))
+    df = delta_f(f)
+    for c_k, f_k, df_k in zip(fourier.T, f, df):
+        sig += df_k * c_k[0] * (freqf / freqs) ** idx * np.cos(2 * np.pi * f_k * toas)
+        sig += df_k * c_k[1] * (freqf / freqs) ** idx * np.sin(2 * np.pi * f_k * toas)
+    return sig
+
+
+# ----------------------------------------------------------------------------- ORFs
+
+def orf_hd(pos):
+    """fakepta/correlated_noises.py:62-71 (vectorised; NaN for coincident pulsars, defect D8)"""
+    pos = np.asarray(pos)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        omc2 = (1 - pos @ pos.T) / 2
+        g = 1.5 * omc2 * np.log(omc2) - 0.25 * omc2 + 0.5
+    np.fill_diagonal(g, 1.0)
+    return g
+
+
+def orf_monopole(pos):
+    """fakepta/correlated_noises.py:91-93"""
+    n = len(pos)
+    return np.ones((n, n))
+
+
+def orf_dipole(pos):
+    """fakepta/correlated_noises.py:95-104"""
+    pos = np.asarray(pos)
+    g = pos @ pos.T
+    np.fill_diagonal(g, 1.0)
+    return g
+
+
+def orf_curn(pos):
+    """fakepta/correlated_noises.py:106-108"""
+    return np.eye(len(pos))
+
+
+ORFS = dict(hd=orf_hd, monopole=orf_monopole, dipole=orf_dipole, curn=orf_curn)
+
+
+def mvn_factor(cov):
+    """numpy legacy multivariate_normal (method='svd'), as called at correlated_noises.py:154-155:
+    x = z @ (sqrt(s)[:, None] * vt). Returned as L = M.T so that x = L @ z."""
+    _, s, vt = np.linalg.svd(cov)
+    return (np.sqrt(s)[:, None] * vt).T
+
+
+def common_synth_loop(toas_list, freqs_list, f, psd, z, L, idx, freqf=1400.0):
+    """Loop-faithful restatement of fakepta/correlated_noises.py:146-160.
+
+    z: [N, 2, P] standard normals in the reference's draw order (sin vector first, then cos).
+    Returns (residual list, fourier [P, 2, N])."""
+    P = len(toas_list)
+    df = delta_f(f)
+    coeffs = np.sqrt(np.repeat(psd, 2))
+    res = [np.zeros(len(t)) for t in toas_list]
+    fourier = np.zeros((P, 2, len(f)))
+    for i in range(len(f)):
+        orf_corr_sin = L @ z[i, 0]
+        orf_corr_cos = L @ z[i, 1]
+        for n in range(P):
+            fourier[n, 0, i] = orf_corr_cos[n] * coeffs[2 * i] / df[i] ** 0.5
+            fourier[n, 1, i] = orf_corr_sin[n] * coeffs[2 * i + 1] / df[i] ** 0.5
+            ch = (freqf / freqs_list[n]) ** idx
+            res[n] += orf_corr_cos[n] * ch * df[i] ** 0.5 * coeffs[2 * i] * np.cos(2 * np.pi * f[i] * toas_list[n])
+            res[n] += orf_corr_sin[n] * ch * df[i] ** 0.5 * coeffs[2 * i + 1] * np.sin(2 * np.pi * f[i] * toas_list[n])
+    return res, fourier
+
+
+# ----------------------------------------------------------------------------- white noise / ECORR
+
+def white_sigma(toaerrs, backend_flags, efac, log10_tnequad):
+    """fakepta/fake_pta.py:214-217: sigma^2 = efac_b^2 sigma_toa^2 + 10^(2 log10_tnequad_b).
+    efac / log10_tnequad: dicts backend -> value."""
+    s2 = np.zeros(len(toaerrs))
+    for b in np.unique(backend_flags):
+        m = backend_flags == b
+        s2[m] = efac[b] ** 2 * toaerrs[m] ** 2 + 10 ** (2 * log10_tnequad[b])
+    return s2 ** 0.5
+
+
+def quantise_ecorr(toas, backend_flags, backends, dt=1):
+    """fakepta/fake_pta.py:232-253 verbatim semantics, including defect D2 (the final block
+    of every backend is never appended)."""
+    times = toas - toas[0]
+    out = []
+    dt *= 24 * 3600
+    for backend in backends:
+        b_idx = np.arange(len(times))[backend_flags == backend]
+        t0 = times[b_idx[0]]
+        q_i = [b_idx[0]]
+        for n in b_idx[1:]:
+            if times[n] - t0 < dt:
+                q_i.append(n)
+            else:
+                t0 = times[n]
+                out.append(np.array(q_i))
+                q_i = [n]
+    return out
+
+
+def ecorr_blocks(toas, backend_flags, backends, dt=1):
+    """The build's ECORR epochs: quantise_ecorr's greedy 1-day blocks per backend, WITH the
+    final block appended (fixes D2)."""
+    times = toas - toas[0]
+    out = []
+    dt *= 24 * 3600
+    for backend in backends:
+        b_idx = np.arange(len(times))[backend_flags == backend]
+        if len(b_idx) == 0:
+            continue
+        t0 = times[b_idx[0]]
+        q_i = [b_idx[0]]
+        for n in b_idx[1:]:
+            if times[n] - t0 < dt:
+                q_i.append(n)
+            else:
+                t0 = times[n]
+                out.append(np.array(q_i))
+                q_i = [n]
+        out.append(np.array(q_i))
+    return out
+
+
+# ----------------------------------------------------------------------------- Philox4x32-10
+
+PHILOX_M0, PHILOX_M1 = np.uint64(0xD2511F53), np.uint64(0xCD9E8D57)
+PHILOX_W0, PHILOX_W1 = np.uint32(0x9E3779B9), np.uint32(0xBB67AE85)
+MASK32 = np.uint64(0xFFFFFFFF)
+
+
+def philox4x32_10(ctr, key):
+    """Random123 Philox4x32-10. ctr: uint32 [..., 4]; key: uint32 [..., 2] (broadcast)."""
+    c = [np.asarray(ctr[..., i], dtype=np.uint64) for i in range(4)]
+    k0 = np.asarray(key[..., 0], dtype=np.uint64)
+    k1 = np.asarray(key[..., 1], dtype=np.uint64)
+    for _ in range(10):
+        p0 = PHILOX_M0 * c[0]
+        p1 = PHILOX_M1 * c[2]
+        c = [((p1 >> np.uint64(32)) ^ c[1] ^ k0) & MASK32, p1 & MASK32,
+             ((p0 >> np.uint64(32)) ^ c[3] ^ k1) & MASK32, p0 & MASK32]
+        k0 = (k0 + np.uint64(PHILOX_W0)) & MASK32
+        k1 = (k1 + np.uint64(PHILOX_W1)) & MASK32
+    return np.stack([x.astype(np.uint32) for x in c], axis=-1)
+
+
+def box_muller(x):
+    """uint32 [..., 4] -> two standard normals [..., 2] (the build's fixed mapping):
+    u1 = ((x0|x1<<32) >> 11) + 1) * 2^-53 in (0, 1], u2 = ((x2|x3<<32) >> 11) * 2^-53 in [0, 1),
+    z0 = sqrt(-2 ln u1) cos(2 pi u2), z1 = sqrt(-2 ln u1) sin(2 pi u2)."""
+    x = x.astype(np.uint64)
+    a = x[..., 0] | (x[..., 1] << np.uint64(32))
+    b = x[..., 2] | (x[..., 3] << np.uint64(32))
+    u1 = ((a >> np.uint64(11)) + np.uint64(1)).astype(np.float64) * 2.0 ** -53
+    u2 = (b >> np.uint64(11)).astype(np.float64) * 2.0 ** -53
+    r = np.sqrt(-2.0 * np.log(u1))
+    th = TWO_PI * u2
+    return np.stack([r * np.cos(th), r * np.sin(th)], axis=-1)
+
+
+# stream identifiers (counter word 1 / 2) for the non-GP draws
+WHITE_PSR_WORD = 0xFFFFFFFF
+WHITE_STREAM = 0xFFFFFFF0
+ECORR_STREAM = 0xFFFFFFF1
+
+
+def seed_key(seed):
+    seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+    return np.array([seed & 0xFFFFFFFF, seed >> 32], dtype=np.uint32)
+
+
+def gp_normals(seed, reals, p, seg, n_modes):
+    """(z_cos, z_sin) for modes 0..N-1 of pulsar p, segment seg, global realizations `reals`:
+    ctr = (mode, pulsar, segment, realization). Returns [R, N, 2]."""
+    reals = np.asarray(reals, dtype=np.uint32)
+    k = np.arange(n_modes, dtype=np.uint32)
+    ctr = np.zeros((len(reals), n_modes, 4), dtype=np.uint32)
+    ctr[..., 0] = k[None, :]
+    ctr[..., 1] = p
+    ctr[..., 2] = seg
+    ctr[..., 3] = reals[:, None]
+    return box_muller(philox4x32_10(ctr, seed_key(seed)))
+
+
+def white_normals(seed, reals, n_toa, stream=WHITE_STREAM):
+    """one normal per (realization, TOA): ctr = (t >> 1, 0xFFFFFFFF, stream, r), pick [t & 1]."""
+    reals = np.asarray(reals, dtype=np.uint32)
+    t = np.arange(n_toa, dtype=np.uint64)
+    ctr = np.zeros((len(reals), n_toa, 4), dtype=np.uint32)
+    ctr[..., 0] = (t >> np.uint64(1)).astype(np.uint32)[None, :]
+    ctr[..., 1] = WHITE_PSR_WORD
+    ctr[..., 2] = stream
+    ctr[..., 3] = reals[:, None]
+    z = box_muller(philox4x32_10(ctr, seed_key(seed)))
+    return np.take_along_axis(z, (t & np.uint64(1)).astype(np.int64)[None, :, None], axis=-1)[..., 0]
+
+
+# ----------------------------------------------------------------------------- batch semantics
+
+class Segment:
+    """One GP signal of the batch layout.
+    kind 0 (per pulsar): w [P, N], amp [P, N];  kind 1 (common): w [N], amp [N], L [P, P].
+    w = 2*pi*f (rad/s); amp = sqrt(S * df) (the standard deviation of each coefficient)."""
+
+    def __init__(self, kind, w, amp, idx=0.0, freqf=1400.0, L=None, mask=None):
+        self.kind, self.w, self.amp = kind, np.asarray(w, float), np.asarray(amp, float)
+        self.idx, self.freqf, self.L, self.mask = float(idx), float(freqf), L, mask
+
+    @property
+    def n_modes(self):
+        return self.w.shape[-1]
+
+
+def batch_coefficients(segments, n_psr, seed, real0, n_real, z_override=None):
+    """Coefficients a[s][R, P, N, 2] (cos, sin) of every segment for realizations
+    real0..real0+n_real-1. z_override: optional dict s -> z [R, P, N, 2] (validation mode)."""
+    reals = np.arange(real0, real0 + n_real)
+    out = []
+    for s, seg in enumerate(segments):
+        if z_override is not None and s in z_override:
+            z = z_override[s]
+        else:
+            z = np.stack([gp_normals(seed, reals, p, s, seg.n_modes) for p in range(n_psr)], axis=1)
+        if seg.kind == 0:
+            a = seg.amp[None, :, :, None] * z
+        else:
+            x = np.einsum("pq,rqnc->rpnc", seg.L, z)
+            a = seg.amp[None, None, :, None] * x
+        out.append(a)
+    return out
+
+
+def batch_synth(offs, toas, freqs, segments, seed, real0, n_real, sigma=None, block_of=None,
+                ecorr_sigma=None, z_override=None):
+    """Full batch semantics: out [n_real, n_toa_total]."""
+    P = len(offs) - 1
+    coeffs = batch_coefficients(segments, P, seed, real0, n_real, z_override)
+    out = np.zeros((n_real, offs[-1]))
+    for s, seg in enumerate(segments):
+        a = coeffs[s]
+        for p in range(P):
+            sl = slice(offs[p], offs[p + 1])
+            w = seg.w[p] if seg.kind == 0 else seg.w
+            ph = np.outer(toas[sl], w)
+            ch = (seg.freqf / freqs[sl]) ** seg.idx
+            if seg.mask is not None:
+                ch = ch * seg.mask[sl]
+            out[:, sl] += ch[None, :] * (a[:, p, :, 0] @ np.cos(ph).T + a[:, p, :, 1] @ np.sin(ph).T)
+    reals = np.arange(real0, real0 + n_real)
+    if sigma is not None:
+        out += sigma[None, :] * white_normals(seed, reals, offs[-1], WHITE_STREAM)
+    if block_of is not None and ecorr_sigma is not None and len(ecorr_sigma):
+        zb = white_normals(seed, reals, len(ecorr_sigma), ECORR_STREAM)
+        has = block_of >= 0
+        out[:, has] += ecorr_sigma[block_of[has]][None, :] * zb[:, block_of[has]]
+    return out

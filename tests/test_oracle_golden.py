@@ -1,0 +1,154 @@
+"""Pin the CPU oracle (oracle/fakepta_oracle.py) against the reference's own outputs
+(tests/golden/, generated from /root/reference by tools/gen_golden.py). CPU only."""
+import json
+
+import numpy as np
+import pytest
+
+from oracle import fakepta_oracle as O
+from tests.conftest import assert_parity
+
+
+def test_psd_all_six(golden):
+    g = golden("g1_psd.npz")
+    meta = json.loads(str(g["meta_json"]))
+    n = 0
+    for key, params in meta.items():
+        name, gi, _ = key.split("__")
+        f = g["grid" + gi[1:]]
+        p = {k: (np.array(v) if isinstance(v, list) else v) for k, v in params.items()}
+        out = O.PSDS[name](f.copy(), **p)
+        np.testing.assert_allclose(out, g[key], rtol=1e-13, atol=0)
+        n += 1
+    assert n == 6 * 9
+
+
+def test_tutorial_psd_known_answer(golden):
+    ka = golden("g5_tutorial.json")
+    T = 1.0 / ka["rn_f_first"]
+    f = O.freq_grid(30, T)
+    psd = O.powerlaw(f, -14.0, 3)
+    np.testing.assert_allclose(psd, ka["rn_psd_log10A_m14_gamma3_30modes_Tobs10"], rtol=1e-8)
+
+
+@pytest.mark.parametrize("lab", ["rn", "dm", "sv"])
+def test_single_pulsar_gp(golden, lab):
+    g = golden("g2_single_psr.npz")
+    toas, freqs = g["toas"], g["freqs"]
+    f, psd, z, idx = g[f"{lab}_f"], g[f"{lab}_psd"], g[f"{lab}_z"], g[f"{lab}_idx"]
+    np.testing.assert_allclose(f, O.freq_grid(len(f), float(g["Tspan"])), rtol=0, atol=0)
+    coeffs = O.gp_coeffs_from_z(psd, z)
+    np.testing.assert_allclose(O.gp_fourier(coeffs, f), g[f"{lab}_fourier"], rtol=1e-15)
+    # loop-faithful restatement reproduces the injected residual increment
+    delta = O.gp_synth_loop(toas, freqs, f, coeffs, idx)
+    assert_parity(delta, g[f"{lab}_delta"], 1e-13)
+    # vectorised form
+    df = O.delta_f(f)
+    vec = O.gp_synth_vec(toas, freqs, f, df ** 0.5 * coeffs[0::2], df ** 0.5 * coeffs[1::2], idx)
+    assert_parity(vec, g[f"{lab}_delta"], 1e-12)
+    # reconstruct_signal
+    rec = O.reconstruct_loop(toas, freqs, f, g[f"{lab}_fourier"], idx)
+    assert_parity(rec, g[f"{lab}_reconstruct"], 1e-13)
+
+
+def test_reinject_replaces(golden):
+    g = golden("g2_single_psr.npz")
+    toas, freqs = g["toas"], g["freqs"]
+    old = O.reconstruct_loop(toas, freqs, g["rn_f"], g["rn_fourier"], 0.0)
+    coeffs = O.gp_coeffs_from_z(g["rn2_psd"], g["rn2_z"])
+    new = O.gp_synth_loop(toas, freqs, g["rn_f"], coeffs, 0.0)
+    assert_parity(g["rn2_before"] - old + new, g["rn2_residuals"], 1e-12)
+
+
+def test_white_noise(golden):
+    g = golden("g2_single_psr.npz")
+    flags = g["backend_flags"]
+    efac = dict(zip(["A.1400", "B.800"], g["wn_efac"]))
+    eq = dict(zip(["A.1400", "B.800"], g["wn_tnequad"]))
+    sig = O.white_sigma(g["toaerrs"], flags, efac, eq)
+    # wn_delta = after - before carries the cancellation error of the GP residual it sits on
+    assert_parity(sig * g["wn_z"], g["wn_delta"], 1e-11)
+
+
+def test_quantise_ecorr_preserves_d2(golden):
+    g = golden("g2_single_psr.npz")
+    flags = g["q_flags"]
+    q = O.quantise_ecorr(g["q_toas"], flags, np.unique(flags))
+    assert [len(b) for b in q] == list(g["q_lens"])
+    np.testing.assert_array_equal(np.concatenate(q), g["q_idx"])
+    fixed = O.ecorr_blocks(g["q_toas"], flags, np.unique(flags))
+    assert len(fixed) == len(q) + len(np.unique(flags))
+    assert sorted(np.concatenate(fixed).tolist()) == list(range(len(g["q_toas"])))
+
+
+@pytest.mark.parametrize("orf", ["hd", "monopole", "dipole", "curn"])
+def test_common_correlated(golden, orf):
+    g = golden("g3_common.npz")
+    offs, toas, freqs, pos = g["offs"], g["toas"], g["freqs"], g["pos"]
+    gam = O.ORFS[orf](pos)
+    np.testing.assert_allclose(gam, g[f"{orf}_orf"], rtol=1e-14, atol=1e-15)
+    L = O.mvn_factor(gam)
+    np.testing.assert_allclose(L.T, g[f"{orf}_svdM"], rtol=0, atol=1e-13)
+    P = len(offs) - 1
+    tl = [toas[offs[i]:offs[i + 1]] for i in range(P)]
+    fl = [freqs[offs[i]:offs[i + 1]] for i in range(P)]
+    res, fourier = O.common_synth_loop(tl, fl, g[f"{orf}_f"], g[f"{orf}_psd"], g[f"{orf}_z"],
+                                       g[f"{orf}_svdM"].T, g[f"{orf}_idx"])
+    np.testing.assert_allclose(fourier, g[f"{orf}_fourier"], rtol=1e-12, atol=1e-12 * np.abs(fourier).max())
+    assert_parity(np.concatenate(res), g[f"{orf}_residuals"], 1e-12)
+    # reconstruct from the stored coefficients
+    rec = np.concatenate([O.reconstruct_loop(tl[i], fl[i], g[f"{orf}_f"], g[f"{orf}_fourier"][i], g[f"{orf}_idx"])
+                          for i in range(P)])
+    assert_parity(rec, g[f"{orf}_reconstruct"], 1e-12)
+
+
+def test_philox_known_answers():
+    kat = [((0, 0, 0, 0), (0, 0), (0x6627e8d5, 0xe169c58d, 0xbc57ac4c, 0x9b00dbd8)),
+           ((0xffffffff,) * 4, (0xffffffff,) * 2, (0x408f276d, 0x41c83b0e, 0xa20bc7c6, 0x6d5451fd)),
+           ((0x243f6a88, 0x85a308d3, 0x13198a2e, 0x03707344), (0xa4093822, 0x299f31d0),
+            (0xd16cfe09, 0x94fdcceb, 0x5001e420, 0x24126ea1))]
+    for c, k, exp in kat:
+        out = O.philox4x32_10(np.array([c], np.uint32), np.array(k, np.uint32))
+        assert tuple(int(x) for x in out[0]) == exp
+
+
+def test_box_muller_moments():
+    z = O.gp_normals(1234, np.arange(4000), 3, 1, 50).ravel()
+    assert abs(z.mean()) < 0.01 and abs(z.std() - 1) < 0.01
+    w = O.white_normals(99, np.arange(10), 20001)
+    assert abs(w.mean()) < 0.01 and abs(w.std() - 1) < 0.01
+
+
+def test_batch_semantics_match_reference_loop():
+    """The batch layout (per-pulsar + common segment, explicit z) reproduces the loop-faithful
+    reference restatements on the same draws."""
+    rng = np.random.default_rng(0)
+    P, N = 4, 6
+    offs = np.array([0, 30, 55, 90, 120])
+    toas = np.concatenate([np.sort(rng.uniform(0, 3e8, offs[i + 1] - offs[i])) for i in range(P)])
+    freqs = rng.normal(1400, 10, offs[-1])
+    T = [np.ptp(toas[offs[i]:offs[i + 1]]) for i in range(P)]
+    f_p = np.array([O.freq_grid(N, t) for t in T])
+    psd_p = np.array([O.powerlaw(f, -13.5, 3.0) for f in f_p])
+    amp_p = np.sqrt(psd_p * np.array([O.delta_f(f) for f in f_p]))
+    fc = O.freq_grid(N, toas.max() - toas.min())
+    psdc = O.powerlaw(fc, -14.0, 13 / 3)
+    v = rng.normal(size=(P, 3))
+    L = O.mvn_factor(O.orf_hd(v / np.linalg.norm(v, axis=1)[:, None]))
+    segs = [O.Segment(0, 2 * np.pi * f_p, amp_p, idx=2.0),
+            O.Segment(1, 2 * np.pi * fc, np.sqrt(psdc * O.delta_f(fc)), idx=0.0, L=L)]
+    z0 = rng.standard_normal((1, P, N, 2))
+    z1 = rng.standard_normal((1, P, N, 2))
+    out = O.batch_synth(offs, toas, freqs, segs, 0, 0, 1, z_override={0: z0, 1: z1})[0]
+    ref = np.zeros(offs[-1])
+    for p in range(P):
+        sl = slice(offs[p], offs[p + 1])
+        c = np.empty(2 * N)
+        c[0::2] = np.sqrt(psd_p[p]) * z0[0, p, :, 0]
+        c[1::2] = np.sqrt(psd_p[p]) * z0[0, p, :, 1]
+        ref[sl] += O.gp_synth_loop(toas[sl], freqs[sl], f_p[p], c, 2.0)
+    zc = np.stack([z1[0, :, :, 1].T, z1[0, :, :, 0].T], axis=1)  # [N, 2(sin, cos), P]
+    res, _ = O.common_synth_loop([toas[offs[i]:offs[i + 1]] for i in range(P)],
+                                 [freqs[offs[i]:offs[i + 1]] for i in range(P)], fc, psdc, zc, L, 0.0)
+    ref += np.concatenate(res)
+    assert_parity(out, ref, 1e-12)
