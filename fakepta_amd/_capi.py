@@ -1,0 +1,263 @@
+"""ctypes binding of libfakepta_amd.so (C-ABI declared in include/fakepta_amd.h).
+
+The product path has no CPU fallback: if the library is missing this module raises at
+import, and if no MI355X is visible the first compute call raises FptaError.
+"""
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("FAKEPTA_AMD_LIB", os.path.join(_HERE, "lib", "libfakepta_amd.so"))
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(
+        f"fakepta_amd: HIP library not found at {LIB_PATH}. Build it with "
+        "`python -c 'import __graft_entry__ as g; g.build()'` (or `make -C fakepta_amd/csrc`).")
+
+_lib = ctypes.CDLL(LIB_PATH)
+
+_c_int = ctypes.c_int
+_i32, _i64, _u64 = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64
+_dbl = ctypes.c_double
+_vp = ctypes.c_void_p
+_ctx_p = ctypes.c_void_p
+
+# (name, restype, argtypes) — mirrors include/fakepta_amd.h
+_SIGS = [
+    ("fpta_version", _c_int, []),
+    ("fpta_create", _c_int, [_c_int, ctypes.POINTER(_ctx_p)]),
+    ("fpta_destroy", _c_int, [_ctx_p]),
+    ("fpta_last_error", ctypes.c_char_p, [_ctx_p]),
+    ("fpta_device_count", _c_int, [ctypes.POINTER(_c_int)]),
+    ("fpta_gp_accumulate", _c_int, [_ctx_p, _i64, _vp, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _dbl, _vp]),
+    ("fpta_common_accumulate", _c_int, [_ctx_p, _i32, _vp, _vp, _vp, _i32, _vp, _vp, _dbl, _dbl, _vp, _vp, _vp,
+                                        _vp]),
+    ("fpta_white_accumulate", _c_int, [_ctx_p, _i64, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp]),
+    ("fpta_batch_set_toas", _c_int, [_ctx_p, _i32, _vp, _vp, _vp]),
+    ("fpta_batch_add_signal", _c_int, [_ctx_p, _i32, _i32, _vp, _vp, _dbl, _dbl, _vp, _vp]),
+    ("fpta_batch_set_white", _c_int, [_ctx_p, _vp, _i64, _vp, _vp, _vp]),
+    ("fpta_batch_clear_signals", _c_int, [_ctx_p]),
+    ("fpta_batch_synth", _c_int, [_ctx_p, _u64, _i64, _i32, _vp, _vp]),
+    ("fpta_batch_synth_from_z", _c_int, [_ctx_p, _i32, _i32, _vp, _vp]),
+    ("fpta_batch_device_out", _c_int, [_ctx_p, ctypes.POINTER(_vp), ctypes.POINTER(_i64), ctypes.POINTER(_i32)]),
+    ("fpta_batch_checksums", _c_int, [_ctx_p, _vp]),
+    ("fpta_batch_info", _c_int, [_ctx_p, _vp]),
+    ("fpta_set_option", _c_int, [_ctx_p, _i32, _i64]),
+    ("fpta_kernel_stats", _c_int, [_ctx_p, _i32, ctypes.POINTER(_i64), ctypes.POINTER(_dbl)]),
+    ("fpta_reset_stats", _c_int, [_ctx_p]),
+    ("fpta_synchronize", _c_int, [_ctx_p]),
+    ("fpta_debug_philox", _c_int, [_ctx_p, _i64, _vp, _vp, _vp]),
+]
+for _name, _res, _args in _SIGS:
+    _fn = getattr(_lib, _name)
+    _fn.restype = _res
+    _fn.argtypes = _args
+
+EXPORTED = [s[0] for s in _SIGS]
+
+OPT_SYNTH_PATH, OPT_MFMA_MIN_REAL, OPT_PROFILE, OPT_ANCHOR = 1, 2, 3, 4
+K_GEN, K_MIX, K_SYNTH, K_WHITE = 0, 1, 2, 3
+
+
+class FptaError(RuntimeError):
+    pass
+
+
+def _f64(a):
+    return np.ascontiguousarray(a, dtype=np.float64)
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data_as(_vp)
+
+
+class Context:
+    """One device context (one GPU, one HIP stream). Not thread-safe: one per thread/process."""
+
+    def __init__(self, device=0):
+        h = _ctx_p()
+        rc = _lib.fpta_create(int(device), ctypes.byref(h))
+        if rc != 0:
+            raise FptaError(f"fpta_create(device={device}) failed ({rc}): "
+                            f"{_lib.fpta_last_error(None).decode()}")
+        self._h = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _lib.fpta_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc, what):
+        if rc < 0:
+            raise FptaError(f"{what} failed ({rc}): {_lib.fpta_last_error(self._h).decode()}")
+        return rc
+
+    # --------------------------------------------------------------- drop-in
+    def gp_accumulate(self, toas, nu, segments, residuals, sign=1.0, masks=None):
+        """segments: list of (f, ccos, csin, idx, freqf). residuals: float64 array updated in place."""
+        toas, nu = _f64(toas), _f64(nu)
+        n = len(toas)
+        assert residuals.dtype == np.float64 and residuals.flags.c_contiguous and len(residuals) == n
+        nm = np.array([len(s[0]) for s in segments], dtype=np.int32)
+        f = _f64(np.concatenate([np.asarray(s[0], float) for s in segments]))
+        cc = _f64(np.concatenate([np.asarray(s[1], float) for s in segments]))
+        cs = _f64(np.concatenate([np.asarray(s[2], float) for s in segments]))
+        idx = _f64([s[3] for s in segments])
+        ff = _f64([s[4] for s in segments])
+        m = None
+        if masks is not None and any(x is not None for x in masks):
+            m = np.ones((len(segments), n), dtype=np.uint8)
+            for i, x in enumerate(masks):
+                if x is not None:
+                    m[i] = np.asarray(x, dtype=bool)
+        self._check(_lib.fpta_gp_accumulate(self._h, n, _ptr(toas), _ptr(nu), len(segments), _ptr(nm), _ptr(f),
+                                            _ptr(cc), _ptr(cs), _ptr(idx), _ptr(ff), _ptr(m), float(sign),
+                                            _ptr(residuals)), "fpta_gp_accumulate")
+
+    def common_accumulate(self, offs, toas, nu, f, amp, idx, freqf, L, z, residuals, want_x=True):
+        offs = np.ascontiguousarray(offs, dtype=np.int64)
+        toas, nu, f, amp, L, z = map(_f64, (toas, nu, f, amp, L, z))
+        P = len(offs) - 1
+        N = len(f)
+        assert z.shape == (N, 2, P) and L.shape == (P, P) and len(residuals) == offs[-1]
+        x = np.empty((N, 2, P)) if want_x else None
+        self._check(_lib.fpta_common_accumulate(self._h, P, _ptr(offs), _ptr(toas), _ptr(nu), N, _ptr(f), _ptr(amp),
+                                                float(idx), float(freqf), _ptr(L), _ptr(z), _ptr(residuals),
+                                                _ptr(x)), "fpta_common_accumulate")
+        return x
+
+    def white_accumulate(self, sigma, z, residuals, blocks=None, ecorr_sigma=None, zb=None):
+        sigma, z = _f64(sigma), _f64(z)
+        n = len(sigma)
+        nb = 0
+        bo = bi = es = zbb = None
+        if blocks:
+            nb = len(blocks)
+            bo = np.concatenate([[0], np.cumsum([len(b) for b in blocks])]).astype(np.int64)
+            bi = np.concatenate([np.asarray(b, dtype=np.int64) for b in blocks]).astype(np.int64)
+            es, zbb = _f64(ecorr_sigma), _f64(zb)
+        self._check(_lib.fpta_white_accumulate(self._h, n, _ptr(sigma), _ptr(z), nb, _ptr(bo), _ptr(bi), _ptr(es),
+                                               _ptr(zbb), _ptr(residuals)), "fpta_white_accumulate")
+
+    # --------------------------------------------------------------- batch
+    def batch_set_toas(self, offs, toas, nu):
+        offs = np.ascontiguousarray(offs, dtype=np.int64)
+        toas, nu = _f64(toas), _f64(nu)
+        self._check(_lib.fpta_batch_set_toas(self._h, len(offs) - 1, _ptr(offs), _ptr(toas), _ptr(nu)),
+                    "fpta_batch_set_toas")
+
+    def batch_add_signal(self, kind, f, amp, idx=0.0, freqf=1400.0, L=None, mask=None):
+        f, amp = _f64(f), _f64(amp)
+        nm = f.shape[-1]
+        L = None if L is None else _f64(L)
+        m = None if mask is None else np.ascontiguousarray(mask, dtype=np.uint8)
+        return self._check(_lib.fpta_batch_add_signal(self._h, int(kind), nm, _ptr(f), _ptr(amp), float(idx),
+                                                      float(freqf), _ptr(L), _ptr(m)), "fpta_batch_add_signal")
+
+    def batch_set_white(self, sigma=None, blocks=None, ecorr_sigma=None):
+        s = None if sigma is None else _f64(sigma)
+        nb = 0
+        bo = bi = es = None
+        if blocks:
+            nb = len(blocks)
+            bo = np.concatenate([[0], np.cumsum([len(b) for b in blocks])]).astype(np.int64)
+            bi = np.concatenate([np.asarray(b, dtype=np.int64) for b in blocks]).astype(np.int64)
+            es = _f64(ecorr_sigma)
+        self._check(_lib.fpta_batch_set_white(self._h, _ptr(s), nb, _ptr(bo), _ptr(bi), _ptr(es)),
+                    "fpta_batch_set_white")
+
+    def batch_clear(self):
+        self._check(_lib.fpta_batch_clear_signals(self._h), "fpta_batch_clear_signals")
+
+    def batch_info(self):
+        info = np.zeros(5, dtype=np.int64)
+        self._check(_lib.fpta_batch_info(self._h, _ptr(info)), "fpta_batch_info")
+        return dict(n_psr=int(info[0]), n_toa=int(info[1]), n_seg=int(info[2]), K=int(info[3]), max_np=int(info[4]))
+
+    def batch_synth(self, seed, real0, n_real, to_host=True, coeffs=False):
+        info = self.batch_info()
+        out = np.empty((n_real, info["n_toa"])) if to_host else None
+        co = np.empty((info["n_psr"], info["K"], n_real)) if coeffs else None
+        self._check(_lib.fpta_batch_synth(self._h, int(seed) & 0xFFFFFFFFFFFFFFFF, int(real0), int(n_real), _ptr(out),
+                                          _ptr(co)), "fpta_batch_synth")
+        return (out, co) if coeffs else out
+
+    def batch_synth_from_z(self, z):
+        z = _f64(z)
+        info = self.batch_info()
+        n_real = z.shape[0]
+        assert z.ndim == 5 and z.shape[1:3] == (info["n_seg"], info["n_psr"]) and z.shape[4] == 2
+        out = np.empty((n_real, info["n_toa"]))
+        self._check(_lib.fpta_batch_synth_from_z(self._h, n_real, z.shape[3], _ptr(z), _ptr(out)),
+                    "fpta_batch_synth_from_z")
+        return out
+
+    def batch_device_out(self):
+        p, ld, nr = _vp(), _i64(), _i32()
+        self._check(_lib.fpta_batch_device_out(self._h, ctypes.byref(p), ctypes.byref(ld), ctypes.byref(nr)),
+                    "fpta_batch_device_out")
+        return p.value, ld.value, nr.value
+
+    def batch_checksums(self):
+        _, _, nr = self.batch_device_out()
+        s = np.empty((nr, 2))
+        self._check(_lib.fpta_batch_checksums(self._h, _ptr(s)), "fpta_batch_checksums")
+        return s
+
+    # --------------------------------------------------------------- tuning / profiling
+    def set_option(self, key, value):
+        self._check(_lib.fpta_set_option(self._h, int(key), int(value)), "fpta_set_option")
+
+    def kernel_stats(self, which):
+        n, ms = _i64(), _dbl()
+        self._check(_lib.fpta_kernel_stats(self._h, int(which), ctypes.byref(n), ctypes.byref(ms)),
+                    "fpta_kernel_stats")
+        return n.value, ms.value
+
+    def reset_stats(self):
+        self._check(_lib.fpta_reset_stats(self._h), "fpta_reset_stats")
+
+    def synchronize(self):
+        self._check(_lib.fpta_synchronize(self._h), "fpta_synchronize")
+
+    def debug_philox(self, ctr, key):
+        ctr = np.ascontiguousarray(ctr, dtype=np.uint32).reshape(-1, 4)
+        key = np.ascontiguousarray(key, dtype=np.uint32)
+        out = np.empty_like(ctr)
+        self._check(_lib.fpta_debug_philox(self._h, len(ctr), _ptr(ctr), _ptr(key), _ptr(out)), "fpta_debug_philox")
+        return out
+
+
+_default = {}
+_lock = threading.Lock()
+
+
+def default_device():
+    return int(os.environ.get("FAKEPTA_AMD_DEVICE", os.environ.get("LOCAL_RANK", "0")))
+
+
+def get_context(device=None):
+    """Process-wide context for the drop-in Pulsar methods (created on first use)."""
+    dev = default_device() if device is None else int(device)
+    with _lock:
+        ctx = _default.get(dev)
+        if ctx is None:
+            ctx = Context(dev)
+            _default[dev] = ctx
+        return ctx
+
+
+def device_count():
+    n = _c_int()
+    rc = _lib.fpta_device_count(ctypes.byref(n))
+    return n.value if rc == 0 else 0

@@ -1,0 +1,786 @@
+// C-ABI of libfakepta_amd.so (declared in include/fakepta_amd.h).
+// Host-side orchestration only: argument checking, device buffers, layout tables,
+// kernel dispatch on the context's stream, HIP-event timing. All arithmetic on the
+// path runs in kernels.hip.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/fakepta_amd.h"
+#include "fpta_internal.h"
+
+using namespace fpta;
+
+namespace {
+
+thread_local std::string g_err;
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  ~DevBuf() { release(); }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+  hipError_t ensure(size_t bytes) {
+    if (bytes <= cap && p) return hipSuccess;
+    release();
+    size_t want = std::max<size_t>(bytes, 256);
+    hipError_t e = hipMalloc(&p, want);
+    if (e != hipSuccess) {
+      p = nullptr;
+      return e;
+    }
+    cap = want;
+    return hipSuccess;
+  }
+  template <class T>
+  T* as() const {
+    return static_cast<T*>(p);
+  }
+};
+
+struct Seg {
+  SegDesc d{};
+  int32_t nm_orig = 0;
+  DevBuf w, amp, L, mask;
+};
+
+// A device-resident pulsar array plus its GP signals.
+struct Layout {
+  int32_t P = 0;
+  int64_t n_toa = 0;
+  int64_t max_np = 0;
+  std::vector<int64_t> h_offs;
+  DevBuf offs, toas, nu, psr_of;
+  std::vector<Seg*> segs;
+  DevBuf segdesc;
+  int32_t K = 0;
+  bool dirty = true;
+  // MFMA tile table cache
+  DevBuf tiles;
+  int32_t n_tiles = 0;
+  int32_t tiles_R = -1;
+  ~Layout() { clear_signals(); }
+  void clear_signals() {
+    for (Seg* s : segs) delete s;
+    segs.clear();
+    K = 0;
+    dirty = true;
+    tiles_R = -1;
+  }
+};
+
+}  // namespace
+
+struct fpta_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+  Layout batch, scratch;
+  // batch white noise
+  DevBuf sigma, block_of, esig;
+  bool has_sigma = false, has_blocks = false;
+  // work buffers
+  DevBuf coef, zbuf, out, sums, zin, xout, hostz, scratch_out, scratch_z, scratch_zb, scratch_sigma,
+      scratch_block_of, scratch_esig, dbg_a, dbg_b;
+  int32_t out_R = 0;
+  int64_t out_ld = 0;
+  // options
+  int synth_path = 0;
+  int mfma_min_real = 16;
+  int profile = 0;
+  int anchor = 8;
+  // profiling
+  struct Pending {
+    int which;
+    hipEvent_t a, b;
+  };
+  std::vector<Pending> pending;
+  std::vector<hipEvent_t> pool;
+  int64_t kcount[FPTA_K_N] = {0, 0, 0, 0};
+  double kms[FPTA_K_N] = {0, 0, 0, 0};
+};
+
+namespace {
+
+int fail(fpta_ctx* c, int code, const std::string& msg) {
+  if (c) c->err = msg;
+  g_err = msg;
+  return code;
+}
+
+int hip_fail(fpta_ctx* c, hipError_t e, const char* what) {
+  std::string m = std::string(what) + ": " + hipGetErrorString(e);
+  return fail(c, e == hipErrorOutOfMemory ? FPTA_ENOMEM : FPTA_EDEVICE, m);
+}
+
+#define HIPCHK(ctx, expr, what)                  \
+  do {                                           \
+    hipError_t _e = (expr);                      \
+    if (_e != hipSuccess) return hip_fail(ctx, _e, what); \
+  } while (0)
+
+hipEvent_t get_event(fpta_ctx* c) {
+  if (!c->pool.empty()) {
+    hipEvent_t e = c->pool.back();
+    c->pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  return e;
+}
+
+// Bracket a launch with HIP events on the ctx stream when profiling is on.
+struct KTimer {
+  fpta_ctx* c;
+  int which;
+  hipEvent_t a = nullptr, b = nullptr;
+  KTimer(fpta_ctx* c_, int w) : c(c_), which(w) {
+    if (c->profile) {
+      a = get_event(c);
+      b = get_event(c);
+      if (a) (void)hipEventRecord(a, c->stream);
+    }
+  }
+  ~KTimer() {
+    if (c->profile && a && b) {
+      (void)hipEventRecord(b, c->stream);
+      c->pending.push_back({which, a, b});
+    }
+  }
+};
+
+int upload(fpta_ctx* c, DevBuf& buf, const void* src, size_t bytes, const char* what) {
+  HIPCHK(c, buf.ensure(bytes), what);
+  if (bytes) HIPCHK(c, hipMemcpyAsync(buf.p, src, bytes, hipMemcpyHostToDevice, c->stream), what);
+  return FPTA_OK;
+}
+
+int layout_set_toas(fpta_ctx* c, Layout& L, int32_t P, const int64_t* offs, const double* toas,
+                    const double* nu) {
+  if (P <= 0 || !offs || !toas || !nu) return fail(c, FPTA_EINVAL, "set_toas: bad arguments");
+  if (offs[0] != 0) return fail(c, FPTA_EINVAL, "set_toas: offs[0] must be 0");
+  int64_t mx = 0;
+  for (int32_t p = 0; p < P; ++p) {
+    const int64_t n = offs[p + 1] - offs[p];
+    if (n <= 0) return fail(c, FPTA_EINVAL, "set_toas: every pulsar needs >= 1 TOA");
+    if (n > (int64_t)1 << 30) return fail(c, FPTA_EINVAL, "set_toas: too many TOAs in one pulsar");
+    mx = std::max(mx, n);
+  }
+  const int64_t N = offs[P];
+  L.clear_signals();
+  L.P = P;
+  L.n_toa = N;
+  L.max_np = mx;
+  L.h_offs.assign(offs, offs + P + 1);
+  std::vector<int32_t> psr_of(N);
+  for (int32_t p = 0; p < P; ++p)
+    for (int64_t t = offs[p]; t < offs[p + 1]; ++t) psr_of[t] = p;
+  int rc;
+  if ((rc = upload(c, L.offs, offs, sizeof(int64_t) * (P + 1), "set_toas offs"))) return rc;
+  if ((rc = upload(c, L.toas, toas, sizeof(double) * N, "set_toas toas"))) return rc;
+  if ((rc = upload(c, L.nu, nu, sizeof(double) * N, "set_toas nu"))) return rc;
+  if ((rc = upload(c, L.psr_of, psr_of.data(), sizeof(int32_t) * N, "set_toas psr_of"))) return rc;
+  HIPCHK(c, hipStreamSynchronize(c->stream), "set_toas sync");
+  return FPTA_OK;
+}
+
+// Harmonic test: w[k] == (k+1) w[0] to a few ulp (the f_k = k/T grids of fake_pta.py:264).
+bool is_harmonic(const double* w, int32_t nm) {
+  if (nm < 2 || !(w[0] > 0.0)) return false;
+  for (int32_t k = 1; k < nm; ++k) {
+    const double want = (k + 1) * w[0];
+    if (std::fabs(w[k] - want) > 8.0 * 2.220446049250313e-16 * std::fabs(want)) return false;
+  }
+  return true;
+}
+
+int layout_add_signal(fpta_ctx* c, Layout& L, int32_t kind, int32_t nm, const double* f, const double* amp,
+                      double idx, double freqf, const double* Lmat, const uint8_t* mask) {
+  if (L.P <= 0) return fail(c, FPTA_ESTATE, "add_signal: set_toas first");
+  if ((kind != 0 && kind != 1) || nm <= 0 || !f || !amp)
+    return fail(c, FPTA_EINVAL, "add_signal: bad kind / n_modes / arrays");
+  if (kind == 1 && !Lmat) return fail(c, FPTA_EINVAL, "add_signal: common signal needs an ORF factor");
+  if (L.segs.size() >= 4096) return fail(c, FPTA_EINVAL, "add_signal: too many signals");
+  const int32_t P = L.P;
+  const int32_t nmp = nm + (nm & 1);
+  const int32_t rows = kind == 0 ? P : 1;
+  std::vector<double> w((size_t)rows * nmp), a((size_t)rows * nmp, 0.0);
+  bool harm = true;
+  for (int32_t r = 0; r < rows; ++r) {
+    for (int32_t k = 0; k < nm; ++k) {
+      // 2*pi*f in the reference's operation order: (2*np.pi) * f  (fake_pta.py:386)
+      w[(size_t)r * nmp + k] = (2.0 * M_PI) * f[(size_t)r * nm + k];
+      a[(size_t)r * nmp + k] = amp[(size_t)r * nm + k];
+      if (!std::isfinite(w[(size_t)r * nmp + k]) || !std::isfinite(a[(size_t)r * nmp + k]))
+        return fail(c, FPTA_EINVAL, "add_signal: non-finite frequency or amplitude");
+    }
+    if (nmp != nm) {  // padding mode: amplitude 0, frequency continues the grid
+      const double w0 = w[(size_t)r * nmp];
+      w[(size_t)r * nmp + nm] = w[(size_t)r * nmp + nm - 1] + w0;
+    }
+    harm = harm && is_harmonic(&w[(size_t)r * nmp], nmp);
+  }
+  Seg* s = new Seg();
+  s->nm_orig = nm;
+  int rc;
+  if ((rc = upload(c, s->w, w.data(), sizeof(double) * w.size(), "add_signal w")) ||
+      (rc = upload(c, s->amp, a.data(), sizeof(double) * a.size(), "add_signal amp"))) {
+    delete s;
+    return rc;
+  }
+  if (kind == 1 && (rc = upload(c, s->L, Lmat, sizeof(double) * (size_t)P * P, "add_signal L"))) {
+    delete s;
+    return rc;
+  }
+  if (mask && (rc = upload(c, s->mask, mask, (size_t)L.n_toa, "add_signal mask"))) {
+    delete s;
+    return rc;
+  }
+  SegDesc& d = s->d;
+  d.w = s->w.as<double>();
+  d.amp = s->amp.as<double>();
+  d.L = kind == 1 ? s->L.as<double>() : nullptr;
+  d.mask = mask ? s->mask.as<uint8_t>() : nullptr;
+  d.w_pstride = kind == 0 ? nmp : 0;
+  d.idx = idx;
+  d.freqf = freqf;
+  d.nm = nmp;
+  d.kind = kind;
+  d.col0 = L.K;
+  d.harmonic = harm ? 1 : 0;
+  L.K += 2 * nmp;
+  L.segs.push_back(s);
+  L.dirty = true;
+  HIPCHK(c, hipStreamSynchronize(c->stream), "add_signal sync");  // host vectors go out of scope
+  return (int)(L.segs.size() - 1);
+}
+
+int layout_finalize(fpta_ctx* c, Layout& L) {
+  if (!L.dirty) return FPTA_OK;
+  std::vector<SegDesc> d;
+  for (Seg* s : L.segs) d.push_back(s->d);
+  int rc = upload(c, L.segdesc, d.data(), sizeof(SegDesc) * d.size(), "segdesc");
+  if (rc) return rc;
+  HIPCHK(c, hipStreamSynchronize(c->stream), "segdesc sync");
+  L.dirty = false;
+  return FPTA_OK;
+}
+
+int32_t round_up(int32_t x, int32_t m) { return (x + m - 1) / m * m; }
+
+// Draw + mix every segment into c->coef [P][K][R_pad].
+int run_coefficients(fpta_ctx* c, Layout& L, uint64_t seed, int64_t real0, int32_t R, int32_t R_pad,
+                     const double* zin, int32_t zin_nm, double* x_out) {
+  const int32_t P = L.P;
+  HIPCHK(c, c->coef.ensure(sizeof(double) * (size_t)P * std::max(L.K, 1) * R_pad), "coef alloc");
+  size_t zb = 0;
+  for (Seg* s : L.segs)
+    if (s->d.kind == 1) zb = std::max(zb, sizeof(double) * (size_t)P * 2 * s->d.nm * R_pad);
+  if (zb) HIPCHK(c, c->zbuf.ensure(zb), "zbuf alloc");
+  const uint32_t k0 = (uint32_t)(seed & 0xFFFFFFFFull), k1 = (uint32_t)(seed >> 32);
+  for (size_t i = 0; i < L.segs.size(); ++i) {
+    const SegDesc& d = L.segs[i]->d;
+    {
+      KTimer kt(c, FPTA_K_GEN);
+      HIPCHK(c,
+             launch_gen(c->stream, d, (int32_t)i, P, R, R_pad, real0, k0, k1, zin, (int32_t)L.segs.size(),
+                        zin_nm, c->coef.as<double>(), L.K, c->zbuf.as<double>()),
+             "k_gen launch");
+    }
+    if (d.kind == 1) {
+      KTimer kt(c, FPTA_K_MIX);
+      HIPCHK(c, launch_mix(c->stream, d, P, R_pad, c->zbuf.as<double>(), c->coef.as<double>(), L.K, x_out),
+             "k_mix launch");
+    }
+  }
+  return FPTA_OK;
+}
+
+int build_tiles(fpta_ctx* c, Layout& L, int32_t R) {
+  if (L.tiles_R == R) return FPTA_OK;
+  std::vector<int4> t;
+  for (int32_t p = 0; p < L.P; ++p) {
+    const int64_t np_ = L.h_offs[p + 1] - L.h_offs[p];
+    for (int32_t r0 = 0; r0 < R; r0 += kTileReal)
+      for (int64_t t0 = 0; t0 < np_; t0 += kTileToa) t.push_back(make_int4(p, (int)t0, r0, 0));
+  }
+  // XCD-aware order: workgroups b, b+8, b+16, ... share an XCD's L2 (round-robin dispatch), so give
+  // them consecutive tiles (same pulsar and realization tile -> same coefficient block).
+  const size_t n = t.size();
+  const size_t per = (n + 7) / 8;
+  std::vector<int4> o(per * 8, make_int4(-1, 0, 0, 0));
+  for (size_t b = 0; b < o.size(); ++b) {
+    const size_t tile = (b % 8) * per + b / 8;
+    if (tile < n) o[b] = t[tile];
+  }
+  int rc = upload(c, L.tiles, o.data(), sizeof(int4) * o.size(), "tiles");
+  if (rc) return rc;
+  HIPCHK(c, hipStreamSynchronize(c->stream), "tiles sync");
+  L.n_tiles = (int32_t)o.size();
+  L.tiles_R = R;
+  return FPTA_OK;
+}
+
+int run_synth(fpta_ctx* c, Layout& L, int32_t R, int32_t R_pad, double* out, int64_t ldo, int accumulate,
+              bool allow_mfma) {
+  SynthArgs a{};
+  a.offs = L.offs.as<int64_t>();
+  a.psr_of = L.psr_of.as<int32_t>();
+  a.toas = L.toas.as<double>();
+  a.nu = L.nu.as<double>();
+  a.segs = L.segdesc.as<SegDesc>();
+  a.n_seg = (int32_t)L.segs.size();
+  a.P = L.P;
+  a.n_toa = L.n_toa;
+  a.coef = c->coef.as<double>();
+  a.K = L.K;
+  a.R_pad = R_pad;
+  a.out = out;
+  a.ldo = ldo;
+  a.n_real = R;
+  a.accumulate = accumulate;
+  a.anchor = std::max(1, c->anchor);
+  bool mfma = allow_mfma && (c->synth_path == 2 || (c->synth_path == 0 && R >= c->mfma_min_real));
+  if (c->synth_path == 1) mfma = false;
+  if (mfma) {
+    int rc = build_tiles(c, L, R);
+    if (rc) return rc;
+    KTimer kt(c, FPTA_K_SYNTH);
+    HIPCHK(c, launch_synth_mfma(c->stream, a, L.tiles.as<int4>(), L.n_tiles), "k_synth_mfma launch");
+  } else {
+    if (R > 65535) return fail(c, FPTA_EINVAL, "direct synthesis path: n_real > 65535");
+    KTimer kt(c, FPTA_K_SYNTH);
+    HIPCHK(c, launch_synth_direct(c->stream, a), "k_synth_direct launch");
+  }
+  return FPTA_OK;
+}
+
+int blocks_to_owner(fpta_ctx* c, int64_t n_toa, int64_t n_blocks, const int64_t* boffs, const int64_t* bidx,
+                    std::vector<int32_t>& owner) {
+  owner.assign(n_toa, -1);
+  if (n_blocks > (int64_t)0x7FFFFFFF) return fail(c, FPTA_EINVAL, "white: too many ECORR blocks");
+  if (n_blocks > 0 && (!boffs || !bidx || boffs[0] != 0))
+    return fail(c, FPTA_EINVAL, "white: bad ECORR block CSR");
+  for (int64_t b = 0; b < n_blocks; ++b) {
+    if (boffs[b + 1] < boffs[b]) return fail(c, FPTA_EINVAL, "white: block offsets not monotone");
+    for (int64_t j = boffs[b]; j < boffs[b + 1]; ++j) {
+      const int64_t t = bidx[j];
+      if (t < 0 || t >= n_toa) return fail(c, FPTA_EINVAL, "white: block TOA index out of range");
+      if (owner[t] >= 0) return fail(c, FPTA_EINVAL, "white: a TOA belongs to two ECORR blocks");
+      owner[t] = (int32_t)b;
+    }
+  }
+  return FPTA_OK;
+}
+
+}  // namespace
+
+// =============================================================================================== API
+extern "C" {
+
+int fpta_version(void) { return 10000; }
+
+const char* fpta_last_error(const fpta_ctx* ctx) { return ctx ? ctx->err.c_str() : g_err.c_str(); }
+
+int fpta_device_count(int* n) {
+  if (!n) return fail(nullptr, FPTA_EINVAL, "device_count: null");
+  int k = 0;
+  hipError_t e = hipGetDeviceCount(&k);
+  if (e != hipSuccess) {
+    *n = 0;
+    return hip_fail(nullptr, e, "hipGetDeviceCount");
+  }
+  *n = k;
+  return FPTA_OK;
+}
+
+int fpta_create(int device, fpta_ctx** out) {
+  if (!out) return fail(nullptr, FPTA_EINVAL, "create: null out");
+  *out = nullptr;
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess || n <= 0) return fail(nullptr, FPTA_EDEVICE, "create: no HIP device visible");
+  if (device < 0 || device >= n) return fail(nullptr, FPTA_EINVAL, "create: device index out of range");
+  e = hipSetDevice(device);
+  if (e != hipSuccess) return hip_fail(nullptr, e, "hipSetDevice");
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess) {
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+      return fail(nullptr, FPTA_EDEVICE, std::string("create: built for gfx950, device is ") + prop.gcnArchName);
+  }
+  fpta_ctx* c = new fpta_ctx();
+  c->device = device;
+  e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    delete c;
+    return hip_fail(nullptr, e, "hipStreamCreate");
+  }
+  *out = c;
+  return FPTA_OK;
+}
+
+int fpta_destroy(fpta_ctx* c) {
+  if (!c) return FPTA_OK;
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(c->stream);
+  for (auto& p : c->pending) {
+    (void)hipEventDestroy(p.a);
+    (void)hipEventDestroy(p.b);
+  }
+  for (auto e : c->pool) (void)hipEventDestroy(e);
+  (void)hipStreamDestroy(c->stream);
+  delete c;
+  return FPTA_OK;
+}
+
+int fpta_set_option(fpta_ctx* c, int32_t key, int64_t value) {
+  if (!c) return fail(nullptr, FPTA_EINVAL, "set_option: null ctx");
+  switch (key) {
+    case FPTA_OPT_SYNTH_PATH:
+      if (value < 0 || value > 2) return fail(c, FPTA_EINVAL, "synth path must be 0, 1 or 2");
+      c->synth_path = (int)value;
+      return FPTA_OK;
+    case FPTA_OPT_MFMA_MIN_REAL:
+      c->mfma_min_real = (int)std::max<int64_t>(1, value);
+      return FPTA_OK;
+    case FPTA_OPT_PROFILE:
+      c->profile = value ? 1 : 0;
+      return FPTA_OK;
+    case FPTA_OPT_ANCHOR:
+      if (value < 1 || value > 1 << 20) return fail(c, FPTA_EINVAL, "anchor must be >= 1");
+      c->anchor = (int)value;
+      return FPTA_OK;
+  }
+  return fail(c, FPTA_EINVAL, "set_option: unknown key");
+}
+
+int fpta_synchronize(fpta_ctx* c) {
+  if (!c) return fail(nullptr, FPTA_EINVAL, "null ctx");
+  HIPCHK(c, hipSetDevice(c->device), "hipSetDevice");
+  HIPCHK(c, hipStreamSynchronize(c->stream), "hipStreamSynchronize");
+  return FPTA_OK;
+}
+
+int fpta_kernel_stats(fpta_ctx* c, int32_t which, int64_t* count, double* total_ms) {
+  if (!c || which < 0 || which >= FPTA_K_N) return fail(c, FPTA_EINVAL, "kernel_stats: bad args");
+  HIPCHK(c, hipSetDevice(c->device), "hipSetDevice");
+  for (auto& p : c->pending) {
+    HIPCHK(c, hipEventSynchronize(p.b), "hipEventSynchronize");
+    float ms = 0.f;
+    HIPCHK(c, hipEventElapsedTime(&ms, p.a, p.b), "hipEventElapsedTime");
+    c->kcount[p.which] += 1;
+    c->kms[p.which] += ms;
+    c->pool.push_back(p.a);
+    c->pool.push_back(p.b);
+  }
+  c->pending.clear();
+  if (count) *count = c->kcount[which];
+  if (total_ms) *total_ms = c->kms[which];
+  return FPTA_OK;
+}
+
+int fpta_reset_stats(fpta_ctx* c) {
+  if (!c) return fail(nullptr, FPTA_EINVAL, "null ctx");
+  int rc = fpta_kernel_stats(c, 0, nullptr, nullptr);
+  if (rc) return rc;
+  for (int i = 0; i < FPTA_K_N; ++i) {
+    c->kcount[i] = 0;
+    c->kms[i] = 0;
+  }
+  return FPTA_OK;
+}
+
+// ------------------------------------------------------------------------------------ drop-in
+int fpta_gp_accumulate(fpta_ctx* c, int64_t n_toa, const double* toas, const double* nu, int32_t n_seg,
+                       const int32_t* seg_nmodes, const double* f, const double* ccos, const double* csin,
+                       const double* seg_idx, const double* seg_freqf, const uint8_t* mask, double sign,
+                       double* residuals) {
+  if (!c) return fail(nullptr, FPTA_EINVAL, "null ctx");
+  if (n_toa <= 0 || n_seg <= 0 || !toas || !nu || !seg_nmodes || !f || !ccos || !csin || !seg_idx ||
+      !seg_freqf || !residuals)
+    return fail(c, FPTA_EINVAL, "gp_accumulate: bad arguments");
+  HIPCHK(c, hipSetDevice(c->device), "hipSetDevice");
+  Layout& L = c->scratch;
+  const int64_t offs[2] = {0, n_toa};
+  int rc = layout_set_toas(c, L, 1, offs, toas, nu);
+  if (rc) return rc;
+  int64_t m0 = 0, nmax = 0;
+  for (int32_t s = 0; s < n_seg; ++s) {
+    const int32_t nm = seg_nmodes[s];
+    if (nm <= 0) return fail(c, FPTA_EINVAL, "gp_accumulate: segment with no modes");
+    std::vector<double> amp(nm, sign);  // coefficient = sign * (ccos, csin) through the from-z path
+    rc = layout_add_signal(c, L, 0, nm, f + m0, amp.data(), seg_idx[s], seg_freqf[s], nullptr,
+                           mask ? mask + (size_t)s * n_toa : nullptr);
+    if (rc < 0) return rc;
+    m0 += nm;
+    nmax = std::max<int64_t>(nmax, nm + (nm & 1));
+  }
+  if ((rc = layout_finalize(c, L))) return rc;
+  // z [1][n_seg][1][nmax][2] = (ccos, csin)
+  std::vector<double> z((size_t)n_seg * nmax * 2, 0.0);
+  m0 = 0;
+  for (int32_t s = 0; s < n_seg; ++s) {
+    for (int32_t k = 0; k < seg_nmodes[s]; ++k) {
+      z[((size_t)s * nmax + k) * 2] = ccos[m0 + k];
+      z[((size_t)s * nmax + k) * 2 + 1] = csin[m0 + k];
+    }
+    m0 += seg_nmodes[s];
+  }
+  if ((rc = upload(c, c->zin, z.data(), sizeof(double) * z.size(), "gp_accumulate z"))) return rc;
+  if ((rc = run_coefficients(c, L, 0, 0, 1, kRealPad, c->zin.as<double>(), (int32_t)nmax, nullptr))) return rc;
+  if ((rc = upload(c, c->scratch_out, residuals, sizeof(double) * n_toa, "gp_accumulate residuals"))) return rc;
+  if ((rc = run_synth(c, L, 1, kRealPad, c->scratch_out.as<double>(), n_toa, 1, false))) return rc;
+  HIPCHK(c, hipMemcpyAsync(residuals, c->scratch_out.p, sizeof(double) * n_toa, hipMemcpyDeviceToHost, c->stream),
+         "gp_accumulate download");
+  HIPCHK(c, hipStreamSynchronize(c->stream), "gp_accumulate sync");
+  return FPTA_OK;
+}
+
+int fpta_common_accumulate(fpta_ctx* c, int32_t n_psr, const int64_t* offs, const double* toas, const double* nu,
+                           int32_t n_modes, const double* f, const double* amp, double idx, double freqf,
+                           const double* Lmat, const double* z, double* residuals, double* x_out) {
+  if (!c) return fail(nullptr, FPTA_EINVAL, "null ctx");
+  if (n_psr <= 0 || n_modes <= 0 || !offs || !toas || !nu || !f || !amp || !Lmat || !z || !residuals)
+    return fail(c, FPTA_EINVAL, "common_accumulate: bad arguments");
+  HIPCHK(c, hipSetDevice(c->device), "hipSetDevice");
+  Layout& L = c->scratch;
+  int rc = layout_set_toas(c, L, n_psr, offs, toas, nu);
+  if (rc) return rc;
+  rc = layout_add_signal(c, L, 1, n_modes, f, amp, idx, freqf, Lmat, nullptr);
+  if (rc < 0) return rc;
+  if ((rc = layout_finalize(c, L))) return rc;
+  const int32_t nmp = L.segs[0]->d.nm;
+  // reference draw order z[k][0 = sin, 1 = cos][p] -> zin[0][0][p][k][0 = cos, 1 = sin]
+  std::vector<double> zz((size_t)n_psr * nmp * 2, 0.0);
+  for (int32_t k = 0; k < n_modes; ++k)
+    for (int32_t p = 0; p < n_psr; ++p) {
+      zz[((size_t)p * nmp + k) * 2] = z[((size_t)k * 2 + 1) * n_psr + p];
+      zz[((size_t)p * nmp + k) * 2 + 1] = z[((size_t)k * 2 + 0) * n_psr + p];
+    }
+  if ((rc = upload(c, c->zin, zz.data(), sizeof(double) * zz.size(), "common z"))) return rc;
+  const int64_t M = (int64_t)2 * nmp * kRealPad;
+  double* xdev = nullptr;
+  if (x_out) {
+    HIPCHK(c, c->xout.ensure(sizeof(double) * (size_t)n_psr * M), "x_out alloc");
+    xdev = c->xout.as<double>();
+  }
+  if ((rc = run_coefficients(c, L, 0, 0, 1, kRealPad, c->zin.as<double>(), nmp, xdev))) return rc;
+  const int64_t N = offs[n_psr];
+  if ((rc = upload(c, c->scratch_out, residuals, sizeof(double) * N, "common residuals"))) return rc;
+  if ((rc = run_synth(c, L, 1, kRealPad, c->scratch_out.as<double>(), N, 1, false))) return rc;
+  HIPCHK(c, hipMemcpyAsync(residuals, c->scratch_out.p, sizeof(double) * N, hipMemcpyDeviceToHost, c->stream),
+         "common download");
+  std::vector<double> xh;
+  if (x_out) {
+    xh.resize((size_t)n_psr * M);
+    HIPCHK(c, hipMemcpyAsync(xh.data(), xdev, sizeof(double) * xh.size(), hipMemcpyDeviceToHost, c->stream),
+           "x download");
+  }
+  HIPCHK(c, hipStreamSynchronize(c->stream), "common sync");
+  if (x_out) {  // [p][j = 2k + c][r = 0] -> x_out[k][c][p]
+    for (int32_t k = 0; k < n_modes; ++k)
+      for (int32_t cc = 0; cc < 2; ++cc)
+        for (int32_t p = 0; p < n_psr; ++p)
+          x_out[((size_t)k * 2 + cc) * n_psr + p] = xh[(size_t)p * M + (size_t)(2 * k + cc) * kRealPad];
+  }
+  return FPTA_OK;
+}
+
+int fpta_white_accumulate(fpta_ctx* c, int64_t n_toa, const double* sigma, const double* z, int64_t n_blocks,
+                          const int64_t* block_offs, const int64_t* block_idx, const double* ecorr_sigma,
+                          const double* zb, double* residuals) {
+  if (!c) return fail(nullptr, FPTA_EINVAL, "null ctx");
+  if (n_toa <= 0 || !sigma || !z || !residuals || n_blocks < 0 || (n_blocks > 0 && (!ecorr_sigma || !zb)))
+    return fail(c, FPTA_EINVAL, "white_accumulate: bad arguments");
+  HIPCHK(c, hipSetDevice(c->device), "hipSetDevice");
+  std::vector<int32_t> owner;
+  int rc = blocks_to_owner(c, n_toa, n_blocks, block_offs, block_idx, owner);
+  if (rc) return rc;
+  if ((rc = upload(c, c->scratch_sigma, sigma, sizeof(double) * n_toa, "white sigma"))) return rc;
+  if ((rc = upload(c, c->scratch_z, z, sizeof(double) * n_toa, "white z"))) return rc;
+  if (n_blocks > 0) {
+    if ((rc = upload(c, c->scratch_block_of, owner.data(), sizeof(int32_t) * n_toa, "white owner"))) return rc;
+    if ((rc = upload(c, c->scratch_esig, ecorr_sigma, sizeof(double) * n_blocks, "white esig"))) return rc;
+    if ((rc = upload(c, c->scratch_zb, zb, sizeof(double) * n_blocks, "white zb"))) return rc;
+  }
+  if ((rc = upload(c, c->scratch_out, residuals, sizeof(double) * n_toa, "white residuals"))) return rc;
+  {
+    KTimer kt(c, FPTA_K_WHITE);
+    HIPCHK(c,
+           launch_white(c->stream, c->scratch_sigma.as<double>(),
+                        n_blocks > 0 ? c->scratch_block_of.as<int32_t>() : nullptr,
+                        n_blocks > 0 ? c->scratch_esig.as<double>() : nullptr, c->scratch_z.as<double>(),
+                        n_blocks > 0 ? c->scratch_zb.as<double>() : nullptr, c->scratch_out.as<double>(), n_toa,
+                        n_toa, 1, 0, 0, 0),
+           "k_white launch");
+  }
+  HIPCHK(c, hipMemcpyAsync(residuals, c->scratch_out.p, sizeof(double) * n_toa, hipMemcpyDeviceToHost, c->stream),
+         "white download");
+  HIPCHK(c, hipStreamSynchronize(c->stream), "white sync");
+  return FPTA_OK;
+}
+
+// ------------------------------------------------------------------------------------ batch
+int fpta_batch_set_toas(fpta_ctx* c, int32_t n_psr, const int64_t* offs, const double* toas, const double* nu) {
+  if (!c) return fail(nullptr, FPTA_EINVAL, "null ctx");
+  HIPCHK(c, hipSetDevice(c->device), "hipSetDevice");
+  c->has_sigma = c->has_blocks = false;
+  c->out_R = 0;
+  return layout_set_toas(c, c->batch, n_psr, offs, toas, nu);
+}
+
+int fpta_batch_add_signal(fpta_ctx* c, int32_t kind, int32_t n_modes, const double* f, const double* amp,
+                          double idx, double freqf, const double* Lmat, const uint8_t* mask) {
+  if (!c) return fail(nullptr, FPTA_EINVAL, "null ctx");
+  HIPCHK(c, hipSetDevice(c->device), "hipSetDevice");
+  return layout_add_signal(c, c->batch, kind, n_modes, f, amp, idx, freqf, Lmat, mask);
+}
+
+int fpta_batch_clear_signals(fpta_ctx* c) {
+  if (!c) return fail(nullptr, FPTA_EINVAL, "null ctx");
+  c->batch.clear_signals();
+  c->has_sigma = c->has_blocks = false;
+  return FPTA_OK;
+}
+
+int fpta_batch_set_white(fpta_ctx* c, const double* sigma, int64_t n_blocks, const int64_t* block_offs,
+                         const int64_t* block_idx, const double* ecorr_sigma) {
+  if (!c) return fail(nullptr, FPTA_EINVAL, "null ctx");
+  if (c->batch.P <= 0) return fail(c, FPTA_ESTATE, "set_white: set_toas first");
+  HIPCHK(c, hipSetDevice(c->device), "hipSetDevice");
+  const int64_t N = c->batch.n_toa;
+  int rc;
+  c->has_sigma = sigma != nullptr;
+  if (sigma && (rc = upload(c, c->sigma, sigma, sizeof(double) * N, "set_white sigma"))) return rc;
+  c->has_blocks = n_blocks > 0;
+  if (n_blocks > 0) {
+    if (!ecorr_sigma) return fail(c, FPTA_EINVAL, "set_white: ecorr_sigma missing");
+    std::vector<int32_t> owner;
+    if ((rc = blocks_to_owner(c, N, n_blocks, block_offs, block_idx, owner))) return rc;
+    if ((rc = upload(c, c->block_of, owner.data(), sizeof(int32_t) * N, "set_white owner"))) return rc;
+    if ((rc = upload(c, c->esig, ecorr_sigma, sizeof(double) * n_blocks, "set_white esig"))) return rc;
+  }
+  HIPCHK(c, hipStreamSynchronize(c->stream), "set_white sync");
+  return FPTA_OK;
+}
+
+static int batch_common(fpta_ctx* c, uint64_t seed, int64_t real0, int32_t n_real, const double* zin,
+                        int32_t zin_nm, double* out, double* coeffs_out, bool white) {
+  if (!c) return fail(nullptr, FPTA_EINVAL, "null ctx");
+  Layout& L = c->batch;
+  if (L.P <= 0) return fail(c, FPTA_ESTATE, "batch_synth: set_toas first");
+  if (n_real <= 0) return fail(c, FPTA_EINVAL, "batch_synth: n_real must be > 0");
+  if (real0 < 0 || real0 + n_real > ((int64_t)1 << 32))
+    return fail(c, FPTA_EINVAL, "batch_synth: realization index exceeds the 32-bit Philox counter word");
+  HIPCHK(c, hipSetDevice(c->device), "hipSetDevice");
+  int rc = layout_finalize(c, L);
+  if (rc) return rc;
+  const int32_t R_pad = round_up(n_real, kRealPad);
+  const size_t out_bytes = sizeof(double) * (size_t)n_real * L.n_toa;
+  HIPCHK(c, c->out.ensure(out_bytes), "out alloc");
+  c->out_R = n_real;
+  c->out_ld = L.n_toa;
+  if (L.segs.empty()) {
+    HIPCHK(c, hipMemsetAsync(c->out.p, 0, out_bytes, c->stream), "out memset");
+  } else {
+    if ((rc = run_coefficients(c, L, seed, real0, n_real, R_pad, zin, zin_nm, nullptr))) return rc;
+    if ((rc = run_synth(c, L, n_real, R_pad, c->out.as<double>(), L.n_toa, 0, true))) return rc;
+  }
+  if (white && (c->has_sigma || c->has_blocks)) {
+    if (n_real > 65535) return fail(c, FPTA_EINVAL, "white: n_real > 65535 per call");
+    KTimer kt(c, FPTA_K_WHITE);
+    HIPCHK(c,
+           launch_white(c->stream, c->has_sigma ? c->sigma.as<double>() : nullptr,
+                        c->has_blocks ? c->block_of.as<int32_t>() : nullptr,
+                        c->has_blocks ? c->esig.as<double>() : nullptr, nullptr, nullptr, c->out.as<double>(),
+                        L.n_toa, L.n_toa, n_real, real0, (uint32_t)(seed & 0xFFFFFFFFull), (uint32_t)(seed >> 32)),
+           "k_white launch");
+  }
+  if (out) HIPCHK(c, hipMemcpyAsync(out, c->out.p, out_bytes, hipMemcpyDeviceToHost, c->stream), "out download");
+  if (coeffs_out && L.K > 0) {
+    // [P][K][R_pad] -> [P][K][n_real]
+    HIPCHK(c,
+           hipMemcpy2DAsync(coeffs_out, sizeof(double) * n_real, c->coef.p, sizeof(double) * R_pad,
+                            sizeof(double) * n_real, (size_t)L.P * L.K, hipMemcpyDeviceToHost, c->stream),
+           "coef download");
+  }
+  if (out || coeffs_out) HIPCHK(c, hipStreamSynchronize(c->stream), "batch sync");
+  return FPTA_OK;
+}
+
+int fpta_batch_synth(fpta_ctx* c, uint64_t seed, int64_t real0, int32_t n_real, double* out, double* coeffs_out) {
+  return batch_common(c, seed, real0, n_real, nullptr, 0, out, coeffs_out, true);
+}
+
+int fpta_batch_synth_from_z(fpta_ctx* c, int32_t n_real, int32_t n_modes_max, const double* z, double* out) {
+  if (!c) return fail(nullptr, FPTA_EINVAL, "null ctx");
+  if (!z || n_modes_max <= 0 || n_real <= 0) return fail(c, FPTA_EINVAL, "synth_from_z: bad arguments");
+  for (Seg* s : c->batch.segs)
+    if (s->nm_orig > n_modes_max) return fail(c, FPTA_EINVAL, "synth_from_z: n_modes_max too small");
+  HIPCHK(c, hipSetDevice(c->device), "hipSetDevice");
+  const size_t bytes = sizeof(double) * (size_t)n_real * c->batch.segs.size() * c->batch.P * n_modes_max * 2;
+  int rc = upload(c, c->zin, z, bytes, "synth_from_z z");
+  if (rc) return rc;
+  return batch_common(c, 0, 0, n_real, c->zin.as<double>(), n_modes_max, out, nullptr, false);
+}
+
+int fpta_batch_device_out(fpta_ctx* c, double** dptr, int64_t* ld, int32_t* n_real) {
+  if (!c) return fail(nullptr, FPTA_EINVAL, "null ctx");
+  if (!c->out_R) return fail(c, FPTA_ESTATE, "device_out: nothing synthesized yet");
+  if (dptr) *dptr = c->out.as<double>();
+  if (ld) *ld = c->out_ld;
+  if (n_real) *n_real = c->out_R;
+  return FPTA_OK;
+}
+
+int fpta_batch_checksums(fpta_ctx* c, double* sums) {
+  if (!c || !sums) return fail(c, FPTA_EINVAL, "checksums: bad arguments");
+  if (!c->out_R) return fail(c, FPTA_ESTATE, "checksums: nothing synthesized yet");
+  HIPCHK(c, hipSetDevice(c->device), "hipSetDevice");
+  HIPCHK(c, c->sums.ensure(sizeof(double) * 2 * c->out_R), "sums alloc");
+  HIPCHK(c, launch_checksums(c->stream, c->out.as<double>(), c->out_ld, c->out_ld, c->out_R, c->sums.as<double>()),
+         "k_checksums launch");
+  HIPCHK(c, hipMemcpyAsync(sums, c->sums.p, sizeof(double) * 2 * c->out_R, hipMemcpyDeviceToHost, c->stream),
+         "sums download");
+  HIPCHK(c, hipStreamSynchronize(c->stream), "checksums sync");
+  return FPTA_OK;
+}
+
+int fpta_batch_info(fpta_ctx* c, int64_t* info) {
+  if (!c || !info) return fail(c, FPTA_EINVAL, "info: bad arguments");
+  info[0] = c->batch.P;
+  info[1] = c->batch.n_toa;
+  info[2] = (int64_t)c->batch.segs.size();
+  info[3] = c->batch.K;
+  info[4] = c->batch.max_np;
+  return FPTA_OK;
+}
+
+int fpta_debug_philox(fpta_ctx* c, int64_t n, const uint32_t* ctr, const uint32_t* key, uint32_t* out) {
+  if (!c || n <= 0 || !ctr || !key || !out) return fail(c, FPTA_EINVAL, "debug_philox: bad arguments");
+  HIPCHK(c, hipSetDevice(c->device), "hipSetDevice");
+  int rc = upload(c, c->dbg_a, ctr, sizeof(uint32_t) * 4 * n, "philox ctr");
+  if (rc) return rc;
+  HIPCHK(c, c->dbg_b.ensure(sizeof(uint32_t) * 4 * n), "philox out");
+  HIPCHK(c, launch_philox(c->stream, n, c->dbg_a.as<uint32_t>(), key[0], key[1], c->dbg_b.as<uint32_t>()),
+         "k_philox launch");
+  HIPCHK(c, hipMemcpyAsync(out, c->dbg_b.p, sizeof(uint32_t) * 4 * n, hipMemcpyDeviceToHost, c->stream),
+         "philox download");
+  HIPCHK(c, hipStreamSynchronize(c->stream), "philox sync");
+  return FPTA_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,65 @@
+// Internal declarations shared by kernels.hip (device code + launchers) and capi.cpp.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace fpta {
+
+// One GP signal ("segment") of a layout, as the kernels see it.
+struct SegDesc {
+  const double* w;      // angular frequencies 2*pi*f: kind 0 -> [P][nm], kind 1 -> [nm]
+  const double* amp;    // coefficient std-devs sqrt(S*df): same shape as w
+  const double* L;      // kind 1: ORF factor [P][P] row-major (x = L z); else null
+  const uint8_t* mask;  // [n_toa_total] or null
+  int64_t w_pstride;    // nm (kind 0) or 0 (kind 1)
+  double idx;           // chromatic index
+  double freqf;         // reference radio frequency (MHz)
+  int32_t nm;           // modes, padded to even (padding modes have amp 0)
+  int32_t kind;         // 0 per-pulsar, 1 common
+  int32_t col0;         // first coefficient column of this segment (cos of mode 0)
+  int32_t harmonic;     // 1: w[k] == (k+1) w[0] to rounding -> angle-addition recurrence
+};
+
+struct SynthArgs {
+  const int64_t* offs;    // [P+1]
+  const int32_t* psr_of;  // [n_toa]
+  const double* toas;     // [n_toa] seconds
+  const double* nu;       // [n_toa] MHz
+  const SegDesc* segs;    // [n_seg] (device)
+  int32_t n_seg;
+  int32_t P;
+  int64_t n_toa;
+  const double* coef;  // [P][K][R_pad]
+  int32_t K;
+  int32_t R_pad;
+  double* out;  // [n_real][ldo]
+  int64_t ldo;
+  int32_t n_real;
+  int32_t accumulate;
+  int32_t anchor;
+};
+
+// MFMA tile geometry
+constexpr int kWR = 4;                  // 16-realization fragments per wave
+constexpr int kWT = 2;                  // 16-TOA fragments per wave
+constexpr int kWaves = 4;               // waves per workgroup
+constexpr int kTileReal = kWR * 16;     // realizations per workgroup
+constexpr int kTileToa = kWaves * kWT * 16;  // TOAs per workgroup
+constexpr int kRealPad = 64;            // R_pad granularity
+
+hipError_t launch_gen(hipStream_t st, const SegDesc& sd, int32_t seg_id, int32_t P, int32_t n_real,
+                      int32_t R_pad, int64_t real0, uint32_t k0, uint32_t k1, const double* zin,
+                      int32_t zin_nseg, int32_t zin_nm, double* coef, int32_t K, double* zbuf);
+hipError_t launch_mix(hipStream_t st, const SegDesc& sd, int32_t P, int32_t R_pad, const double* zbuf,
+                      double* coef, int32_t K, double* x_out);
+hipError_t launch_synth_direct(hipStream_t st, const SynthArgs& a);
+hipError_t launch_synth_mfma(hipStream_t st, const SynthArgs& a, const int4* tiles, int32_t n_tiles);
+hipError_t launch_white(hipStream_t st, const double* sigma, const int32_t* block_of, const double* esig,
+                        const double* z, const double* zb, double* out, int64_t ldo, int64_t n_toa,
+                        int32_t n_real, int64_t real0, uint32_t k0, uint32_t k1);
+hipError_t launch_checksums(hipStream_t st, const double* out, int64_t ldo, int64_t n_toa, int32_t n_real,
+                            double* sums);
+hipError_t launch_philox(hipStream_t st, int64_t n, const uint32_t* ctr, uint32_t k0, uint32_t k1,
+                         uint32_t* out);
+
+}  // namespace fpta

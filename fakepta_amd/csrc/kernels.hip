@@ -1,0 +1,392 @@
+// HIP kernels for gfx950 (MI355X): Fourier-basis GP residual synthesis.
+//
+//   k_gen          Philox4x32-10 -> Box-Muller -> coefficient scaling  (north-star step 1)
+//   k_mix          ORF factor applied to the common-signal draws       (step 2)
+//   k_synth_mfma   fused basis generation + contraction on fp64 MFMA   (steps 3/4)
+//   k_synth_direct one sincos per basis element, used for few realizations and
+//                  for the drop-in single-realization calls (exact reference phases)
+//   k_white        white noise + ECORR epochs                          (step 4)
+//
+// Reference semantics: fakepta/fake_pta.py:357-387 (per-pulsar GP), :526-555
+// (reconstruct_signal), :201-230 (white noise); fakepta/correlated_noises.py:111-160
+// (common GP). See DESIGN.md for layouts and rooflines.
+#include <hip/hip_runtime.h>
+
+#include "fpta_internal.h"
+#include "philox.h"
+
+namespace fpta {
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+// (freqf / nu)^idx with numpy's scalar-power fast paths (idx 0 -> 1, idx 2 -> square).
+__device__ __forceinline__ double chrom_factor(double freqf, double nu, double idx) {
+  if (idx == 0.0) return 1.0;
+  const double x = freqf / nu;
+  if (idx == 2.0) return x * x;
+  if (idx == 1.0) return x;
+  return pow(x, idx);
+}
+
+// ----------------------------------------------------------------------------- k_gen
+// grid (ceil(R_pad/256), nm, P). One Philox call per (mode, pulsar, segment, realization)
+// gives the (cos, sin) pair of that mode. Writes every entry of the realization padding.
+__global__ __launch_bounds__(256) void k_gen(SegDesc sd, int32_t seg_id, int32_t P, int32_t n_real,
+                                             int32_t R_pad, int64_t real0, uint32_t k0, uint32_t k1,
+                                             const double* __restrict__ zin, int32_t zin_nseg,
+                                             int32_t zin_nm, double* __restrict__ coef, int32_t K,
+                                             double* __restrict__ zbuf) {
+  const int r = blockIdx.x * 256 + threadIdx.x;
+  if (r >= R_pad) return;
+  const int k = blockIdx.y;
+  const int p = blockIdx.z;
+  double zc = 0.0, zs = 0.0;
+  if (r < n_real) {
+    if (zin) {
+      if (k < zin_nm) {
+        const double* zz = zin + ((((int64_t)r * zin_nseg + seg_id) * P + p) * zin_nm + k) * 2;
+        zc = zz[0];
+        zs = zz[1];
+      }
+    } else {
+      const u32x4 c = {(uint32_t)k, (uint32_t)p, (uint32_t)seg_id, (uint32_t)(real0 + r)};
+      box_muller(philox4x32_10(c, k0, k1), zc, zs);
+    }
+  }
+  if (sd.kind == 0) {
+    const double a = sd.amp[(int64_t)p * sd.nm + k];
+    double* cp = coef + ((int64_t)p * K + sd.col0 + 2 * k) * R_pad + r;
+    cp[0] = a * zc;
+    cp[R_pad] = a * zs;
+  } else {
+    double* zp = zbuf + ((int64_t)p * sd.nm + k) * 2 * R_pad + r;
+    zp[0] = zc;
+    zp[R_pad] = zs;
+  }
+}
+
+// ----------------------------------------------------------------------------- k_mix
+// coef[p][col0 + j][r] = amp[j/2] * sum_q L[p][q] zbuf[q][j][r],  j = 2k + (0 cos | 1 sin).
+// One thread per (j, r) column, MIX_PT pulsar rows per block; L tiles broadcast from LDS.
+constexpr int MIX_PT = 16;
+constexpr int MIX_QT = 64;
+__global__ __launch_bounds__(256) void k_mix(const double* __restrict__ L, const double* __restrict__ amp,
+                                             int32_t P, int64_t M, int32_t R_pad,
+                                             const double* __restrict__ zbuf, double* __restrict__ coef,
+                                             int32_t K, int32_t col0, double* __restrict__ x_out) {
+  __shared__ double Ls[MIX_PT][MIX_QT];
+  const int64_t m = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int p0 = blockIdx.y * MIX_PT;
+  double acc[MIX_PT];
+#pragma unroll
+  for (int i = 0; i < MIX_PT; ++i) acc[i] = 0.0;
+  for (int q0 = 0; q0 < P; q0 += MIX_QT) {
+    for (int e = threadIdx.x; e < MIX_PT * MIX_QT; e += 256) {
+      const int i = e / MIX_QT, jj = e % MIX_QT;
+      const int p = p0 + i, q = q0 + jj;
+      Ls[i][jj] = (p < P && q < P) ? L[(int64_t)p * P + q] : 0.0;
+    }
+    __syncthreads();
+    if (m < M) {
+      const int qmax = min(MIX_QT, P - q0);
+      const double* zp = zbuf + (int64_t)q0 * M + m;
+      for (int jj = 0; jj < qmax; ++jj) {
+        const double zv = zp[(int64_t)jj * M];
+#pragma unroll
+        for (int i = 0; i < MIX_PT; ++i) acc[i] = fma(Ls[i][jj], zv, acc[i]);
+      }
+    }
+    __syncthreads();
+  }
+  if (m < M) {
+    const int j = (int)(m / R_pad);
+    const int r = (int)(m % R_pad);
+    const double a = amp[j >> 1];
+#pragma unroll
+    for (int i = 0; i < MIX_PT; ++i) {
+      const int p = p0 + i;
+      if (p < P) {
+        coef[((int64_t)p * K + col0 + j) * R_pad + r] = a * acc[i];
+        if (x_out) x_out[(int64_t)p * M + m] = acc[i];
+      }
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------- k_synth_direct
+// grid (ceil(n_toa/256), n_real). One thread per (TOA, realization); the phase of every basis
+// element is (2 pi f_k) t computed exactly as fake_pta.py:386, then sincos.
+__global__ __launch_bounds__(256) void k_synth_direct(SynthArgs a) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int r = blockIdx.y;
+  if (t >= a.n_toa) return;
+  const int p = a.psr_of[t];
+  const double toa = a.toas[t];
+  const double nu = a.nu[t];
+  const double* cbase = a.coef + (int64_t)p * a.K * a.R_pad + r;
+  double acc = 0.0;
+  for (int s = 0; s < a.n_seg; ++s) {
+    const SegDesc sd = a.segs[s];
+    if (sd.mask && !sd.mask[t]) continue;
+    const double ch = chrom_factor(sd.freqf, nu, sd.idx);
+    const double* w = sd.w + (int64_t)p * sd.w_pstride;
+    const double* cs = cbase + (int64_t)sd.col0 * a.R_pad;
+    double accs = 0.0;
+    for (int k = 0; k < sd.nm; ++k) {
+      double sn, cn;
+      sincos(w[k] * toa, &sn, &cn);
+      accs = fma(cs[(int64_t)(2 * k) * a.R_pad], cn, accs);
+      accs = fma(cs[(int64_t)(2 * k + 1) * a.R_pad], sn, accs);
+    }
+    acc = fma(ch, accs, acc);
+  }
+  double* o = a.out + (int64_t)r * a.ldo + t;
+  *o = a.accumulate ? *o + acc : acc;
+}
+
+// ----------------------------------------------------------------------------- k_synth_mfma
+// out^T tile [realizations x TOAs] = A [realizations x K] * B [K x TOAs] on
+// v_mfma_f64_16x16x4_f64, where A = coefficients (read from L2) and B = chromatic Fourier basis
+// generated in registers: lane l owns TOA (l & 15) and basis column (l >> 4) of each 4-column
+// K-step (cos m, sin m, cos m+1, sin m+1). On harmonic grids the lane's phasor
+// ch * exp(i w_m t) is advanced two modes per K-step by one complex multiply with
+// exp(i 2 w_0 t), and re-anchored to an exact sincos every `anchor` K-steps.
+// Fragment maps (cdna_hip_programming.md §3): A[i = l&15][k = l>>4], B[k = l>>4][j = l&15],
+// D: col = l&15 (TOA), row = (l>>4) + 4*reg (realization).
+template <int WR, int WT>
+__global__ __launch_bounds__(256, 2) void k_synth_mfma(SynthArgs a, const int4* __restrict__ tiles) {
+  const int4 tl = tiles[blockIdx.x];
+  const int p = tl.x;
+  if (p < 0) return;
+  const int wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int lr = lane & 15;
+  const int lg = lane >> 4;
+  const int64_t base = a.offs[p];
+  const int np_ = (int)(a.offs[p + 1] - base);
+  const int tw0 = tl.y + wave * WT * 16;
+  const int r0 = tl.z;
+  if (tw0 >= np_) return;  // whole wave past the pulsar's last TOA (no cross-wave sync below)
+
+  double t[WT], nuv[WT];
+  int tc[WT];
+#pragma unroll
+  for (int f = 0; f < WT; ++f) {
+    const int tloc = tw0 + f * 16 + lr;
+    tc[f] = tloc < np_ ? tloc : np_ - 1;
+    t[f] = a.toas[base + tc[f]];
+    nuv[f] = a.nu[base + tc[f]];
+  }
+  d4 acc[WR][WT];
+#pragma unroll
+  for (int i = 0; i < WR; ++i)
+#pragma unroll
+    for (int f = 0; f < WT; ++f) acc[i][f] = d4{0.0, 0.0, 0.0, 0.0};
+
+  const int moff = lg >> 1;
+  const bool is_sin = (lg & 1) != 0;
+  const double* cp = a.coef + (int64_t)p * a.K * a.R_pad + r0 + lr;
+
+  for (int s = 0; s < a.n_seg; ++s) {
+    const SegDesc sd = a.segs[s];
+    const double* w = sd.w + (int64_t)p * sd.w_pstride;
+    double ch[WT];
+#pragma unroll
+    for (int f = 0; f < WT; ++f) {
+      ch[f] = chrom_factor(sd.freqf, nuv[f], sd.idx);
+      if (sd.mask && !sd.mask[base + tc[f]]) ch[f] = 0.0;
+    }
+    const bool harm = sd.harmonic != 0;
+    const int anchor = harm ? a.anchor : 1;
+    double rr[WT], ri[WT], zr[WT], zi[WT];
+    if (harm) {
+      const double dw = 2.0 * w[0];
+#pragma unroll
+      for (int f = 0; f < WT; ++f) sincos(dw * t[f], &ri[f], &rr[f]);
+    }
+    const double* cs = cp + (int64_t)(sd.col0 + lg) * a.R_pad;
+    const int nsteps = sd.nm >> 1;
+    for (int j = 0; j < nsteps; ++j) {
+      double av[WR];
+      const double* cj = cs + (int64_t)(4 * j) * a.R_pad;
+#pragma unroll
+      for (int i = 0; i < WR; ++i) av[i] = cj[i * 16];
+      if (j % anchor == 0) {
+        const double wk = w[2 * j + moff];
+#pragma unroll
+        for (int f = 0; f < WT; ++f) {
+          double sn, cn;
+          sincos(wk * t[f], &sn, &cn);
+          zr[f] = ch[f] * cn;
+          zi[f] = ch[f] * sn;
+        }
+      } else {
+#pragma unroll
+        for (int f = 0; f < WT; ++f) {
+          const double nr = fma(zr[f], rr[f], -zi[f] * ri[f]);
+          const double ni = fma(zr[f], ri[f], zi[f] * rr[f]);
+          zr[f] = nr;
+          zi[f] = ni;
+        }
+      }
+#pragma unroll
+      for (int f = 0; f < WT; ++f) {
+        const double b = is_sin ? zi[f] : zr[f];
+#pragma unroll
+        for (int i = 0; i < WR; ++i) acc[i][f] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[i], b, acc[i][f], 0, 0, 0);
+      }
+    }
+  }
+
+#pragma unroll
+  for (int i = 0; i < WR; ++i) {
+#pragma unroll
+    for (int f = 0; f < WT; ++f) {
+      const int tloc = tw0 + f * 16 + lr;
+      if (tloc >= np_) continue;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int r = r0 + i * 16 + lg + 4 * g;
+        if (r < a.n_real) {
+          double* o = a.out + (int64_t)r * a.ldo + base + tloc;
+          *o = a.accumulate ? *o + acc[i][f][g] : acc[i][f][g];
+        }
+      }
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------- k_white
+// grid (ceil(n_toa/256), n_real). out[r][t] += sigma[t] z(t, r) + ecorr[b(t)] zb(b(t), r).
+__global__ __launch_bounds__(256) void k_white(const double* __restrict__ sigma,
+                                               const int32_t* __restrict__ block_of,
+                                               const double* __restrict__ esig, const double* __restrict__ z,
+                                               const double* __restrict__ zb, double* __restrict__ out,
+                                               int64_t ldo, int64_t n_toa, int64_t real0, uint32_t k0,
+                                               uint32_t k1) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int r = blockIdx.y;
+  if (t >= n_toa) return;
+  double v = 0.0;
+  if (sigma) {
+    double zt;
+    if (z) {
+      zt = z[(int64_t)r * n_toa + t];
+    } else {
+      const u32x4 c = {(uint32_t)(t >> 1), kWhitePsrWord, kWhiteStream, (uint32_t)(real0 + r)};
+      double z0, z1;
+      box_muller(philox4x32_10(c, k0, k1), z0, z1);
+      zt = (t & 1) ? z1 : z0;
+    }
+    v = sigma[t] * zt;
+  }
+  if (block_of) {
+    const int b = block_of[t];
+    if (b >= 0) {
+      double zbv;
+      if (zb) {
+        zbv = zb[b];
+      } else {
+        const u32x4 c = {(uint32_t)(b >> 1), kWhitePsrWord, kEcorrStream, (uint32_t)(real0 + r)};
+        double z0, z1;
+        box_muller(philox4x32_10(c, k0, k1), z0, z1);
+        zbv = (b & 1) ? z1 : z0;
+      }
+      v = fma(esig[b], zbv, v);
+    }
+  }
+  out[(int64_t)r * ldo + t] += v;
+}
+
+// ----------------------------------------------------------------------------- k_checksums
+__global__ __launch_bounds__(256) void k_checksums(const double* __restrict__ out, int64_t ldo, int64_t n_toa,
+                                                   double* __restrict__ sums) {
+  __shared__ double s1[256], s2[256];
+  const int r = blockIdx.x;
+  double a = 0.0, b = 0.0;
+  for (int64_t t = threadIdx.x; t < n_toa; t += 256) {
+    const double v = out[(int64_t)r * ldo + t];
+    a += v;
+    b = fma(v, v, b);
+  }
+  s1[threadIdx.x] = a;
+  s2[threadIdx.x] = b;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) {
+      s1[threadIdx.x] += s1[threadIdx.x + w];
+      s2[threadIdx.x] += s2[threadIdx.x + w];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    sums[2 * r] = s1[0];
+    sums[2 * r + 1] = s2[0];
+  }
+}
+
+__global__ void k_philox(int64_t n, const uint32_t* __restrict__ ctr, uint32_t k0, uint32_t k1,
+                         uint32_t* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const u32x4 c = {ctr[4 * i], ctr[4 * i + 1], ctr[4 * i + 2], ctr[4 * i + 3]};
+  const u32x4 v = philox4x32_10(c, k0, k1);
+  out[4 * i] = v.x;
+  out[4 * i + 1] = v.y;
+  out[4 * i + 2] = v.z;
+  out[4 * i + 3] = v.w;
+}
+
+// ----------------------------------------------------------------------------- launchers
+
+hipError_t launch_gen(hipStream_t st, const SegDesc& sd, int32_t seg_id, int32_t P, int32_t n_real,
+                      int32_t R_pad, int64_t real0, uint32_t k0, uint32_t k1, const double* zin,
+                      int32_t zin_nseg, int32_t zin_nm, double* coef, int32_t K, double* zbuf) {
+  dim3 grid((R_pad + 255) / 256, sd.nm, P);
+  hipLaunchKernelGGL(k_gen, grid, dim3(256), 0, st, sd, seg_id, P, n_real, R_pad, real0, k0, k1, zin,
+                     zin_nseg, zin_nm, coef, K, zbuf);
+  return hipGetLastError();
+}
+
+hipError_t launch_mix(hipStream_t st, const SegDesc& sd, int32_t P, int32_t R_pad, const double* zbuf,
+                      double* coef, int32_t K, double* x_out) {
+  const int64_t M = (int64_t)2 * sd.nm * R_pad;
+  dim3 grid((unsigned)((M + 255) / 256), (P + MIX_PT - 1) / MIX_PT);
+  hipLaunchKernelGGL(k_mix, grid, dim3(256), 0, st, sd.L, sd.amp, P, M, R_pad, zbuf, coef, K, sd.col0,
+                     x_out);
+  return hipGetLastError();
+}
+
+hipError_t launch_synth_direct(hipStream_t st, const SynthArgs& a) {
+  dim3 grid((unsigned)((a.n_toa + 255) / 256), a.n_real);
+  hipLaunchKernelGGL(k_synth_direct, grid, dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_synth_mfma(hipStream_t st, const SynthArgs& a, const int4* tiles, int32_t n_tiles) {
+  hipLaunchKernelGGL((k_synth_mfma<kWR, kWT>), dim3(n_tiles), dim3(kWaves * 64), 0, st, a, tiles);
+  return hipGetLastError();
+}
+
+hipError_t launch_white(hipStream_t st, const double* sigma, const int32_t* block_of, const double* esig,
+                        const double* z, const double* zb, double* out, int64_t ldo, int64_t n_toa,
+                        int32_t n_real, int64_t real0, uint32_t k0, uint32_t k1) {
+  dim3 grid((unsigned)((n_toa + 255) / 256), n_real);
+  hipLaunchKernelGGL(k_white, grid, dim3(256), 0, st, sigma, block_of, esig, z, zb, out, ldo, n_toa, real0,
+                     k0, k1);
+  return hipGetLastError();
+}
+
+hipError_t launch_checksums(hipStream_t st, const double* out, int64_t ldo, int64_t n_toa, int32_t n_real,
+                            double* sums) {
+  hipLaunchKernelGGL(k_checksums, dim3(n_real), dim3(256), 0, st, out, ldo, n_toa, sums);
+  return hipGetLastError();
+}
+
+hipError_t launch_philox(hipStream_t st, int64_t n, const uint32_t* ctr, uint32_t k0, uint32_t k1,
+                         uint32_t* out) {
+  hipLaunchKernelGGL(k_philox, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, n, ctr, k0, k1, out);
+  return hipGetLastError();
+}
+
+}  // namespace fpta

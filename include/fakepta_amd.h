@@ -1,0 +1,160 @@
+/*
+ * fakepta_amd.h — C-ABI of libfakepta_amd.so, the MI355X (gfx950) Fourier-basis
+ * Gaussian-process residual synthesis for pulsar-timing arrays.
+ *
+ * The reference (mfalxa/fakepta) has no FFI: its hot path is numpy loops inside
+ * Python methods. Each entry point below names the reference code it replaces;
+ * the Python host layer (fakepta_amd/fake_pta.py, correlated_noises.py, batch.py)
+ * binds them through ctypes (fakepta_amd/_capi.py) behind the reference's own
+ * method signatures. INTEGRATION.md shows the binding.
+ *
+ * Conventions
+ *   - Plain pointers + sizes, no torch types. Host buffers are owned by the caller;
+ *     the library copies inputs to device buffers owned by the context.
+ *   - Every call returns 0 on success or a negative FPTA_E* code; the message is
+ *     available from fpta_last_error(ctx) (or fpta_last_error(NULL) for calls
+ *     that failed before a context existed). The library never aborts or exits.
+ *   - A context owns one device and one HIP stream and is single-threaded; use
+ *     one context per GPU (one process per GPU for multi-GPU).
+ *   - All arithmetic is IEEE fp64.
+ *   - Angular frequencies: the library computes the phase as (2*pi*f_k) * t with
+ *     the same operation order as fakepta/fake_pta.py:386, so drop-in results
+ *     match the numpy reference to rounding.
+ */
+#ifndef FAKEPTA_AMD_H
+#define FAKEPTA_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FPTA_OK 0
+#define FPTA_EINVAL (-22)   /* bad argument / shape */
+#define FPTA_ENOMEM (-12)   /* device allocation failed */
+#define FPTA_EDEVICE (-19)  /* no device / HIP runtime error */
+#define FPTA_ESTATE (-77)   /* call out of order (e.g. synth before set_toas) */
+
+typedef struct fpta_ctx fpta_ctx;
+
+/* ------------------------------------------------------------------ lifetime */
+int fpta_version(void);
+int fpta_create(int device, fpta_ctx** out);
+int fpta_destroy(fpta_ctx* ctx);
+const char* fpta_last_error(const fpta_ctx* ctx);
+int fpta_device_count(int* n);
+
+/* ------------------------------------------------------------------ drop-in, one realization
+ * These replace the per-call numpy loops of the reference; the host keeps the
+ * reference's RNG draws (np.random legacy stream) and bookkeeping, so a seeded
+ * script produces the same residuals.
+ */
+
+/* Replaces fakepta/fake_pta.py:385-387 (Pulsar.add_time_correlated_noise hot loop)
+ * and fakepta/fake_pta.py:538-554 (Pulsar.reconstruct_signal GP branches).
+ *   residuals[t] += sign * sum_s m_s(t) (freqf_s/nu_t)^idx_s *
+ *                   sum_k ( ccos[k] cos(2 pi f[k] t) + csin[k] sin(2 pi f[k] t) )
+ * Segments s are concatenated: seg_nmodes[n_seg]; f/ccos/csin hold sum(seg_nmodes)
+ * values. ccos = sqrt(df)*coeffs[0::2] when injecting, df*fourier[0] when reconstructing.
+ * mask: NULL, or uint8 [n_seg][n_toa] (1 = TOA belongs to the backend of that segment).
+ * residuals: host fp64 [n_toa], read and written. */
+int fpta_gp_accumulate(fpta_ctx* ctx, int64_t n_toa, const double* toas, const double* nu,
+                       int32_t n_seg, const int32_t* seg_nmodes, const double* f,
+                       const double* ccos, const double* csin, const double* seg_idx,
+                       const double* seg_freqf, const uint8_t* mask, double sign,
+                       double* residuals);
+
+/* Replaces fakepta/correlated_noises.py:146-160 (add_common_correlated_noise hot loop).
+ * n_psr pulsars, CSR offsets offs[n_psr+1] into toas/nu (seconds / MHz).
+ * For mode k: x_sin = L z[k][0], x_cos = L z[k][1] (z in the reference's draw order,
+ * [n_modes][2][n_psr], sin vector drawn first), L = [n_psr][n_psr] row-major factor with
+ * L L^T = ORF (for exact reference parity pass the transpose of numpy's SVD factor).
+ *   residuals[t in p] += (freqf/nu_t)^idx * sum_k amp[k] ( x_cos[p] cos(2 pi f_k t)
+ *                                                        + x_sin[p] sin(2 pi f_k t) )
+ * with amp[k] = sqrt(df_k) * sqrt(psd_k) (the reference's df**0.5 * coeffs[2k]; cos and sin
+ * share it because coeffs = sqrt(repeat(psd, 2)), correlated_noises.py:146-147).
+ * x_out (optional, may be NULL): [n_modes][2][n_psr] mixed draws (cos, sin) for the
+ * host's signal_model bookkeeping (correlated_noises.py:157-158). */
+int fpta_common_accumulate(fpta_ctx* ctx, int32_t n_psr, const int64_t* offs, const double* toas,
+                           const double* nu, int32_t n_modes, const double* f, const double* amp,
+                           double idx, double freqf, const double* L,
+                           const double* z, double* residuals, double* x_out);
+
+/* Replaces fakepta/fake_pta.py:201-230 (add_white_noise), with ECORR fixed (defects D1/D2):
+ *   residuals[t] += sigma[t] * z[t]  +  sum over blocks b containing t: ecorr_sigma[b] * zb[b]
+ * Blocks are CSR: block_offs[n_blocks+1] into block_idx (TOA indices, any order).
+ * n_blocks may be 0 (then block_* / ecorr_sigma / zb may be NULL). */
+int fpta_white_accumulate(fpta_ctx* ctx, int64_t n_toa, const double* sigma, const double* z,
+                          int64_t n_blocks, const int64_t* block_offs, const int64_t* block_idx,
+                          const double* ecorr_sigma, const double* zb, double* residuals);
+
+/* ------------------------------------------------------------------ batched realizations
+ * Many independent realizations of the whole array on device (north-star steps 1-4):
+ * Philox4x32-10 draws -> ORF mixing -> fused basis/contraction -> white/ECORR.
+ * Draw streams (invariant to batching and to the number of GPUs):
+ *   GP   : ctr = (mode, pulsar, segment, realization), key = seed -> (z_cos, z_sin)
+ *   white: ctr = (toa>>1, 0xFFFFFFFF, 0xFFFFFFF0, realization), pick [toa&1]
+ *   ECORR: ctr = (block>>1, 0xFFFFFFFF, 0xFFFFFFF1, realization), pick [block&1]
+ * Replaces the Python loop of fakepta/fake_pta.py:648-668 + correlated_noises.py:153-160
+ * when many realizations of one array are needed. */
+
+/* Array layout: CSR offsets [n_psr+1], toas [s], nu [MHz]. Clears previously added signals. */
+int fpta_batch_set_toas(fpta_ctx* ctx, int32_t n_psr, const int64_t* offs, const double* toas,
+                        const double* nu);
+/* kind 0 = per-pulsar GP: f, amp are [n_psr][n_modes] (amp 0 disables a pulsar);
+ * kind 1 = common GP:    f, amp are [n_modes], L is [n_psr][n_psr] (x = L z).
+ * amp = sqrt(psd * df). mask: NULL or uint8 [n_toa_total]. Returns the segment id (>= 0). */
+int fpta_batch_add_signal(fpta_ctx* ctx, int32_t kind, int32_t n_modes, const double* f,
+                          const double* amp, double idx, double freqf, const double* L,
+                          const uint8_t* mask);
+/* White noise sigma [n_toa_total] (NULL disables) and ECORR blocks (CSR over global TOA
+ * indices, ecorr_sigma [n_blocks]; n_blocks 0 disables). */
+int fpta_batch_set_white(fpta_ctx* ctx, const double* sigma, int64_t n_blocks,
+                         const int64_t* block_offs, const int64_t* block_idx,
+                         const double* ecorr_sigma);
+int fpta_batch_clear_signals(fpta_ctx* ctx);
+/* Synthesize realizations real0 .. real0+n_real-1 into the context's device buffer
+ * [n_real][n_toa_total]. If out != NULL the result is also copied to host memory
+ * (row-major, same shape). coeffs_out: NULL or host [n_psr][K][n_real] coefficient dump
+ * (K = fpta_batch_info column count) for validation. */
+int fpta_batch_synth(fpta_ctx* ctx, uint64_t seed, int64_t real0, int32_t n_real, double* out,
+                     double* coeffs_out);
+/* Validation mode: same as fpta_batch_synth but the standard normals come from the host:
+ * z [n_real][n_seg][n_psr][n_modes_max][2] (cos, sin); white/ECORR are not added. */
+int fpta_batch_synth_from_z(fpta_ctx* ctx, int32_t n_real, int32_t n_modes_max, const double* z,
+                            double* out);
+/* Device pointer of the last synthesized block and its leading dimension (n_toa_total). */
+int fpta_batch_device_out(fpta_ctx* ctx, double** dptr, int64_t* ld, int32_t* n_real);
+/* Per-realization sum and sum of squares of the last block, computed on device
+ * (deterministic order). sums: host [n_real][2]. */
+int fpta_batch_checksums(fpta_ctx* ctx, double* sums);
+/* info[0]=n_psr info[1]=n_toa_total info[2]=n_seg info[3]=K columns info[4]=max toas/pulsar */
+int fpta_batch_info(fpta_ctx* ctx, int64_t* info);
+
+/* ------------------------------------------------------------------ tuning / profiling */
+#define FPTA_OPT_SYNTH_PATH 1     /* 0 auto, 1 force direct (sincos per basis element), 2 force MFMA */
+#define FPTA_OPT_MFMA_MIN_REAL 2  /* auto: MFMA path when n_real >= this (default 16) */
+#define FPTA_OPT_PROFILE 3        /* 1: time every batch kernel with HIP events on the ctx stream */
+#define FPTA_OPT_ANCHOR 4         /* harmonic recurrence re-anchor interval in K-steps (default 8) */
+int fpta_set_option(fpta_ctx* ctx, int32_t key, int64_t value);
+/* Kernel ids for fpta_kernel_stats */
+#define FPTA_K_GEN 0
+#define FPTA_K_MIX 1
+#define FPTA_K_SYNTH 2
+#define FPTA_K_WHITE 3
+#define FPTA_K_N 4
+/* Accumulated launches and HIP-event milliseconds of kernel `which` since the last reset. */
+int fpta_kernel_stats(fpta_ctx* ctx, int32_t which, int64_t* count, double* total_ms);
+int fpta_reset_stats(fpta_ctx* ctx);
+int fpta_synchronize(fpta_ctx* ctx);
+
+/* ------------------------------------------------------------------ test hooks */
+/* Philox4x32-10 on device: ctr [n][4], key [2] -> out [n][4]. */
+int fpta_debug_philox(fpta_ctx* ctx, int64_t n, const uint32_t* ctr, const uint32_t* key,
+                      uint32_t* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FAKEPTA_AMD_H */

@@ -1,0 +1,42 @@
+"""Shared helpers for the GPU parity tests: random array layouts and oracle conversion."""
+import numpy as np
+
+from oracle import fakepta_oracle as O
+
+
+def oracle_segments(sim):
+    """BatchSimulator.segments -> oracle Segment list (same layout and semantics)."""
+    return [O.Segment(s["kind"], (2.0 * np.pi) * s["f"], s["amp"], idx=s["idx"], freqf=s["freqf"], L=s["L"],
+                      mask=s["mask"]) for s in sim.segments]
+
+
+def random_layout(rng, P, n_range=(40, 300), t_max=3.2e8, ragged=True):
+    if ragged:
+        n = rng.integers(n_range[0], n_range[1], size=P)
+    else:
+        n = np.full(P, n_range[1])
+    offs = np.concatenate([[0], np.cumsum(n)]).astype(np.int64)
+    toas = np.concatenate([np.sort(rng.uniform(0.05 * t_max, t_max, k)) for k in n])
+    nu = np.abs(rng.choice([1400.0, 800.0, 2500.0], size=offs[-1]) + rng.normal(0, 10, offs[-1]))
+    return offs, toas, nu
+
+
+def per_psr_signal(rng, offs, toas, n_modes, log10_A=-13.5, gamma=3.0):
+    P = len(offs) - 1
+    T = np.maximum([np.ptp(toas[offs[i]:offs[i + 1]]) for i in range(P)], 1e7)
+    f = np.arange(1, n_modes + 1)[None, :] / T[:, None]
+    df = np.diff(np.concatenate([np.zeros((P, 1)), f], axis=1), axis=1)
+    la = rng.uniform(log10_A - 1, log10_A + 0.5, size=P)[:, None]
+    amp = np.sqrt(O.powerlaw(f, la, gamma) * df)
+    return f, amp
+
+
+def common_signal(rng, offs, toas, n_modes, log10_A=-14.5, gamma=13 / 3, orf="hd", pos=None):
+    P = len(offs) - 1
+    f = np.arange(1, n_modes + 1) / np.ptp(toas)
+    amp = np.sqrt(O.powerlaw(f, log10_A, gamma) * O.delta_f(f))
+    if pos is None:
+        v = rng.normal(size=(P, 3))
+        pos = v / np.linalg.norm(v, axis=1)[:, None]
+    L = O.mvn_factor(O.ORFS[orf](pos))
+    return f, amp, L, pos

@@ -1,0 +1,335 @@
+"""Parity of the HIP path (through the C-ABI) against the CPU oracle and the reference's golden
+vectors. Run on an MI355X: python -m pytest tests -m gpu.
+
+Tolerance: relative L2 <= 1e-10 and max-abs <= 1e-10 * max|ref| (fp64),
+unless a test states otherwise (bit-exact for Philox words and for batch-split invariance).
+"""
+import zlib
+
+import numpy as np
+import pytest
+
+from oracle import fakepta_oracle as O
+from tests.conftest import assert_parity
+from tests.helpers import common_signal, oracle_segments, per_psr_signal, random_layout
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-10
+
+
+@pytest.fixture(scope="module")
+def capi():
+    from fakepta_amd import _capi
+    return _capi
+
+
+@pytest.fixture(scope="module")
+def ctx(capi):
+    c = capi.Context(0)
+    yield c
+    c.close()
+
+
+# ----------------------------------------------------------------------------- RNG
+def test_philox_device_bit_exact(ctx):
+    kat = np.array([[0, 0, 0, 0], [0xffffffff] * 4, [0x243f6a88, 0x85a308d3, 0x13198a2e, 0x03707344]], np.uint32)
+    keys = [(0, 0), (0xffffffff, 0xffffffff), (0xa4093822, 0x299f31d0)]
+    want = [(0x6627e8d5, 0xe169c58d, 0xbc57ac4c, 0x9b00dbd8), (0x408f276d, 0x41c83b0e, 0xa20bc7c6, 0x6d5451fd),
+            (0xd16cfe09, 0x94fdcceb, 0x5001e420, 0x24126ea1)]
+    for c, k, w in zip(kat, keys, want):
+        assert tuple(int(x) for x in ctx.debug_philox(c[None], np.array(k, np.uint32))[0]) == w
+    rng = np.random.default_rng(0)
+    ctr = rng.integers(0, 2 ** 32, size=(20000, 4), dtype=np.uint64).astype(np.uint32)
+    key = np.array([123456789, 987654321], np.uint32)
+    np.testing.assert_array_equal(ctx.debug_philox(ctr, key), O.philox4x32_10(ctr, key))
+
+
+# ----------------------------------------------------------------------------- drop-in kernels vs fixtures
+@pytest.mark.parametrize("lab", ["rn", "dm", "sv"])
+def test_gp_accumulate_vs_reference(ctx, golden, lab):
+    g = golden("g2_single_psr.npz")
+    f, psd, z, idx = g[f"{lab}_f"], g[f"{lab}_psd"], g[f"{lab}_z"], float(g[f"{lab}_idx"])
+    c = O.gp_coeffs_from_z(psd, z)
+    sq = O.delta_f(f) ** 0.5
+    r = np.zeros(len(g["toas"]))
+    ctx.gp_accumulate(g["toas"], g["freqs"], [(f, sq * c[0::2], sq * c[1::2], idx, 1400.0)], r)
+    assert_parity(r, g[f"{lab}_delta"], 1e-12)
+    rec = np.zeros_like(r)
+    df = O.delta_f(f)
+    ctx.gp_accumulate(g["toas"], g["freqs"], [(f, df * g[f"{lab}_fourier"][0], df * g[f"{lab}_fourier"][1], idx,
+                                               1400.0)], rec)
+    assert_parity(rec, g[f"{lab}_reconstruct"], 1e-12)
+
+
+def test_dropin_single_pulsar_replay(golden):
+    """The reference's own call sequence (tools/gen_golden.py gen_g2) through fakepta_amd."""
+    from fakepta_amd import fake_pta as fp
+    g = golden("g2_single_psr.npz")
+    rng = np.random.default_rng(7)
+    yr = 365.25 * 24 * 3600
+    keep = rng.random(330) < 0.75
+    cadence = 12.3 * 24 * 3600
+    epochs = 0.35 * yr + np.arange(1, 331)[keep] * cadence
+    np.random.seed(11)
+    psr = fp.Pulsar(epochs, 3e-7, 1.1, 4.2, pdist=(1.0, 0.2), freqs=[1400], backends=["A.1400", "B.800"],
+                    custom_model={"RN": 30, "DM": 100, "Sv": 30})
+    for b in psr.backends:
+        psr.noisedict[f"{psr.name}_{b}_efac"] = {"A.1400": 1.3, "B.800": 0.8}[b]
+        psr.noisedict[f"{psr.name}_{b}_log10_tnequad"] = {"A.1400": -6.5, "B.800": -7.2}[b]
+    for lab, call in (("rn", lambda: psr.add_red_noise(spectrum="powerlaw", log10_A=-13.4, gamma=3.3)),
+                      ("dm", lambda: psr.add_dm_noise(spectrum="powerlaw", log10_A=-13.1, gamma=2.5)),
+                      ("sv", lambda: psr.add_chromatic_noise(spectrum="powerlaw", log10_A=-13.6, gamma=2.0))):
+        before = psr.residuals.copy()
+        call()
+        assert_parity(psr.residuals - before, g[f"{lab}_delta"], 1e-11)
+    for sig, lab in (("red_noise", "rn"), ("dm_gp", "dm"), ("chrom_gp", "sv")):
+        np.testing.assert_allclose(psr.signal_model[sig]["fourier"], g[f"{lab}_fourier"], rtol=1e-15)
+        assert_parity(psr.reconstruct_signal([sig]), g[f"{lab}_reconstruct"], 1e-12)
+    assert_parity(psr.residuals, g["total_after_gp"], 1e-12)
+    assert_parity(psr.reconstruct_signal(), g["reconstruct_all"], 1e-12)
+    psr.add_red_noise(spectrum="powerlaw", log10_A=-13.0, gamma=4.1)  # replace-on-reinject
+    assert_parity(psr.residuals, g["rn2_residuals"], 1e-11)
+    before = psr.residuals.copy()
+    psr.add_white_noise()
+    assert_parity(psr.residuals - before, g["wn_delta"], 1e-10)
+    # remove_signal returns the residuals to white noise + the remaining GPs
+    psr.remove_signal(["red_noise", "dm_gp", "chrom_gp"])
+    assert_parity(psr.residuals, g["wn_delta"], 1e-8)
+
+
+@pytest.mark.parametrize("orf", ["hd", "monopole", "dipole", "curn"])
+def test_dropin_common_vs_reference(golden, orf):
+    from fakepta_amd import correlated_noises as cn
+    from fakepta_amd import fake_pta as fp
+    g = golden("g3_common.npz")
+    np.random.seed(5)
+    psrs = fp.make_fake_array(npsrs=25, Tobs=None, ntoas=120, gaps=True, toaerr=1e-7, isotropic=True,
+                              backends=["A.1400", "B.800"], custom_model={"RN": None, "DM": None, "Sv": None})
+    np.testing.assert_array_equal(np.concatenate([p.toas for p in psrs]), g["toas"])
+    np.testing.assert_array_equal(np.concatenate([p.freqs for p in psrs]), g["freqs"])
+    # replay the fixture generator's ORF loop up to this ORF (the RNG stream is shared)
+    for o in ("hd", "monopole", "dipole", "curn"):
+        for p in psrs:
+            p.make_ideal()
+        cn.add_common_correlated_noise(psrs, orf=o, spectrum="powerlaw", name="gw",
+                                       idx=2.0 if o == "dipole" else 0, components=30, log10_A=-14.2,
+                                       gamma=13 / 3)
+        if o == orf:
+            break
+    fourier = np.array([p.signal_model["gw_common"]["fourier"] for p in psrs])
+    np.testing.assert_allclose(fourier, g[f"{orf}_fourier"], rtol=1e-10, atol=1e-10 * np.abs(fourier).max())
+    assert_parity(np.concatenate([p.residuals for p in psrs]), g[f"{orf}_residuals"], TOL)
+    assert_parity(np.concatenate([p.reconstruct_signal(["gw_common"]) for p in psrs]), g[f"{orf}_reconstruct"],
+                  TOL)
+
+
+@pytest.mark.parametrize("fixture,kwargs", [
+    ("g4_make_fake_array.npz", dict(seed=0, npsrs=25, Tobs=10, ntoas=1000, isotropic=True, gaps=True, toaerr=1e-7,
+                                    backends="NUPPI.1400", custom_model={"RN": 30, "DM": None, "Sv": None})),
+    ("g4b_make_fake_array.npz", dict(seed=1, npsrs=6, Tobs=None, ntoas=None, gaps=True, toaerr=None,
+                                     backends=["A.1400", "B.800"], isotropic=False)),
+])
+def test_make_fake_array_end_to_end(golden, fixture, kwargs):
+    """BASELINE configs[0]: seeded make_fake_array reproduces the reference's residuals."""
+    from fakepta_amd import fake_pta as fp
+    g = golden(fixture)
+    kwargs = dict(kwargs)
+    np.random.seed(kwargs.pop("seed"))
+    psrs = fp.make_fake_array(**kwargs)
+    assert [p.name for p in psrs] == list(g["names"])
+    np.testing.assert_array_equal(np.concatenate([p.toas for p in psrs]), g["toas"])
+    assert_parity(np.concatenate([p.residuals for p in psrs]), g["residuals"], TOL)
+    if "rn_fourier" in g:
+        np.testing.assert_allclose(np.array([p.signal_model["red_noise"]["fourier"] for p in psrs]), g["rn_fourier"],
+                                   rtol=1e-15)
+
+
+def test_white_ecorr_dropin(ctx):
+    rng = np.random.default_rng(3)
+    n = 500
+    sigma = rng.uniform(1e-7, 1e-6, n)
+    z = rng.standard_normal(n)
+    blocks = [np.arange(i, min(i + 4, n)) for i in range(0, n, 4)]
+    es = rng.uniform(1e-8, 1e-7, len(blocks))
+    zb = rng.standard_normal(len(blocks))
+    r = rng.normal(size=n) * 1e-6
+    want = r + sigma * z
+    for b, e, zz in zip(blocks, es, zb):
+        want[b] += e * zz
+    ctx.white_accumulate(sigma, z, r, blocks=blocks, ecorr_sigma=es, zb=zb)
+    assert_parity(r, want, 1e-14)
+
+
+def test_masked_system_noise(ctx):
+    """Backend mask (fake_pta.py:361-368, D9 fixed) and add_system_noise (D3 fixed)."""
+    from fakepta_amd import fake_pta as fp
+    np.random.seed(4)
+    psr = fp.Pulsar(np.linspace(0, 3e8, 200), 1e-7, 0.3, 0.4, backends=["A.1400", "B.800"],
+                    custom_model={"RN": None, "DM": None, "Sv": None})
+    psr.add_system_noise(backend="B.800", components=12, log10_A=-13.0, gamma=3.0)
+    name = "B.800_system_noise_B.800"
+    sm = psr.signal_model[name]
+    m = psr.backend_flags == "B.800"
+    coeffs = np.empty(24)
+    df = O.delta_f(sm["f"])
+    coeffs[0::2], coeffs[1::2] = sm["fourier"][0] * df ** 0.5, sm["fourier"][1] * df ** 0.5
+    want = O.gp_synth_loop(psr.toas, psr.freqs, sm["f"], coeffs, 0.0, mask=m)
+    assert_parity(psr.residuals, want, 1e-12)
+    assert np.all(psr.residuals[~m] == 0)
+    psr.add_system_noise(backend="B.800", components=12, log10_A=-13.0, gamma=3.0)  # replaces, not adds
+    assert_parity(psr.reconstruct_signal([name]), psr.residuals, 1e-12)
+
+
+# ----------------------------------------------------------------------------- batch path vs oracle
+def _build(ctx, rng, P=7, n_range=(20, 260), per_psr=((30, 0.0), (41, 2.0)), common=((30, 0.0),), masked=False,
+           white=False, ecorr=False):
+    offs, toas, nu = random_layout(rng, P, n_range)
+    ctx.batch_set_toas(offs, toas, nu)
+    segs = []
+    for nm, idx in per_psr:
+        f, a = per_psr_signal(rng, offs, toas, nm)
+        mask = None
+        if masked:
+            mask = (rng.random(offs[-1]) < 0.5).astype(np.uint8)
+        ctx.batch_add_signal(0, f, a, idx=idx, mask=mask)
+        segs.append(O.Segment(0, 2 * np.pi * f, a, idx, mask=mask))
+    for nm, idx in common:
+        f, a, L, _ = common_signal(rng, offs, toas, nm)
+        ctx.batch_add_signal(1, f, a, idx=idx, L=L)
+        segs.append(O.Segment(1, 2 * np.pi * f, a, idx, L=L))
+    sigma = blocks = es = block_of = None
+    if white:
+        sigma = rng.uniform(1e-7, 1e-6, offs[-1])
+    if ecorr:
+        starts = np.arange(0, offs[-1], 3)
+        blocks = [np.arange(s, min(s + 2, offs[-1])) for s in starts]
+        es = rng.uniform(1e-8, 1e-7, len(blocks))
+        block_of = -np.ones(offs[-1], dtype=np.int64)
+        for b, q in enumerate(blocks):
+            block_of[q] = b
+    if white or ecorr:
+        ctx.batch_set_white(sigma, blocks, es)
+    return offs, toas, nu, segs, sigma, block_of, es
+
+
+@pytest.mark.parametrize("path", [1, 2])
+@pytest.mark.parametrize("case", ["basic", "masked_odd_modes", "white_ecorr", "common_only", "tiny_pulsars"])
+def test_batch_vs_oracle(ctx, capi, path, case):
+    rng = np.random.default_rng(zlib.crc32(case.encode()))
+    kw = dict(basic={}, masked_odd_modes=dict(per_psr=((7, 4.0), (1, 0.0)), masked=True),
+              white_ecorr=dict(white=True, ecorr=True), common_only=dict(per_psr=(), common=((30, 0.0), (13, 2.0))),
+              tiny_pulsars=dict(P=5, n_range=(1, 18)))[case]
+    offs, toas, nu, segs, sigma, block_of, es = _build(ctx, rng, **kw)
+    ctx.set_option(capi.OPT_SYNTH_PATH, path)
+    try:
+        for real0, R in ((0, 70), (1000003, 3)):
+            got = ctx.batch_synth(99, real0, R)
+            want = O.batch_synth(offs, toas, nu, segs, 99, real0, R, sigma=sigma, block_of=block_of,
+                                 ecorr_sigma=es)
+            assert_parity(got, want, TOL)
+    finally:
+        ctx.set_option(capi.OPT_SYNTH_PATH, 0)
+
+
+def test_batch_from_z_vs_oracle(ctx):
+    rng = np.random.default_rng(11)
+    offs, toas, nu, segs, *_ = _build(ctx, rng)
+    R, nmax = 33, max(s.n_modes for s in segs)
+    z = rng.standard_normal((R, len(segs), len(offs) - 1, nmax, 2))
+    got = ctx.batch_synth_from_z(z)
+    zo = {s: z[:, s, :, :segs[s].n_modes, :] for s in range(len(segs))}
+    want = O.batch_synth(offs, toas, nu, segs, 0, 0, R, z_override=zo)
+    assert_parity(got, want, TOL)
+
+
+@pytest.mark.parametrize("anchor", [1, 3, 8, 64])
+def test_recurrence_anchor_accuracy(ctx, capi, anchor):
+    """The MFMA path's phasor recurrence stays within tolerance for every re-anchor interval,
+    including 100-mode grids on real-MJD-like epochs (t ~ 5e9 s)."""
+    rng = np.random.default_rng(5)
+    offs, toas, nu = random_layout(rng, 4, (100, 300), t_max=1.6e8)
+    toas = toas + 4.5e9
+    ctx.batch_set_toas(offs, toas, nu)
+    f, a = per_psr_signal(rng, offs, toas, 100)
+    ctx.batch_add_signal(0, f, a, idx=2.0)
+    ctx.set_option(capi.OPT_SYNTH_PATH, 2)
+    ctx.set_option(capi.OPT_ANCHOR, anchor)
+    try:
+        got = ctx.batch_synth(5, 0, 64)
+    finally:
+        ctx.set_option(capi.OPT_SYNTH_PATH, 0)
+        ctx.set_option(capi.OPT_ANCHOR, 8)
+    want = O.batch_synth(offs, toas, nu, [O.Segment(0, 2 * np.pi * f, a, 2.0)], 5, 0, 64)
+    assert_parity(got, want, TOL)
+
+
+def test_batch_split_invariance_bitwise(ctx):
+    """Realization r is bit-identical whatever batch it is drawn in (multi-GPU sharding contract)."""
+    rng = np.random.default_rng(8)
+    _build(ctx, rng, P=6, white=True)
+    full = ctx.batch_synth(2024, 0, 200)
+    parts = np.concatenate([ctx.batch_synth(2024, r0, n) for r0, n in ((0, 64), (64, 100), (164, 36))])
+    np.testing.assert_array_equal(full, parts)
+    again = ctx.batch_synth(2024, 0, 200)
+    np.testing.assert_array_equal(full, again)
+
+
+def test_checksums_device(ctx):
+    rng = np.random.default_rng(9)
+    _build(ctx, rng, P=4, white=True)
+    out = ctx.batch_synth(1, 0, 50)
+    s = ctx.batch_checksums()
+    np.testing.assert_allclose(s[:, 0], out.sum(1), rtol=1e-9, atol=1e-12 * np.abs(out).sum(1).max())
+    np.testing.assert_allclose(s[:, 1], (out ** 2).sum(1), rtol=1e-12)
+
+
+def test_errors_are_loud(ctx, capi):
+    with pytest.raises(capi.FptaError):
+        ctx.batch_set_toas(np.array([0, 5, 5]), np.zeros(5), np.ones(5))  # empty pulsar
+    with pytest.raises(capi.FptaError):
+        ctx.set_option(capi.OPT_SYNTH_PATH, 7)
+    with pytest.raises(capi.FptaError):
+        ctx.batch_add_signal(1, np.ones(3), np.ones(3))  # common without ORF factor
+
+
+# ----------------------------------------------------------------------------- C2 at full size
+def test_c2_full_size(ctx):
+    """BASELINE configs[1] shape: 100 psr x 2000 TOAs, RN30 + DM100 + HD30, R = 1024 on device.
+    Size-independent checks: 4 realizations re-synthesized by the oracle from the device's own
+    coefficients; determinism; per-realization checksums."""
+    from fakepta_amd import correlated_noises as cn
+    from fakepta_amd import fake_pta as fp
+    from fakepta_amd.batch import BatchSimulator
+    np.random.seed(0)
+    psrs = fp.make_fake_array(npsrs=100, Tobs=10, ntoas=2000, gaps=False, isotropic=True, toaerr=1e-7,
+                              backends="NUPPI.1400", custom_model={"RN": 30, "DM": 100, "Sv": None})
+    cn.add_common_correlated_noise(psrs, orf="hd", log10_A=-15, gamma=13 / 3)
+    sim = BatchSimulator(psrs, white=False, ctx=ctx)
+    info = ctx.batch_info()
+    assert info["n_toa"] == 200000 and info["K"] == 320
+    out, co = sim.synth(1024, seed=1234, coeffs=True)
+    assert np.all(np.isfinite(out))
+    pick = [0, 1, 511, 1023]
+    segs = oracle_segments(sim)
+    for r in pick:
+        want = np.zeros(sim.n_toa)
+        col = 0
+        for s in segs:
+            for p in range(len(psrs)):
+                sl = slice(sim.offs[p], sim.offs[p + 1])
+                w = s.w[p] if s.kind == 0 else s.w
+                ph = np.outer(sim.toas[sl], w)
+                ch = (s.freqf / sim.freqs[sl]) ** s.idx
+                a = co[p, col:col + 2 * s.n_modes, r]
+                want[sl] += ch * (np.cos(ph) @ a[0::2] + np.sin(ph) @ a[1::2])
+            col += 2 * s.n_modes
+        assert_parity(out[r], want, TOL)
+    # coefficients follow the Philox stream of the oracle
+    z = O.gp_normals(1234, np.array(pick), 17, 0, 30)
+    np.testing.assert_allclose(co[17, 0:60:2, pick].T, sim.segments[0]["amp"][17][None, :] * z[:, :, 0],
+                               rtol=1e-13)
+    s1 = sim.checksums()
+    out2 = sim.synth(1024, seed=1234)
+    np.testing.assert_array_equal(out, out2)
+    np.testing.assert_allclose(s1[:, 1], (out ** 2).sum(1), rtol=1e-12)

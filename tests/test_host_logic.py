@@ -1,0 +1,118 @@
+"""Host-side logic of the drop-in package against the reference's fixtures (CPU only:
+nothing here launches a kernel)."""
+import numpy as np
+import pytest
+
+from fakepta_amd import correlated_noises as cn
+from fakepta_amd import fake_pta as fp
+from fakepta_amd import spectrum as sp
+from tests.conftest import assert_parity
+
+
+def test_psd_registry_matches_reference_names():
+    assert sorted(fp.spec) == ["broken_powerlaw", "powerlaw", "t_process", "t_process_adapt", "turnover",
+                               "turnover_knee"]
+    assert fp.spec_params["powerlaw"] == ["log10_A", "gamma"]
+    assert fp.spec_params["turnover_knee"] == ["log10_A", "gamma", "lfb", "lfk", "kappa", "delta"]
+
+
+def test_psds_bitwise_vs_reference(golden):
+    import json
+    g = golden("g1_psd.npz")
+    for key, params in json.loads(str(g["meta_json"])).items():
+        name, gi, _ = key.split("__")
+        p = {k: (np.array(v) if isinstance(v, list) else v) for k, v in params.items()}
+        np.testing.assert_allclose(getattr(sp, name)(g["grid" + gi[1:]].copy(), **p), g[key], rtol=1e-14)
+
+
+def test_pulsar_construction_rng_parity(golden):
+    """Same np.random draws as the reference constructor: jittered radio frequencies, flags, name."""
+    g = golden("g2_single_psr.npz")
+    rng = np.random.default_rng(7)
+    yr = 365.25 * 24 * 3600
+    keep = rng.random(330) < 0.75
+    cadence = 12.3 * 24 * 3600
+    epochs = 0.35 * yr + np.arange(1, 331)[keep] * cadence
+    np.random.seed(11)
+    psr = fp.Pulsar(epochs, 3e-7, 1.1, 4.2, pdist=(1.0, 0.2), freqs=[1400], backends=["A.1400", "B.800"],
+                    custom_model={"RN": 30, "DM": 100, "Sv": 30})
+    np.testing.assert_array_equal(psr.toas, g["toas"])
+    np.testing.assert_array_equal(psr.freqs, g["freqs"])
+    np.testing.assert_array_equal(psr.backend_flags.astype("U"), g["backend_flags"])
+    assert psr.name == str(g["name"]) and psr.Tspan == g["Tspan"]
+
+
+def test_tutorial_names(golden):
+    """examples/tutorial.ipynb cell 5: names of the 25-pulsar isotropic array."""
+    names = golden("g5_tutorial.json")["names_npsrs25_isotropic"]
+    i = np.arange(25, dtype=float) + 0.5
+    cost = 1 - 2 * i / 25
+    phis = np.mod(2 * np.pi * i / ((1 + 5 ** 0.5) / 2), 2 * np.pi)
+    got = []
+    for c, ph in zip(cost, phis):
+        p = fp.Pulsar.__new__(fp.Pulsar)
+        p.theta, p.phi = np.arccos(c), ph
+        got.append(p.get_psrname())
+    assert got == names
+
+
+def test_g4_names_and_design_matrix(golden):
+    g = golden("g4_make_fake_array.npz")
+    assert len(g["names"]) == 25 and g["Mmat0"].shape[1] == 8
+
+
+def test_quantise_ecorr_verbatim(golden):
+    g = golden("g2_single_psr.npz")
+    p = fp.Pulsar.__new__(fp.Pulsar)
+    p.toas, p.backend_flags = g["q_toas"], g["q_flags"]
+    p.backends = np.unique(p.backend_flags)
+    q = p.quantise_ecorr()
+    assert [len(b) for b in q] == list(g["q_lens"])
+    np.testing.assert_array_equal(np.concatenate(q), g["q_idx"])
+    full = p.ecorr_blocks()
+    assert sorted(np.concatenate(full).tolist()) == list(range(len(p.toas)))
+
+
+@pytest.mark.parametrize("orf", ["hd", "monopole", "dipole", "curn"])
+def test_orfs_and_factor(golden, orf):
+    g = golden("g3_common.npz")
+
+    class P:
+        def __init__(self, pos):
+            self.pos = pos
+    psrs = [P(x) for x in g["pos"]]
+    gam = cn.ORF_FUNCS[orf](psrs)
+    np.testing.assert_allclose(gam, g[f"{orf}_orf"], rtol=1e-14, atol=1e-15)
+    L = cn.orf_factor(gam)
+    np.testing.assert_allclose(L.T, g[f"{orf}_svdM"], atol=1e-13)
+    assert_parity(L @ L.T, gam, 1e-12)
+
+
+def test_mvn_draw_order_equivalence():
+    """numpy's legacy multivariate_normal == standard_normal(P) @ (sqrt(s) vt): the host draws
+    z in that order and the GPU applies L = M^T."""
+    rng_cov = np.random.default_rng(1).normal(size=(7, 7))
+    cov = rng_cov @ rng_cov.T
+    np.random.seed(3)
+    a = np.random.multivariate_normal(np.zeros(7), cov)
+    np.random.seed(3)
+    z = np.random.standard_normal(7)
+    np.testing.assert_allclose(cn.orf_factor(cov) @ z, a, rtol=1e-12, atol=1e-12)
+
+
+def test_noisedict_conventions():
+    p = fp.Pulsar.__new__(fp.Pulsar)
+    p.name, p.backends = "J0000+0000", np.array(["A", "B"])
+    p.init_noisedict(None)
+    assert p.noisedict["J0000+0000_A_efac"] == 1.0 and len(p.noisedict) == 8
+    p.init_noisedict({"J0000+0000_A_efac": 2.0, "J1111+1111_A_efac": 3.0, "red_noise_gamma": 1})
+    assert p.noisedict == {"J0000+0000_A_efac": 2.0}
+    p.init_noisedict({"A_efac": 1.1, "A_log10_tnequad": -7, "B_efac": 1.2, "B_log10_tnequad": -6,
+                      "A_log10_t2equad": -7, "A_log10_ecorr": -8, "red_noise_log10_A": -14,
+                      "red_noise_gamma": 3})
+    nd = p.noisedict
+    assert nd["J0000+0000_B_efac"] == 1.2 and "J0000+0000_B_log10_t2equad" not in nd
+    assert nd["J0000+0000_A_log10_ecorr"] == -8 and nd["J0000+0000_red_noise_gamma"] == 3
+    p.init_noisedict({"efac": 1.5, "log10_tnequad": -6.5})
+    assert p.noisedict == {"J0000+0000_A_efac": 1.5, "J0000+0000_A_log10_tnequad": -6.5,
+                           "J0000+0000_B_efac": 1.5, "J0000+0000_B_log10_tnequad": -6.5}
