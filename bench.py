@@ -28,6 +28,8 @@ sys.path.insert(0, ROOT)
 METRIC = "residual samples/sec (TOA×realization) for 100-psr HD GWB; % FP64 peak"
 FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 matrix (= vector) peak, AMD datasheet (MI355X_MICROARCH.md lists none)
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+SYNTH_KERNELS = {0: ("k_synth_valu_seeded<2,16>", "fp64-valu"), 3: ("k_synth_valu_seeded<2,16>", "fp64-valu"),
+                 2: ("k_synth_mfma<4,2>", "fp64-mfma"), 1: ("k_synth_direct", "fp64-valu")}
 
 
 def parse():
@@ -40,7 +42,7 @@ def parse():
     ap.add_argument("--ntoa", type=int, default=2000)
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--cpu-sample", type=int, default=8, help="realizations timed for the CPU baseline (0: skip)")
-    ap.add_argument("--path", type=int, default=0, help="synthesis path: 0 auto, 1 direct, 2 MFMA")
+    ap.add_argument("--path", type=int, default=0, help="synthesis path: 0 auto, 1 direct, 2 MFMA, 3 VALU")
     ap.add_argument("--anchor", type=int, default=0, help="recurrence re-anchor interval (0: library default)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-derived HBM bytes per synth launch (written by profiles/collect_pmc.py)")
@@ -219,9 +221,14 @@ def main():
                                    "%d realizations/GPU/step, Philox seed %d" % (args.npsr, args.ntoa, R, args.seed),
                        "n_psr": args.npsr, "n_toa_total": info["n_toa"], "K": info["K"], "realizations_per_gpu": R,
                        "parallelism": "realization-sharded x%d" % world},
-            "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+            # compute (FP64) bound: 2K FLOP per 8-byte sample = 80 FLOP/B at K = 320. The peak is the
+            # MI355X FP64 datasheet figure, equal for the vector and matrix pipes; the default kernel
+            # issues v_fma_f64 (DESIGN.md §5 Calibration), the MFMA kernel is --path 2.
+            "roofline": {"bound": "mfma", "pipe": SYNTH_KERNELS[args.path][1], "achieved": achieved,
+                         "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
-                         "kernel": "k_synth_mfma", "flops_per_launch": flops, "avg_launch_ms": synth_avg_s * 1e3,
+                         "kernel": SYNTH_KERNELS[args.path][0], "flops_per_launch": flops,
+                         "avg_launch_ms": synth_avg_s * 1e3,
                          "write_GBps": 8.0 * info["n_toa"] * R / synth_avg_s / 1e9},
             "kernels_ms_per_step": {k: (v[1] / max(v[0], 1)) * (v[0] / max(args.steps, 1)) for k, v in kstats.items()},
             "checksum": float(np.sum(all_sums[..., 1])),

@@ -7,6 +7,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -67,10 +68,13 @@ struct Layout {
   DevBuf segdesc;
   int32_t K = 0;
   bool dirty = true;
+  // recurrence seeds [n_seg][n_toa] (double4), valid when every segment is harmonic
+  DevBuf seeds;
+  bool all_harmonic = false;
   // MFMA tile table cache
   DevBuf tiles;
   int32_t n_tiles = 0;
-  int32_t tiles_R = -1;
+  int64_t tiles_R = -1;
   ~Layout() { clear_signals(); }
   void clear_signals() {
     for (Seg* s : segs) delete s;
@@ -100,7 +104,8 @@ struct fpta_ctx {
   int synth_path = 0;
   int mfma_min_real = 16;
   int profile = 0;
-  int anchor = 8;
+  int anchor = 0;  // 0: phasor recurrence anchored once per segment
+  int valu_variant = 1;  // seeded (MT 2, NT 16): fastest on C2 (profiles/r01_sweep_*.txt)
   // profiling
   struct Pending {
     int which;
@@ -125,10 +130,22 @@ int hip_fail(fpta_ctx* c, hipError_t e, const char* what) {
   return fail(c, e == hipErrorOutOfMemory ? FPTA_ENOMEM : FPTA_EDEVICE, m);
 }
 
-#define HIPCHK(ctx, expr, what)                  \
-  do {                                           \
-    hipError_t _e = (expr);                      \
-    if (_e != hipSuccess) return hip_fail(ctx, _e, what); \
+// FPTA_DEBUG_SYNC=1: synchronize after every launch so a device fault is reported by the launch
+// that caused it (debugging aid; off by default).
+bool debug_sync() {
+  static const bool on = [] {
+    const char* e = std::getenv("FPTA_DEBUG_SYNC");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
+#define HIPCHK(ctx, expr, what)                                                           \
+  do {                                                                                    \
+    hipError_t _e = (expr);                                                               \
+    if (_e == hipSuccess && debug_sync() && std::strstr(what, "launch"))                  \
+      _e = hipStreamSynchronize((ctx)->stream);                                           \
+    if (_e != hipSuccess) return hip_fail(ctx, _e, what);                                 \
   } while (0)
 
 hipEvent_t get_event(fpta_ctx* c) {
@@ -271,9 +288,21 @@ int layout_add_signal(fpta_ctx* c, Layout& L, int32_t kind, int32_t nm, const do
 int layout_finalize(fpta_ctx* c, Layout& L) {
   if (!L.dirty) return FPTA_OK;
   std::vector<SegDesc> d;
-  for (Seg* s : L.segs) d.push_back(s->d);
+  bool harm = !L.segs.empty();
+  for (Seg* s : L.segs) {
+    d.push_back(s->d);
+    harm = harm && s->d.harmonic;
+  }
   int rc = upload(c, L.segdesc, d.data(), sizeof(SegDesc) * d.size(), "segdesc");
   if (rc) return rc;
+  L.all_harmonic = harm;
+  if (harm) {
+    HIPCHK(c, L.seeds.ensure(sizeof(double4) * (size_t)L.n_toa * d.size()), "seeds alloc");
+    HIPCHK(c,
+           launch_seeds(c->stream, L.segdesc.as<SegDesc>(), (int32_t)d.size(), L.psr_of.as<int32_t>(),
+                        L.toas.as<double>(), L.nu.as<double>(), L.n_toa, L.seeds.as<double4>()),
+           "k_seeds launch");
+  }
   HIPCHK(c, hipStreamSynchronize(c->stream), "segdesc sync");
   L.dirty = false;
   return FPTA_OK;
@@ -309,13 +338,14 @@ int run_coefficients(fpta_ctx* c, Layout& L, uint64_t seed, int64_t real0, int32
   return FPTA_OK;
 }
 
-int build_tiles(fpta_ctx* c, Layout& L, int32_t R) {
-  if (L.tiles_R == R) return FPTA_OK;
+int build_tiles(fpta_ctx* c, Layout& L, int32_t R, int32_t tile_toa, int32_t tile_real) {
+  const int64_t key = ((int64_t)tile_toa << 40) ^ ((int64_t)tile_real << 32) ^ (int64_t)R;
+  if (L.tiles_R == key) return FPTA_OK;
   std::vector<int4> t;
   for (int32_t p = 0; p < L.P; ++p) {
     const int64_t np_ = L.h_offs[p + 1] - L.h_offs[p];
-    for (int32_t r0 = 0; r0 < R; r0 += kTileReal)
-      for (int64_t t0 = 0; t0 < np_; t0 += kTileToa) t.push_back(make_int4(p, (int)t0, r0, 0));
+    for (int32_t r0 = 0; r0 < R; r0 += tile_real)
+      for (int64_t t0 = 0; t0 < np_; t0 += tile_toa) t.push_back(make_int4(p, (int)t0, r0, 0));
   }
   // XCD-aware order: workgroups b, b+8, b+16, ... share an XCD's L2 (round-robin dispatch), so give
   // them consecutive tiles (same pulsar and realization tile -> same coefficient block).
@@ -330,7 +360,7 @@ int build_tiles(fpta_ctx* c, Layout& L, int32_t R) {
   if (rc) return rc;
   HIPCHK(c, hipStreamSynchronize(c->stream), "tiles sync");
   L.n_tiles = (int32_t)o.size();
-  L.tiles_R = R;
+  L.tiles_R = key;
   return FPTA_OK;
 }
 
@@ -352,14 +382,39 @@ int run_synth(fpta_ctx* c, Layout& L, int32_t R, int32_t R_pad, double* out, int
   a.ldo = ldo;
   a.n_real = R;
   a.accumulate = accumulate;
-  a.anchor = std::max(1, c->anchor);
-  bool mfma = allow_mfma && (c->synth_path == 2 || (c->synth_path == 0 && R >= c->mfma_min_real));
-  if (c->synth_path == 1) mfma = false;
-  if (mfma) {
-    int rc = build_tiles(c, L, R);
+  a.anchor = c->anchor;
+  // path: 1 direct, 2 MFMA, 3 VALU; auto (0) = VALU for R >= mfma_min_real, direct below
+  int path = c->synth_path;
+  if (path == 0) path = R >= c->mfma_min_real ? 3 : 1;
+  if (!allow_mfma) path = 1;
+  // host-side guards of what the tiled kernels assume (every tile's realization block lies inside
+  // the coefficient padding; the coefficient buffer holds P*K*R_pad values)
+  if (R_pad % kRealPad != 0 || R > R_pad || kRealPad % kTileReal != 0 ||
+      kRealPad % (4 * kValuVariants[c->valu_variant].nt) != 0)
+    return fail(c, FPTA_EINVAL, "synth: realization padding inconsistent with the tile geometry");
+  if (c->coef.cap < sizeof(double) * (size_t)L.P * std::max(L.K, 1) * R_pad)
+    return fail(c, FPTA_ESTATE, "synth: coefficient buffer smaller than P*K*R_pad");
+  if (path == 2) {
+    int rc = build_tiles(c, L, R, kTileToa, kTileReal);
     if (rc) return rc;
     KTimer kt(c, FPTA_K_SYNTH);
     HIPCHK(c, launch_synth_mfma(c->stream, a, L.tiles.as<int4>(), L.n_tiles), "k_synth_mfma launch");
+  } else if (path == 3 && L.all_harmonic && c->anchor == 0) {
+    const ValuVariant v = kSeededVariants[c->valu_variant];
+    int rc = build_tiles(c, L, R, 4 * 64 * v.mt, v.nt);
+    if (rc) return rc;
+    KTimer kt(c, FPTA_K_SYNTH);
+    HIPCHK(c,
+           launch_synth_valu_seeded(c->stream, a, L.tiles.as<int4>(), L.n_tiles, L.seeds.as<double4>(),
+                                    c->valu_variant),
+           "k_synth_valu_seeded launch");
+  } else if (path == 3) {
+    const ValuVariant v = kValuVariants[c->valu_variant];
+    int rc = build_tiles(c, L, R, 64 * v.mt, 4 * v.nt);
+    if (rc) return rc;
+    KTimer kt(c, FPTA_K_SYNTH);
+    HIPCHK(c, launch_synth_valu(c->stream, a, L.tiles.as<int4>(), L.n_tiles, c->valu_variant),
+           "k_synth_valu launch");
   } else {
     if (R > 65535) return fail(c, FPTA_EINVAL, "direct synthesis path: n_real > 65535");
     KTimer kt(c, FPTA_K_SYNTH);
@@ -450,8 +505,12 @@ int fpta_set_option(fpta_ctx* c, int32_t key, int64_t value) {
   if (!c) return fail(nullptr, FPTA_EINVAL, "set_option: null ctx");
   switch (key) {
     case FPTA_OPT_SYNTH_PATH:
-      if (value < 0 || value > 2) return fail(c, FPTA_EINVAL, "synth path must be 0, 1 or 2");
+      if (value < 0 || value > 3) return fail(c, FPTA_EINVAL, "synth path must be 0, 1, 2 or 3");
       c->synth_path = (int)value;
+      return FPTA_OK;
+    case FPTA_OPT_VALU_VARIANT:
+      if (value < 0 || value >= kNumValuVariants) return fail(c, FPTA_EINVAL, "unknown VALU variant");
+      c->valu_variant = (int)value;
       return FPTA_OK;
     case FPTA_OPT_MFMA_MIN_REAL:
       c->mfma_min_real = (int)std::max<int64_t>(1, value);
@@ -460,7 +519,7 @@ int fpta_set_option(fpta_ctx* c, int32_t key, int64_t value) {
       c->profile = value ? 1 : 0;
       return FPTA_OK;
     case FPTA_OPT_ANCHOR:
-      if (value < 1 || value > 1 << 20) return fail(c, FPTA_EINVAL, "anchor must be >= 1");
+      if (value < 0 || value > 1 << 20) return fail(c, FPTA_EINVAL, "anchor must be >= 0");
       c->anchor = (int)value;
       return FPTA_OK;
   }

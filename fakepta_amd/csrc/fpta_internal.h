@@ -45,7 +45,23 @@ constexpr int kWT = 2;                  // 16-TOA fragments per wave
 constexpr int kWaves = 4;               // waves per workgroup
 constexpr int kTileReal = kWR * 16;     // realizations per workgroup
 constexpr int kTileToa = kWaves * kWT * 16;  // TOAs per workgroup
-constexpr int kRealPad = 64;            // R_pad granularity
+constexpr int kRealPad = 128;           // R_pad granularity (multiple of every realization tile)
+
+// VALU fused-kernel variants: (TOAs per lane MT, realizations per wave NT); workgroup tile is
+// 64*MT TOAs x 4*NT realizations.
+struct ValuVariant {
+  int mt, nt;
+};
+constexpr ValuVariant kValuVariants[] = {{2, 16}, {4, 16}, {4, 8}, {2, 8}, {1, 32}, {1, 16}};
+constexpr int kNumValuVariants = sizeof(kValuVariants) / sizeof(kValuVariants[0]);
+// Seeded VALU kernel (harmonic grids): (MT, NT); workgroup tile 256*MT TOAs x NT realizations.
+constexpr ValuVariant kSeededVariants[] = {{1, 16}, {2, 16}, {1, 8}, {2, 8}, {1, 32}, {4, 16}};
+static_assert(sizeof(kSeededVariants) == sizeof(kValuVariants), "one variant index selects both tables");
+
+hipError_t launch_seeds(hipStream_t st, const SegDesc* segs, int32_t n_seg, const int32_t* psr_of,
+                        const double* toas, const double* nu, int64_t n_toa, double4* seeds);
+hipError_t launch_synth_valu_seeded(hipStream_t st, const SynthArgs& a, const int4* tiles, int32_t n_tiles,
+                                    const double4* seeds, int variant);
 
 hipError_t launch_gen(hipStream_t st, const SegDesc& sd, int32_t seg_id, int32_t P, int32_t n_real,
                       int32_t R_pad, int64_t real0, uint32_t k0, uint32_t k1, const double* zin,
@@ -54,6 +70,7 @@ hipError_t launch_mix(hipStream_t st, const SegDesc& sd, int32_t P, int32_t R_pa
                       double* coef, int32_t K, double* x_out);
 hipError_t launch_synth_direct(hipStream_t st, const SynthArgs& a);
 hipError_t launch_synth_mfma(hipStream_t st, const SynthArgs& a, const int4* tiles, int32_t n_tiles);
+hipError_t launch_synth_valu(hipStream_t st, const SynthArgs& a, const int4* tiles, int32_t n_tiles, int variant);
 hipError_t launch_white(hipStream_t st, const double* sigma, const int32_t* block_of, const double* esig,
                         const double* z, const double* zb, double* out, int64_t ldo, int64_t n_toa,
                         int32_t n_real, int64_t real0, uint32_t k0, uint32_t k1);

@@ -197,13 +197,8 @@ __global__ __launch_bounds__(256, 2) void k_synth_mfma(SynthArgs a, const int4* 
       if (sd.mask && !sd.mask[base + tc[f]]) ch[f] = 0.0;
     }
     const bool harm = sd.harmonic != 0;
-    const int anchor = harm ? a.anchor : 1;
+    const int anchor = harm ? (a.anchor > 0 ? a.anchor : 0x7fffffff) : 1;
     double rr[WT], ri[WT], zr[WT], zi[WT];
-    if (harm) {
-      const double dw = 2.0 * w[0];
-#pragma unroll
-      for (int f = 0; f < WT; ++f) sincos(dw * t[f], &ri[f], &rr[f]);
-    }
     const double* cs = cp + (int64_t)(sd.col0 + lg) * a.R_pad;
     const int nsteps = sd.nm >> 1;
     for (int j = 0; j < nsteps; ++j) {
@@ -219,6 +214,11 @@ __global__ __launch_bounds__(256, 2) void k_synth_mfma(SynthArgs a, const int4* 
           sincos(wk * t[f], &sn, &cn);
           zr[f] = ch[f] * cn;
           zi[f] = ch[f] * sn;
+          if (j == 0) {
+            // step exp(i 2 w_0 t): the square of the mode-0 phasor, or the mode-1 phasor itself
+            rr[f] = moff ? cn : fma(cn, cn, -sn * sn);
+            ri[f] = moff ? sn : 2.0 * cn * sn;
+          }
         }
       } else {
 #pragma unroll
@@ -252,6 +252,223 @@ __global__ __launch_bounds__(256, 2) void k_synth_mfma(SynthArgs a, const int4* 
           *o = a.accumulate ? *o + acc[i][f][g] : acc[i][f][g];
         }
       }
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------- k_synth_valu
+// Fused basis + contraction on the fp64 VALU (v_fma_f64 runs faster than v_mfma_f64 on gfx950:
+// DESIGN.md §Calibration). Lane l owns TOAs t0 + l + 64 m (m < MT); the wave owns NT
+// realizations, so every coefficient is wave-uniform and is read with scalar loads straight
+// into SGPR operands of v_fma_f64. Per mode k each lane advances its phasors
+// z_m = ch_m exp(i w_k t_m) by one complex multiply (harmonic grids), then
+//   acc[m][n] += Re z_m * A[2k][n] + Im z_m * A[2k+1][n]
+// i.e. 2*NT FMAs per 4 recurrence ops per TOA. Workgroup = 4 waves on the same TOAs,
+// realizations r0 + NT * wave.
+template <int MT, int NT>
+__global__ __launch_bounds__(256) void k_synth_valu(SynthArgs a, const int4* __restrict__ tiles) {
+  const int4 tl = tiles[blockIdx.x];
+  const int p = tl.x;
+  if (p < 0) return;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int64_t base = a.offs[p];
+  const int np_ = (int)(a.offs[p + 1] - base);
+  const int r0 = tl.z + wave * NT;
+  if (r0 >= a.n_real) return;
+
+  double t[MT], nuv[MT];
+  int tc[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    const int tloc = tl.y + lane + 64 * m;
+    tc[m] = tloc < np_ ? tloc : np_ - 1;
+    t[m] = a.toas[base + tc[m]];
+    nuv[m] = a.nu[base + tc[m]];
+  }
+  double acc[MT][NT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int n = 0; n < NT; ++n) acc[m][n] = 0.0;
+
+  const double* __restrict__ cb = a.coef + (int64_t)p * a.K * a.R_pad + r0;
+  for (int s = 0; s < a.n_seg; ++s) {
+    const SegDesc sd = a.segs[s];
+    const double* w = sd.w + (int64_t)p * sd.w_pstride;
+    double ch[MT];
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      ch[m] = chrom_factor(sd.freqf, nuv[m], sd.idx);
+      if (sd.mask && !sd.mask[base + tc[m]]) ch[m] = 0.0;
+    }
+    const bool harm = sd.harmonic != 0;
+    const int anchor = harm ? (a.anchor > 0 ? 2 * a.anchor : 0x7fffffff) : 1;
+    double zr[MT], zi[MT], rr[MT], ri[MT];
+    const double* ck = cb + (int64_t)sd.col0 * a.R_pad;
+    for (int k = 0; k < sd.nm; ++k, ck += 2 * (int64_t)a.R_pad) {
+      if (k % anchor == 0) {
+        const double wk = w[k];
+#pragma unroll
+        for (int m = 0; m < MT; ++m) {
+          double sn, cn;
+          sincos(wk * t[m], &sn, &cn);
+          zr[m] = ch[m] * cn;
+          zi[m] = ch[m] * sn;
+          if (k == 0) {
+            rr[m] = cn;
+            ri[m] = sn;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int m = 0; m < MT; ++m) {
+          const double nr = fma(zr[m], rr[m], -zi[m] * ri[m]);
+          const double ni = fma(zr[m], ri[m], zi[m] * rr[m]);
+          zr[m] = nr;
+          zi[m] = ni;
+        }
+      }
+      double cc[NT], cs[NT];
+#pragma unroll
+      for (int n = 0; n < NT; ++n) {
+        cc[n] = ck[n];
+        cs[n] = ck[a.R_pad + n];
+      }
+#pragma unroll
+      for (int n = 0; n < NT; ++n)
+#pragma unroll
+        for (int m = 0; m < MT; ++m) acc[m][n] = fma(zi[m], cs[n], fma(zr[m], cc[n], acc[m][n]));
+    }
+  }
+
+#pragma unroll
+  for (int n = 0; n < NT; ++n) {
+    const int r = r0 + n;
+    if (r >= a.n_real) break;
+    double* orow = a.out + (int64_t)r * a.ldo + base;
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      const int tloc = tl.y + lane + 64 * m;
+      if (tloc < np_) orow[tloc] = a.accumulate ? orow[tloc] + acc[m][n] : acc[m][n];
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------- k_seeds
+// Per (segment, TOA) recurrence seed, computed once per layout (TOAs and grids are fixed across
+// batches): {ch cos(w0 t), ch sin(w0 t), 2 cos(w0 t), ch} with ch = (freqf/nu)^idx * mask and
+// w0 = the segment's first angular frequency for the TOA's pulsar. grid (ceil(n_toa/256), n_seg).
+__global__ __launch_bounds__(256) void k_seeds(const SegDesc* __restrict__ segs, const int32_t* __restrict__ psr_of,
+                                               const double* __restrict__ toas, const double* __restrict__ nu,
+                                               int64_t n_toa, double4* __restrict__ seeds) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int s = blockIdx.y;
+  if (t >= n_toa) return;
+  const SegDesc sd = segs[s];
+  const int p = psr_of[t];
+  double ch = chrom_factor(sd.freqf, nu[t], sd.idx);
+  if (sd.mask && !sd.mask[t]) ch = 0.0;
+  double sn, cn;
+  sincos(sd.w[(int64_t)p * sd.w_pstride] * toas[t], &sn, &cn);
+  seeds[(int64_t)s * n_toa + t] = make_double4(ch * cn, ch * sn, 2.0 * cn, ch);
+}
+
+// ----------------------------------------------------------------------------- k_synth_valu_seeded
+// The production fused kernel for harmonic grids (every f_k = k/T signal of fake_pta.py:264 and
+// correlated_noises.py:120). No transcendental in the kernel: each lane loads its TOA's seed and
+// advances the phasor one mode per complex multiply. Workgroup = 4 waves on 4 consecutive TOA
+// blocks (64*MT TOAs each) sharing the same NT realizations, so the wave-uniform coefficient
+// stream (scalar loads into v_fma_f64 SGPR operands) is shared through the scalar cache.
+template <int MT, int NT>
+__global__ __launch_bounds__(256) void k_synth_valu_seeded(SynthArgs a, const int4* __restrict__ tiles,
+                                                           const double4* __restrict__ seeds) {
+  const int4 tl = tiles[blockIdx.x];
+  const int p = tl.x;
+  if (p < 0) return;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int64_t base = a.offs[p];
+  const int np_ = (int)(a.offs[p + 1] - base);
+  const int tw0 = tl.y + wave * 64 * MT;
+  const int r0 = tl.z;
+  if (tw0 >= np_) return;  // whole wave past the pulsar's last TOA (no cross-wave sync below)
+
+  int tc[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    const int tloc = tw0 + lane + 64 * m;
+    tc[m] = tloc < np_ ? tloc : np_ - 1;
+  }
+  double acc[MT][NT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int n = 0; n < NT; ++n) acc[m][n] = 0.0;
+
+  const double* __restrict__ cb = a.coef + (int64_t)p * a.K * a.R_pad + r0;
+  for (int s = 0; s < a.n_seg; ++s) {
+    const SegDesc sd = a.segs[s];
+    // three-term recurrence z_{k+1} = 2 cos(w0 t) z_k - z_{k-1} (2 FMAs per mode and TOA), started
+    // from z_{-1} = (ch, 0) (frequency 0) and z_0 = ch exp(i w0 t). A rounding error made at step j
+    // reaches step k multiplied by U_{k-j-1}(cos w0 t), |U_n| <= n + 1: the error stays below
+    // ~k^2/2 ulp (5e-13 at 100 modes) for every phase, including w0 t near 0 or pi.
+    double zr[MT], zi[MT], pr[MT], pi_[MT], c2[MT];
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      const double4 q = seeds[(int64_t)s * a.n_toa + base + tc[m]];
+      zr[m] = q.x;
+      zi[m] = q.y;
+      c2[m] = q.z;
+      pr[m] = q.w;
+      pi_[m] = 0.0;
+    }
+    const double* ck = cb + (int64_t)sd.col0 * a.R_pad;
+    // nm is even (padded on the host): two modes per trip; the halves alternate which register
+    // pair holds the current mode, so the recurrence needs no copies
+    for (int k = 0; k < sd.nm; k += 2, ck += 4 * (int64_t)a.R_pad) {
+      double cc[NT], cs[NT];
+#pragma unroll
+      for (int n = 0; n < NT; ++n) {
+        cc[n] = ck[n];
+        cs[n] = ck[a.R_pad + n];
+      }
+#pragma unroll
+      for (int n = 0; n < NT; ++n)
+#pragma unroll
+        for (int m = 0; m < MT; ++m) acc[m][n] = fma(zi[m], cs[n], fma(zr[m], cc[n], acc[m][n]));
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        pr[m] = fma(c2[m], zr[m], -pr[m]);
+        pi_[m] = fma(c2[m], zi[m], -pi_[m]);
+      }
+      const double* ck1 = ck + 2 * (int64_t)a.R_pad;
+#pragma unroll
+      for (int n = 0; n < NT; ++n) {
+        cc[n] = ck1[n];
+        cs[n] = ck1[a.R_pad + n];
+      }
+#pragma unroll
+      for (int n = 0; n < NT; ++n)
+#pragma unroll
+        for (int m = 0; m < MT; ++m) acc[m][n] = fma(pi_[m], cs[n], fma(pr[m], cc[n], acc[m][n]));
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        zr[m] = fma(c2[m], pr[m], -zr[m]);
+        zi[m] = fma(c2[m], pi_[m], -zi[m]);
+      }
+    }
+  }
+
+#pragma unroll
+  for (int n = 0; n < NT; ++n) {
+    const int r = r0 + n;
+    if (r >= a.n_real) break;
+    double* orow = a.out + (int64_t)r * a.ldo + base;
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      const int tloc = tw0 + lane + 64 * m;
+      if (tloc < np_) orow[tloc] = a.accumulate ? orow[tloc] + acc[m][n] : acc[m][n];
     }
   }
 }
@@ -365,6 +582,54 @@ hipError_t launch_synth_direct(hipStream_t st, const SynthArgs& a) {
 
 hipError_t launch_synth_mfma(hipStream_t st, const SynthArgs& a, const int4* tiles, int32_t n_tiles) {
   hipLaunchKernelGGL((k_synth_mfma<kWR, kWT>), dim3(n_tiles), dim3(kWaves * 64), 0, st, a, tiles);
+  return hipGetLastError();
+}
+
+hipError_t launch_synth_valu(hipStream_t st, const SynthArgs& a, const int4* tiles, int32_t n_tiles, int variant) {
+  switch (variant) {
+#define FPTA_VALU_CASE(i)                                                                          \
+  case i:                                                                                          \
+    hipLaunchKernelGGL((k_synth_valu<kValuVariants[i].mt, kValuVariants[i].nt>), dim3(n_tiles), dim3(256), 0, \
+                       st, a, tiles);                                                              \
+    break;
+    FPTA_VALU_CASE(0)
+    FPTA_VALU_CASE(1)
+    FPTA_VALU_CASE(2)
+    FPTA_VALU_CASE(3)
+    FPTA_VALU_CASE(4)
+    FPTA_VALU_CASE(5)
+#undef FPTA_VALU_CASE
+    default:
+      return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_seeds(hipStream_t st, const SegDesc* segs, int32_t n_seg, const int32_t* psr_of,
+                        const double* toas, const double* nu, int64_t n_toa, double4* seeds) {
+  hipLaunchKernelGGL(k_seeds, dim3((unsigned)((n_toa + 255) / 256), n_seg), dim3(256), 0, st, segs, psr_of, toas,
+                     nu, n_toa, seeds);
+  return hipGetLastError();
+}
+
+hipError_t launch_synth_valu_seeded(hipStream_t st, const SynthArgs& a, const int4* tiles, int32_t n_tiles,
+                                    const double4* seeds, int variant) {
+  switch (variant) {
+#define FPTA_SEEDED_CASE(i)                                                                               \
+  case i:                                                                                                 \
+    hipLaunchKernelGGL((k_synth_valu_seeded<kSeededVariants[i].mt, kSeededVariants[i].nt>), dim3(n_tiles), \
+                       dim3(256), 0, st, a, tiles, seeds);                                                \
+    break;
+    FPTA_SEEDED_CASE(0)
+    FPTA_SEEDED_CASE(1)
+    FPTA_SEEDED_CASE(2)
+    FPTA_SEEDED_CASE(3)
+    FPTA_SEEDED_CASE(4)
+    FPTA_SEEDED_CASE(5)
+#undef FPTA_SEEDED_CASE
+    default:
+      return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }
 

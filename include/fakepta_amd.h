@@ -133,10 +133,11 @@ int fpta_batch_checksums(fpta_ctx* ctx, double* sums);
 int fpta_batch_info(fpta_ctx* ctx, int64_t* info);
 
 /* ------------------------------------------------------------------ tuning / profiling */
-#define FPTA_OPT_SYNTH_PATH 1     /* 0 auto, 1 force direct (sincos per basis element), 2 force MFMA */
+#define FPTA_OPT_SYNTH_PATH 1     /* 0 auto, 1 direct (sincos per basis element), 2 fp64 MFMA, 3 fp64 VALU fused */
 #define FPTA_OPT_MFMA_MIN_REAL 2  /* auto: MFMA path when n_real >= this (default 16) */
 #define FPTA_OPT_PROFILE 3        /* 1: time every batch kernel with HIP events on the ctx stream */
-#define FPTA_OPT_ANCHOR 4         /* harmonic recurrence re-anchor interval in K-steps (default 8) */
+#define FPTA_OPT_ANCHOR 4         /* recurrence re-anchor interval in K-steps of 2 modes (0 = once per signal, default) */
+#define FPTA_OPT_VALU_VARIANT 5   /* tile variant of the VALU fused kernel (0..5) */
 int fpta_set_option(fpta_ctx* ctx, int32_t key, int64_t value);
 /* Kernel ids for fpta_kernel_stats */
 #define FPTA_K_GEN 0

@@ -213,23 +213,28 @@ def _build(ctx, rng, P=7, n_range=(20, 260), per_psr=((30, 0.0), (41, 2.0)), com
     return offs, toas, nu, segs, sigma, block_of, es
 
 
-@pytest.mark.parametrize("path", [1, 2])
+PATHS = [(1, 0), (2, 0)] + [(3, v) for v in range(6)]  # (synth path, VALU variant)
+
+
+@pytest.mark.parametrize("path,variant", PATHS)
 @pytest.mark.parametrize("case", ["basic", "masked_odd_modes", "white_ecorr", "common_only", "tiny_pulsars"])
-def test_batch_vs_oracle(ctx, capi, path, case):
+def test_batch_vs_oracle(ctx, capi, path, variant, case):
     rng = np.random.default_rng(zlib.crc32(case.encode()))
     kw = dict(basic={}, masked_odd_modes=dict(per_psr=((7, 4.0), (1, 0.0)), masked=True),
               white_ecorr=dict(white=True, ecorr=True), common_only=dict(per_psr=(), common=((30, 0.0), (13, 2.0))),
               tiny_pulsars=dict(P=5, n_range=(1, 18)))[case]
     offs, toas, nu, segs, sigma, block_of, es = _build(ctx, rng, **kw)
     ctx.set_option(capi.OPT_SYNTH_PATH, path)
+    ctx.set_option(capi.OPT_VALU_VARIANT, variant)
     try:
-        for real0, R in ((0, 70), (1000003, 3)):
+        for real0, R in ((0, 70), (1000003, 3), (5, 257)):
             got = ctx.batch_synth(99, real0, R)
             want = O.batch_synth(offs, toas, nu, segs, 99, real0, R, sigma=sigma, block_of=block_of,
                                  ecorr_sigma=es)
             assert_parity(got, want, TOL)
     finally:
         ctx.set_option(capi.OPT_SYNTH_PATH, 0)
+        ctx.set_option(capi.OPT_VALU_VARIANT, 0)
 
 
 def test_batch_from_z_vs_oracle(ctx):
@@ -243,23 +248,26 @@ def test_batch_from_z_vs_oracle(ctx):
     assert_parity(got, want, TOL)
 
 
-@pytest.mark.parametrize("anchor", [1, 3, 8, 64])
-def test_recurrence_anchor_accuracy(ctx, capi, anchor):
-    """The MFMA path's phasor recurrence stays within tolerance for every re-anchor interval,
-    including 100-mode grids on real-MJD-like epochs (t ~ 5e9 s)."""
+@pytest.mark.parametrize("path", [2, 3])
+@pytest.mark.parametrize("anchor", [0, 1, 3, 8, 64])
+def test_recurrence_anchor_accuracy(ctx, capi, path, anchor):
+    """The fused kernels' phasor recurrence stays within tolerance for every re-anchor interval
+    (0 = once per signal, the default), on 100-mode grids with a FLAT spectrum (every mode
+    weighs equally) and real-MJD-like epochs (t ~ 5e9 s, phases up to ~2e4 rad)."""
     rng = np.random.default_rng(5)
     offs, toas, nu = random_layout(rng, 4, (100, 300), t_max=1.6e8)
     toas = toas + 4.5e9
     ctx.batch_set_toas(offs, toas, nu)
-    f, a = per_psr_signal(rng, offs, toas, 100)
+    f, _ = per_psr_signal(rng, offs, toas, 100)
+    a = np.full_like(f, 1e-7)
     ctx.batch_add_signal(0, f, a, idx=2.0)
-    ctx.set_option(capi.OPT_SYNTH_PATH, 2)
+    ctx.set_option(capi.OPT_SYNTH_PATH, path)
     ctx.set_option(capi.OPT_ANCHOR, anchor)
     try:
         got = ctx.batch_synth(5, 0, 64)
     finally:
         ctx.set_option(capi.OPT_SYNTH_PATH, 0)
-        ctx.set_option(capi.OPT_ANCHOR, 8)
+        ctx.set_option(capi.OPT_ANCHOR, 0)
     want = O.batch_synth(offs, toas, nu, [O.Segment(0, 2 * np.pi * f, a, 2.0)], 5, 0, 64)
     assert_parity(got, want, TOL)
 
