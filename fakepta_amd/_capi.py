@@ -42,6 +42,7 @@ _SIGS = [
     ("fpta_batch_clear_signals", _c_int, [_ctx_p]),
     ("fpta_batch_synth", _c_int, [_ctx_p, _u64, _i64, _i32, _vp, _vp]),
     ("fpta_batch_synth_from_z", _c_int, [_ctx_p, _i32, _i32, _vp, _vp]),
+    ("fpta_batch_download", _c_int, [_ctx_p, _i32, _i32, _vp]),
     ("fpta_batch_device_out", _c_int, [_ctx_p, ctypes.POINTER(_vp), ctypes.POINTER(_i64), ctypes.POINTER(_i32)]),
     ("fpta_batch_checksums", _c_int, [_ctx_p, _vp]),
     ("fpta_batch_info", _c_int, [_ctx_p, _vp]),
@@ -200,6 +201,13 @@ class Context:
         out = np.empty((n_real, info["n_toa"]))
         self._check(_lib.fpta_batch_synth_from_z(self._h, n_real, z.shape[3], _ptr(z), _ptr(out)),
                     "fpta_batch_synth_from_z")
+        return out
+
+    def batch_download(self, r_begin, r_count):
+        """Realizations [r_begin, r_begin + r_count) of the last block -> host [r_count, n_toa]."""
+        _, ld, _ = self.batch_device_out()
+        out = np.empty((r_count, ld))
+        self._check(_lib.fpta_batch_download(self._h, int(r_begin), int(r_count), _ptr(out)), "fpta_batch_download")
         return out
 
     def batch_device_out(self):

@@ -796,6 +796,21 @@ int fpta_batch_synth_from_z(fpta_ctx* c, int32_t n_real, int32_t n_modes_max, co
   return batch_common(c, 0, 0, n_real, c->zin.as<double>(), n_modes_max, out, nullptr, false);
 }
 
+int fpta_batch_download(fpta_ctx* c, int32_t r_begin, int32_t r_count, double* host) {
+  if (!c || !host) return fail(c, FPTA_EINVAL, "download: bad arguments");
+  if (!c->out_R) return fail(c, FPTA_ESTATE, "download: nothing synthesized yet");
+  if (r_begin < 0 || r_count <= 0 || r_begin + r_count > c->out_R)
+    return fail(c, FPTA_EINVAL, "download: realization range outside the last block");
+  HIPCHK(c, hipSetDevice(c->device), "hipSetDevice");
+  const size_t row = sizeof(double) * (size_t)c->out_ld;
+  HIPCHK(c,
+         hipMemcpyAsync(host, c->out.as<char>() + row * r_begin, row * r_count, hipMemcpyDeviceToHost,
+                        c->stream),
+         "download copy");
+  HIPCHK(c, hipStreamSynchronize(c->stream), "download sync");
+  return FPTA_OK;
+}
+
 int fpta_batch_device_out(fpta_ctx* c, double** dptr, int64_t* ld, int32_t* n_real) {
   if (!c) return fail(nullptr, FPTA_EINVAL, "null ctx");
   if (!c->out_R) return fail(c, FPTA_ESTATE, "device_out: nothing synthesized yet");

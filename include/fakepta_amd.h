@@ -124,6 +124,9 @@ int fpta_batch_synth(fpta_ctx* ctx, uint64_t seed, int64_t real0, int32_t n_real
  * z [n_real][n_seg][n_psr][n_modes_max][2] (cos, sin); white/ECORR are not added. */
 int fpta_batch_synth_from_z(fpta_ctx* ctx, int32_t n_real, int32_t n_modes_max, const double* z,
                             double* out);
+/* Copy realizations [r_begin, r_begin + r_count) of the last block to host [r_count][n_toa_total]
+ * (the "residual block" gather of SURVEY.md §8(e); the full block can be tens of GB). */
+int fpta_batch_download(fpta_ctx* ctx, int32_t r_begin, int32_t r_count, double* host);
 /* Device pointer of the last synthesized block and its leading dimension (n_toa_total). */
 int fpta_batch_device_out(fpta_ctx* ctx, double** dptr, int64_t* ld, int32_t* n_real);
 /* Per-realization sum and sum of squares of the last block, computed on device

@@ -1,0 +1,108 @@
+"""BASELINE configs at full size on the GPU, checked through size-independent properties:
+realizations picked from the device block are re-synthesized by the oracle (from the device's
+own coefficient dump, and from the oracle's own Philox stream) on a subset of pulsars.
+
+C4: 1000 pulsars x 10k TOAs, HD GWB 100 modes, 1000x1000 ORF factor, R = 256.
+C5: 100 pulsars, 2 backends x 2 sub-epoch TOAs, RN30 + DM100 (nu^-2) + Sv100 (nu^-4) + HD30 +
+    monopole30 + dipole30 + EFAC/EQUAD + ECORR (ENTERPRISE convention), R = 128.
+"""
+import numpy as np
+import pytest
+
+from oracle import fakepta_oracle as O
+from tests.conftest import assert_parity
+from tests.helpers import oracle_segments
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-10
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from fakepta_amd import _capi
+    c = _capi.Context(0)
+    yield c
+    c.close()
+
+
+def fibonacci(P):
+    i = np.arange(P) + 0.5
+    th = np.arccos(1 - 2 * i / P)
+    ph = np.mod(2 * np.pi * i / ((1 + 5 ** 0.5) / 2), 2 * np.pi)
+    return np.stack([np.cos(ph) * np.sin(th), np.sin(ph) * np.sin(th), np.cos(th)], 1)
+
+
+def test_c4_ska_scale(ctx):
+    P, n_p, N, R, seed = 1000, 10000, 100, 256, 4242
+    rng = np.random.default_rng(0)
+    T = 10 * O.JULIAN_YEAR
+    offs = (np.arange(P + 1) * n_p).astype(np.int64)
+    toas = (np.linspace(0, T, n_p)[None, :] + rng.uniform(0, 86400, (P, 1))).ravel()
+    nu = np.abs(1400.0 + rng.normal(0, 10, P * n_p))
+    pos = fibonacci(P)
+    L = O.mvn_factor(O.orf_hd(pos))
+    f = O.freq_grid(N, np.ptp(toas))
+    amp = np.sqrt(O.powerlaw(f, -15.0, 13 / 3) * O.delta_f(f))
+    ctx.batch_set_toas(offs, toas, nu)
+    ctx.batch_add_signal(1, f, amp, idx=0.0, L=L)
+    out_none, co = ctx.batch_synth(seed, 0, R, to_host=False, coeffs=True)
+    assert out_none is None and co.shape == (P, 2 * N, R)
+    picks = [0, 255]
+    rows = np.concatenate([ctx.batch_download(r, 1) for r in picks])
+    sub = [0, 1, 333, 999]
+    w = 2 * np.pi * f
+    for j, r in enumerate(picks):
+        z = np.stack([O.gp_normals(seed, np.array([r]), q, 0, N)[0] for q in range(P)])  # [P, N, 2]
+        x = np.einsum("pq,qnc->pnc", L, z)
+        for p in sub:
+            a = co[p, :, r]
+            np.testing.assert_allclose(a[0::2], amp * x[p, :, 0], rtol=1e-11, atol=1e-11 * np.abs(a).max())
+            np.testing.assert_allclose(a[1::2], amp * x[p, :, 1], rtol=1e-11, atol=1e-11 * np.abs(a).max())
+            sl = slice(offs[p], offs[p + 1])
+            ph = np.outer(toas[sl], w)
+            want = np.cos(ph) @ a[0::2] + np.sin(ph) @ a[1::2]
+            assert_parity(rows[j, sl], want, TOL)
+    sums = ctx.batch_checksums()
+    assert np.all(np.isfinite(sums)) and sums.shape == (R, 2)
+    np.testing.assert_allclose(sums[picks, 1], (rows ** 2).sum(1), rtol=1e-9)
+
+
+def test_c5_mixed(ctx):
+    from fakepta_amd import correlated_noises as cn
+    from fakepta_amd import fake_pta as fp
+    from fakepta_amd.batch import BatchSimulator
+    P, R, seed = 100, 128, 99
+    np.random.seed(7)
+    pos = fibonacci(P)
+    epochs = np.arange(1, 501) * 7.3 * 86400.0
+    psrs = []
+    for p in range(P):
+        th, ph = np.arccos(pos[p, 2]), np.mod(np.arctan2(pos[p, 1], pos[p, 0]), 2 * np.pi)
+        t = np.sort(np.concatenate([epochs, epochs + 3600.0]))
+        psr = fp.Pulsar(t, 1e-7, th, ph, backends=["A.1400", "B.800"],
+                        custom_model={"RN": 30, "DM": 100, "Sv": 100})
+        psr.add_white_noise(add_ecorr=True, randomize=True)
+        for b in psr.backends:
+            psr.noisedict[f"{psr.name}_{b}_log10_ecorr"] = -7.0
+        psr.add_red_noise(log10_A=np.random.uniform(-15, -13), gamma=np.random.uniform(1, 5))
+        psr.add_dm_noise(log10_A=np.random.uniform(-15, -13), gamma=np.random.uniform(1, 5))
+        psr.add_chromatic_noise(log10_A=np.random.uniform(-15, -13), gamma=np.random.uniform(1, 5))
+        psrs.append(psr)
+    assert len(psrs[0].toas) == 2000
+    cn.add_common_correlated_noise(psrs, orf="hd", name="gw", log10_A=-14.5, gamma=13 / 3)
+    cn.add_common_correlated_noise(psrs, orf="monopole", name="clk", log10_A=-15.0, gamma=4.0)
+    cn.add_common_correlated_noise(psrs, orf="dipole", name="eph", log10_A=-15.0, gamma=4.0)
+    sim = BatchSimulator(psrs, white=True, ecorr=True, ctx=ctx)
+    info = ctx.batch_info()
+    assert info["K"] == 640 and info["n_seg"] == 6
+    assert len(sim.blocks) == P * 2 * 500  # one 2-TOA ECORR epoch per backend per epoch
+    sim.synth(R, seed=seed, to_host=False)
+    block_of = -np.ones(sim.n_toa, dtype=np.int64)
+    for b, q in enumerate(sim.blocks):
+        block_of[q] = b
+    segs = oracle_segments(sim)
+    for r0, n in ((0, 2), (127, 1)):
+        got = ctx.batch_download(r0, n)
+        want = O.batch_synth(sim.offs, sim.toas, sim.freqs, segs, seed, r0, n, sigma=sim.sigma, block_of=block_of,
+                             ecorr_sigma=sim.ecorr_sigma)
+        assert_parity(got, want, TOL)
