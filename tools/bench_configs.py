@@ -1,0 +1,167 @@
+"""Timings of the BASELINE configs other than the driver's headline (bench.py = C2), one GPU.
+
+    python tools/bench_configs.py [c1] [c3] [c4] [c5] [--c3-real 100000]
+
+c1  make_fake_array(25 psr, Tobs 10, ntoas 1000, gaps, RN30) drop-in latency, seed 0
+    (the reference: 0.045 s on the survey container's CPU)
+c3  100-psr HD GWB30 only (K = 60), realizations streamed in batches of 4096, checksums only
+c4  1000 psr x 10k TOAs, HD GWB100 (K = 200), 1000x1000 ORF factor, R = 256
+c5  100 psr, RN30 + DM100 + Sv100 + HD30 + monopole30 + dipole30 + white + ECORR (K = 640), R = 1024
+Prints one JSON line per config: samples/s end-to-end, and per-kernel HIP-event times.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def kernel_times(ctx, capi, steps):
+    return {n: ctx.kernel_stats(k)[1] / steps for n, k in
+            (("gen", capi.K_GEN), ("mix", capi.K_MIX), ("synth", capi.K_SYNTH), ("white", capi.K_WHITE))}
+
+
+def timed(ctx, capi, fn, steps, warmup=2):
+    for _ in range(warmup):
+        fn(0)
+    ctx.synchronize()
+    ctx.set_option(capi.OPT_PROFILE, 1)
+    ctx.reset_stats()
+    t0 = time.perf_counter()
+    for s in range(steps):
+        fn(s + warmup)
+    ctx.synchronize()
+    dt = time.perf_counter() - t0
+    kt = kernel_times(ctx, capi, steps)
+    ctx.set_option(capi.OPT_PROFILE, 0)
+    return dt, kt
+
+
+def c1():
+    from fakepta_amd import fake_pta as fp
+    kw = dict(npsrs=25, Tobs=10, ntoas=1000, isotropic=True, gaps=True, toaerr=1e-7, backends="NUPPI.1400",
+              custom_model={"RN": 30, "DM": None, "Sv": None})
+    np.random.seed(0)
+    fp.make_fake_array(**kw)  # warm (context creation, code objects)
+    ts = []
+    for _ in range(5):
+        np.random.seed(0)
+        t0 = time.perf_counter()
+        psrs = fp.make_fake_array(**kw)
+        ts.append(time.perf_counter() - t0)
+    n = sum(len(p.toas) for p in psrs)
+    return dict(config="c1", n_toa=n, latency_s_median=float(np.median(ts)), latency_s_min=float(min(ts)),
+                samples_per_s=n / float(np.median(ts)), reference_cpu_s=0.045,
+                note="drop-in path: host np.random draws + one GPU call per injection; latency-bound")
+
+
+def fib(P):
+    i = np.arange(P) + 0.5
+    th = np.arccos(1 - 2 * i / P)
+    ph = np.mod(2 * np.pi * i / ((1 + 5 ** 0.5) / 2), 2 * np.pi)
+    return np.stack([np.cos(ph) * np.sin(th), np.sin(ph) * np.sin(th), np.cos(th)], 1)
+
+
+def c3(total):
+    import bench
+    from fakepta_amd import _capi
+    from fakepta_amd import correlated_noises as cn
+    from fakepta_amd.batch import BatchSimulator
+    ctx = _capi.Context(0)
+    psrs = bench.build_c2(100, 2000)
+    sim = BatchSimulator(psrs, signals=["gw_common"], white=False, ctx=ctx)
+    B = 4096
+    nb = (total + B - 1) // B
+    sums = []
+
+    def step(s):
+        n = min(B, total - (s % nb) * B)
+        ctx.batch_synth(1234, (s % nb) * B, n, to_host=False)
+
+    dt, kt = timed(ctx, _capi, step, nb, warmup=1)
+    sums = ctx.batch_checksums()
+    info = ctx.batch_info()
+    del cn
+    return dict(config="c3", K=info["K"], realizations=total, batch=B, wall_s=dt,
+                samples_per_s=info["n_toa"] * total / dt, kernels_ms_per_batch={k: v for k, v in kt.items()},
+                last_checksum=float(sums[:, 1].sum()))
+
+
+def c4():
+    from fakepta_amd import _capi
+    from oracle import fakepta_oracle as O  # host-side ORF/PSD helpers only (setup, untimed)
+    ctx = _capi.Context(0)
+    P, n_p, N, R = 1000, 10000, 100, 256
+    rng = np.random.default_rng(0)
+    T = 10 * O.JULIAN_YEAR
+    offs = (np.arange(P + 1) * n_p).astype(np.int64)
+    toas = (np.linspace(0, T, n_p)[None, :] + rng.uniform(0, 86400, (P, 1))).ravel()
+    nu = np.abs(1400.0 + rng.normal(0, 10, P * n_p))
+    from fakepta_amd.correlated_noises import orf_factor
+    class _P:  # noqa: E306
+        def __init__(self, p):
+            self.pos = p
+    from fakepta_amd.correlated_noises import hd
+    L = orf_factor(hd([_P(x) for x in fib(P)]))
+    f = np.arange(1, N + 1) / np.ptp(toas)
+    amp = np.sqrt(O.powerlaw(f, -15.0, 13 / 3) * O.delta_f(f))
+    ctx.batch_set_toas(offs, toas, nu)
+    ctx.batch_add_signal(1, f, amp, idx=0.0, L=L)
+    dt, kt = timed(ctx, _capi, lambda s: ctx.batch_synth(7, s * R, R, to_host=False), 5, warmup=1)
+    flops = 2.0 * 2 * N * P * n_p * R
+    return dict(config="c4", K=2 * N, n_toa=P * n_p, realizations=R, ms_per_step=dt / 5 * 1e3,
+                samples_per_s=P * n_p * R * 5 / dt, kernels_ms_per_step=kt,
+                synth_tflops=flops / (kt["synth"] / 1e3) / 1e12,
+                mix_tflops=2.0 * P * P * 2 * N * R / (kt["mix"] / 1e3) / 1e12 if kt["mix"] else None)
+
+
+def c5():
+    from fakepta_amd import _capi
+    from fakepta_amd import correlated_noises as cn
+    from fakepta_amd import fake_pta as fp
+    from fakepta_amd.batch import BatchSimulator
+    ctx = _capi.Context(0)
+    P = 100
+    np.random.seed(7)
+    pos = fib(P)
+    epochs = np.arange(1, 501) * 7.3 * 86400.0
+    psrs = []
+    for p in range(P):
+        th, ph = np.arccos(pos[p, 2]), np.mod(np.arctan2(pos[p, 1], pos[p, 0]), 2 * np.pi)
+        t = np.sort(np.concatenate([epochs, epochs + 3600.0]))
+        psr = fp.Pulsar(t, 1e-7, th, ph, backends=["A.1400", "B.800"], custom_model={"RN": 30, "DM": 100, "Sv": 100})
+        psr.add_white_noise(add_ecorr=True, randomize=True)
+        psr.add_red_noise(log10_A=-14, gamma=3)
+        psr.add_dm_noise(log10_A=-14, gamma=3)
+        psr.add_chromatic_noise(log10_A=-14, gamma=3)
+        psrs.append(psr)
+    cn.add_common_correlated_noise(psrs, orf="hd", name="gw", log10_A=-14.5, gamma=13 / 3)
+    cn.add_common_correlated_noise(psrs, orf="monopole", name="clk", log10_A=-15.0, gamma=4.0)
+    cn.add_common_correlated_noise(psrs, orf="dipole", name="eph", log10_A=-15.0, gamma=4.0)
+    sim = BatchSimulator(psrs, white=True, ecorr=True, ctx=ctx)
+    R = 1024
+    dt, kt = timed(ctx, _capi, lambda s: ctx.batch_synth(9, s * R, R, to_host=False), 10)
+    info = ctx.batch_info()
+    return dict(config="c5", K=info["K"], n_toa=info["n_toa"], realizations=R, ms_per_step=dt / 10 * 1e3,
+                samples_per_s=info["n_toa"] * R * 10 / dt, kernels_ms_per_step=kt,
+                synth_tflops=2.0 * info["K"] * info["n_toa"] * R / (kt["synth"] / 1e3) / 1e12,
+                n_ecorr_blocks=len(sim.blocks))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("configs", nargs="*", default=["c1", "c3", "c4", "c5"])
+    ap.add_argument("--c3-real", type=int, default=100000)
+    args = ap.parse_args()
+    for c in args.configs:
+        res = c3(args.c3_real) if c == "c3" else globals()[c]()
+        print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()
