@@ -24,6 +24,17 @@ def _df(f):
     return np.diff(np.append(0.0, f))
 
 
+def batch_factor(orf_mat):
+    """Square root of the ORF for batched draws: the lower Cholesky factor when the ORF is
+    positive definite (HD, curn: triangular mixing on device, half the FLOPs), otherwise the SVD
+    factor numpy's multivariate_normal uses (singular monopole / dipole ORFs). Any L with
+    L L^T = ORF gives the reference's distribution; the drop-in path keeps numpy's exact factor."""
+    try:
+        return np.ascontiguousarray(np.linalg.cholesky(orf_mat))
+    except np.linalg.LinAlgError:
+        return orf_factor(orf_mat)
+
+
 class BatchSimulator:
     """Device-resident noise model of an array of Pulsar objects.
 
@@ -63,7 +74,7 @@ class BatchSimulator:
         if "common" in name:
             f = np.asarray(sm0["f"], float)
             amp = np.sqrt(np.asarray(sm0["psd"], float) * _df(f))
-            L = orf_factor(orf_matrix(self.psrs, sm0["orf"], sm0.get("hmap")))
+            L = batch_factor(orf_matrix(self.psrs, sm0["orf"], sm0.get("hmap")))
             self.add_signal(name, 1, f, amp, idx=float(sm0["idx"]), L=L)
             return
         nm = max(len(p.signal_model[name]["f"]) for p in have)

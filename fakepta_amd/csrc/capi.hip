@@ -93,8 +93,9 @@ struct fpta_ctx {
   std::string err;
   Layout batch, scratch;
   // batch white noise
-  DevBuf sigma, block_of, esig;
+  DevBuf sigma, block_of, esig, zb_epochs;
   bool has_sigma = false, has_blocks = false;
+  int64_t n_blocks = 0;
   // work buffers
   DevBuf coef, zbuf, out, sums, zin, xout, hostz, scratch_out, scratch_z, scratch_zb, scratch_sigma,
       scratch_block_of, scratch_esig, dbg_a, dbg_b;
@@ -278,6 +279,17 @@ int layout_add_signal(fpta_ctx* c, Layout& L, int32_t kind, int32_t nm, const do
   d.kind = kind;
   d.col0 = L.K;
   d.harmonic = harm ? 1 : 0;
+  d.l_lower = 0;
+  if (kind == 1) {  // a Cholesky factor (exact zeros above the diagonal) allows triangular mixing
+    bool low = true;
+    for (int32_t p = 0; p < P && low; ++p)
+      for (int32_t q = p + 1; q < P; ++q)
+        if (Lmat[(size_t)p * P + q] != 0.0) {
+          low = false;
+          break;
+        }
+    d.l_lower = low ? 1 : 0;
+  }
   L.K += 2 * nmp;
   L.segs.push_back(s);
   L.dirty = true;
@@ -331,8 +343,12 @@ int run_coefficients(fpta_ctx* c, Layout& L, uint64_t seed, int64_t real0, int32
     }
     if (d.kind == 1) {
       KTimer kt(c, FPTA_K_MIX);
-      HIPCHK(c, launch_mix(c->stream, d, P, R_pad, c->zbuf.as<double>(), c->coef.as<double>(), L.K, x_out),
-             "k_mix launch");
+      if (P >= kMixTiledMinP && R_pad % 128 == 0)
+        HIPCHK(c, launch_mix_tiled(c->stream, d, P, R_pad, c->zbuf.as<double>(), c->coef.as<double>(), L.K, x_out),
+               "k_mix_tiled launch");
+      else
+        HIPCHK(c, launch_mix(c->stream, d, P, R_pad, c->zbuf.as<double>(), c->coef.as<double>(), L.K, x_out),
+               "k_mix launch");
     }
   }
   return FPTA_OK;
@@ -725,6 +741,7 @@ int fpta_batch_set_white(fpta_ctx* c, const double* sigma, int64_t n_blocks, con
   c->has_sigma = sigma != nullptr;
   if (sigma && (rc = upload(c, c->sigma, sigma, sizeof(double) * N, "set_white sigma"))) return rc;
   c->has_blocks = n_blocks > 0;
+  c->n_blocks = n_blocks;
   if (n_blocks > 0) {
     if (!ecorr_sigma) return fail(c, FPTA_EINVAL, "set_white: ecorr_sigma missing");
     std::vector<int32_t> owner;
@@ -760,13 +777,15 @@ static int batch_common(fpta_ctx* c, uint64_t seed, int64_t real0, int32_t n_rea
   }
   if (white && (c->has_sigma || c->has_blocks)) {
     if (n_real > 65535) return fail(c, FPTA_EINVAL, "white: n_real > 65535 per call");
+    if (c->has_blocks) HIPCHK(c, c->zb_epochs.ensure(sizeof(double) * (size_t)n_real * c->n_blocks), "zb alloc");
     KTimer kt(c, FPTA_K_WHITE);
     HIPCHK(c,
-           launch_white(c->stream, c->has_sigma ? c->sigma.as<double>() : nullptr,
-                        c->has_blocks ? c->block_of.as<int32_t>() : nullptr,
-                        c->has_blocks ? c->esig.as<double>() : nullptr, nullptr, nullptr, c->out.as<double>(),
-                        L.n_toa, L.n_toa, n_real, real0, (uint32_t)(seed & 0xFFFFFFFFull), (uint32_t)(seed >> 32)),
-           "k_white launch");
+           launch_white_batch(c->stream, c->has_sigma ? c->sigma.as<double>() : nullptr,
+                              c->has_blocks ? c->block_of.as<int32_t>() : nullptr,
+                              c->has_blocks ? c->esig.as<double>() : nullptr, c->has_blocks ? c->n_blocks : 0,
+                              c->zb_epochs.as<double>(), c->out.as<double>(), L.n_toa, L.n_toa, n_real, real0,
+                              (uint32_t)(seed & 0xFFFFFFFFull), (uint32_t)(seed >> 32)),
+           "k_white_pairs launch");
   }
   if (out) HIPCHK(c, hipMemcpyAsync(out, c->out.p, out_bytes, hipMemcpyDeviceToHost, c->stream), "out download");
   if (coeffs_out && L.K > 0) {

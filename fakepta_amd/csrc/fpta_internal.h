@@ -18,6 +18,7 @@ struct SegDesc {
   int32_t kind;         // 0 per-pulsar, 1 common
   int32_t col0;         // first coefficient column of this segment (cos of mode 0)
   int32_t harmonic;     // 1: w[k] == (k+1) w[0] to rounding -> angle-addition recurrence
+  int32_t l_lower;      // kind 1: L is lower-triangular (Cholesky factor) -> triangular mixing
 };
 
 struct SynthArgs {
@@ -46,6 +47,7 @@ constexpr int kWaves = 4;               // waves per workgroup
 constexpr int kTileReal = kWR * 16;     // realizations per workgroup
 constexpr int kTileToa = kWaves * kWT * 16;  // TOAs per workgroup
 constexpr int kRealPad = 128;           // R_pad granularity (multiple of every realization tile)
+constexpr int kMixTiledMinP = 64;       // ORF mixing: tiled GEMM from this many pulsars up
 
 // VALU fused-kernel variants: (TOAs per lane MT, realizations per wave NT); workgroup tile is
 // 64*MT TOAs x 4*NT realizations.
@@ -68,6 +70,11 @@ hipError_t launch_gen(hipStream_t st, const SegDesc& sd, int32_t seg_id, int32_t
                       int32_t zin_nseg, int32_t zin_nm, double* coef, int32_t K, double* zbuf);
 hipError_t launch_mix(hipStream_t st, const SegDesc& sd, int32_t P, int32_t R_pad, const double* zbuf,
                       double* coef, int32_t K, double* x_out);
+hipError_t launch_mix_tiled(hipStream_t st, const SegDesc& sd, int32_t P, int32_t R_pad, const double* zbuf,
+                            double* coef, int32_t K, double* x_out);
+hipError_t launch_white_batch(hipStream_t st, const double* sigma, const int32_t* block_of, const double* esig,
+                              int64_t n_blocks, double* zb, double* out, int64_t ldo, int64_t n_toa, int32_t n_real,
+                              int64_t real0, uint32_t k0, uint32_t k1);
 hipError_t launch_synth_direct(hipStream_t st, const SynthArgs& a);
 hipError_t launch_synth_mfma(hipStream_t st, const SynthArgs& a, const int4* tiles, int32_t n_tiles);
 hipError_t launch_synth_valu(hipStream_t st, const SynthArgs& a, const int4* tiles, int32_t n_tiles, int variant);

@@ -113,6 +113,92 @@ __global__ __launch_bounds__(256) void k_mix(const double* __restrict__ L, const
   }
 }
 
+// ----------------------------------------------------------------------------- k_mix_tiled
+// The same product as k_mix as a register/LDS-tiled fp64 GEMM for large arrays (C4: P = 1000):
+// C[P x M] = L[P x P] Z[P x M], block tile 128 rows x 128 columns, 8 x 8 outputs per thread,
+// q-chunks of 16 staged through LDS (L transposed), next chunk prefetched into registers.
+// Each Z element is re-read P/128 times instead of P/16. With a lower-triangular L (Cholesky of
+// a positive-definite ORF) the q loop stops at the tile's last row: half the work.
+// LDS reads are ds_read_b128: L rows ty*8.. are broadcast within a 16-lane group, Z columns
+// {2tx, 2tx+1} + 32 jj give every 16-lane group 256 contiguous bytes (conflict-free).
+constexpr int MT_P = 128, MT_M = 128, MT_Q = 16;
+__global__ __launch_bounds__(256) void k_mix_tiled(const double* __restrict__ L, const double* __restrict__ amp,
+                                                   int32_t P, int64_t M, int32_t R_pad, int32_t lower,
+                                                   const double* __restrict__ zbuf, double* __restrict__ coef,
+                                                   int32_t K, int32_t col0, double* __restrict__ x_out) {
+  __shared__ __attribute__((aligned(16))) double Ls[MT_Q][MT_P + 2];  // +2: transposed writes spread banks
+  __shared__ __attribute__((aligned(16))) double Zs[MT_Q][MT_M];
+  const int tid = threadIdx.x;
+  const int tx = tid & 15, ty = tid >> 4;
+  const int p0 = blockIdx.y * MT_P;
+  const int64_t m0 = (int64_t)blockIdx.x * MT_M;
+  const int qend = lower ? min(P, p0 + MT_P) : P;
+  double acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = 0.0;
+  double lreg[8], zreg[8];
+  auto fetch = [&](int q0) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int idx = tid + 256 * e;
+      const int i = idx >> 4, jj = idx & 15;  // L[p0 + i][q0 + jj]
+      const int p = p0 + i, q = q0 + jj;
+      lreg[e] = (p < P && q < P) ? L[(int64_t)p * P + q] : 0.0;
+      const int zq = idx >> 7, c = idx & 127;  // Z[q0 + zq][m0 + c]
+      zreg[e] = (q0 + zq < P) ? zbuf[(int64_t)(q0 + zq) * M + m0 + c] : 0.0;
+    }
+  };
+  fetch(0);
+  for (int q0 = 0; q0 < qend; q0 += MT_Q) {
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int idx = tid + 256 * e;
+      Ls[idx & 15][idx >> 4] = lreg[e];
+      Zs[idx >> 7][idx & 127] = zreg[e];
+    }
+    __syncthreads();
+    if (q0 + MT_Q < qend) fetch(q0 + MT_Q);
+#pragma unroll
+    for (int q = 0; q < MT_Q; ++q) {
+      double lv[8], zv[8];
+#pragma unroll
+      for (int i = 0; i < 8; i += 2) {
+        const double2 a = *reinterpret_cast<const double2*>(&Ls[q][ty * 8 + i]);
+        lv[i] = a.x;
+        lv[i + 1] = a.y;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const double2 b = *reinterpret_cast<const double2*>(&Zs[q][2 * tx + 32 * j]);
+        zv[2 * j] = b.x;
+        zv[2 * j + 1] = b.y;
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] = fma(lv[i], zv[j], acc[i][j]);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int p = p0 + ty * 8 + i;
+    if (p >= P) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t m = m0 + 2 * tx + 32 * j;  // columns m, m+1 share j (R_pad is even)
+      const int jc = (int)(m / R_pad);
+      const int r = (int)(m % R_pad);
+      const double a = amp[jc >> 1];
+      double2 v = make_double2(a * acc[i][2 * j], a * acc[i][2 * j + 1]);
+      *reinterpret_cast<double2*>(&coef[((int64_t)p * K + col0 + jc) * R_pad + r]) = v;
+      if (x_out) *reinterpret_cast<double2*>(&x_out[(int64_t)p * M + m]) = make_double2(acc[i][2 * j], acc[i][2 * j + 1]);
+    }
+  }
+}
+
 // ----------------------------------------------------------------------------- k_synth_direct
 // grid (ceil(n_toa/256), n_real). One thread per (TOA, realization); the phase of every basis
 // element is (2 pi f_k) t computed exactly as fake_pta.py:386, then sincos.
@@ -515,6 +601,53 @@ __global__ __launch_bounds__(256) void k_white(const double* __restrict__ sigma,
   out[(int64_t)r * ldo + t] += v;
 }
 
+// ----------------------------------------------------------------------------- batch white / ECORR
+// k_epoch_normals: zb[r][b] for every ECORR epoch, one Philox call per epoch pair (the ECORR
+// stream of the oracle). grid (ceil(ceil(n_blocks/2)/256), n_real).
+__global__ __launch_bounds__(256) void k_epoch_normals(int64_t n_blocks, int64_t real0, uint32_t k0, uint32_t k1,
+                                                       double* __restrict__ zb) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;  // epoch pair
+  const int r = blockIdx.y;
+  if (2 * i >= n_blocks) return;
+  const u32x4 c = {(uint32_t)i, kWhitePsrWord, kEcorrStream, (uint32_t)(real0 + r)};
+  double z0, z1;
+  box_muller(philox4x32_10(c, k0, k1), z0, z1);
+  double* row = zb + (int64_t)r * n_blocks;
+  row[2 * i] = z0;
+  if (2 * i + 1 < n_blocks) row[2 * i + 1] = z1;
+}
+
+// k_white_pairs: out[r][t] += sigma[t] z(t, r) + ecorr[b(t)] zb[r][b(t)], one Philox call and
+// one Box-Muller per TOA pair (t even -> z0, t odd -> z1). grid (ceil(ceil(n_toa/2)/256), n_real).
+__global__ __launch_bounds__(256) void k_white_pairs(const double* __restrict__ sigma,
+                                                     const int32_t* __restrict__ block_of,
+                                                     const double* __restrict__ esig, const double* __restrict__ zb,
+                                                     int64_t n_blocks, double* __restrict__ out, int64_t ldo,
+                                                     int64_t n_toa, int64_t real0, uint32_t k0, uint32_t k1) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int r = blockIdx.y;
+  const int64_t t = 2 * i;
+  if (t >= n_toa) return;
+  double z[2] = {0.0, 0.0};
+  if (sigma) {
+    const u32x4 c = {(uint32_t)i, kWhitePsrWord, kWhiteStream, (uint32_t)(real0 + r)};
+    box_muller(philox4x32_10(c, k0, k1), z[0], z[1]);
+  }
+  double* orow = out + (int64_t)r * ldo;
+  const double* zbr = zb ? zb + (int64_t)r * n_blocks : nullptr;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int64_t tt = t + h;
+    if (tt >= n_toa) break;
+    double v = sigma ? sigma[tt] * z[h] : 0.0;
+    if (block_of) {
+      const int b = block_of[tt];
+      if (b >= 0) v = fma(esig[b], zbr[b], v);
+    }
+    orow[tt] += v;
+  }
+}
+
 // ----------------------------------------------------------------------------- k_checksums
 __global__ __launch_bounds__(256) void k_checksums(const double* __restrict__ out, int64_t ldo, int64_t n_toa,
                                                    double* __restrict__ sums) {
@@ -571,6 +704,28 @@ hipError_t launch_mix(hipStream_t st, const SegDesc& sd, int32_t P, int32_t R_pa
   dim3 grid((unsigned)((M + 255) / 256), (P + MIX_PT - 1) / MIX_PT);
   hipLaunchKernelGGL(k_mix, grid, dim3(256), 0, st, sd.L, sd.amp, P, M, R_pad, zbuf, coef, K, sd.col0,
                      x_out);
+  return hipGetLastError();
+}
+
+hipError_t launch_mix_tiled(hipStream_t st, const SegDesc& sd, int32_t P, int32_t R_pad, const double* zbuf,
+                            double* coef, int32_t K, double* x_out) {
+  const int64_t M = (int64_t)2 * sd.nm * R_pad;  // multiple of 256: R_pad is a multiple of 128
+  dim3 grid((unsigned)(M / MT_M), (P + MT_P - 1) / MT_P);
+  hipLaunchKernelGGL(k_mix_tiled, grid, dim3(256), 0, st, sd.L, sd.amp, P, M, R_pad, sd.l_lower, zbuf, coef, K,
+                     sd.col0, x_out);
+  return hipGetLastError();
+}
+
+hipError_t launch_white_batch(hipStream_t st, const double* sigma, const int32_t* block_of, const double* esig,
+                              int64_t n_blocks, double* zb, double* out, int64_t ldo, int64_t n_toa, int32_t n_real,
+                              int64_t real0, uint32_t k0, uint32_t k1) {
+  if (block_of && n_blocks > 0) {
+    hipLaunchKernelGGL(k_epoch_normals, dim3((unsigned)(((n_blocks + 1) / 2 + 255) / 256), n_real), dim3(256), 0, st,
+                       n_blocks, real0, k0, k1, zb);
+  }
+  hipLaunchKernelGGL(k_white_pairs, dim3((unsigned)(((n_toa + 1) / 2 + 255) / 256), n_real), dim3(256), 0, st,
+                     sigma, n_blocks > 0 ? block_of : nullptr, esig, n_blocks > 0 ? zb : nullptr, n_blocks, out, ldo,
+                     n_toa, real0, k0, k1);
   return hipGetLastError();
 }
 

@@ -283,6 +283,28 @@ def test_batch_split_invariance_bitwise(ctx):
     np.testing.assert_array_equal(full, again)
 
 
+@pytest.mark.parametrize("factor", ["cholesky", "svd"])
+def test_tiled_mix_vs_oracle(ctx, factor):
+    """P >= 64 takes the tiled GEMM mix (triangular when L is a Cholesky factor)."""
+    from fakepta_amd.batch import batch_factor
+    rng = np.random.default_rng(21)
+    P = 150
+    offs, toas, nu = random_layout(rng, P, (5, 40))
+    ctx.batch_set_toas(offs, toas, nu)
+    f, amp, _, pos = common_signal(rng, offs, toas, 17)
+    gam = O.orf_hd(pos) if factor == "cholesky" else O.orf_monopole(pos)
+    L = batch_factor(gam)
+    assert (np.allclose(L, np.tril(L)) if factor == "cholesky" else not np.allclose(L, np.tril(L)))
+    ctx.batch_add_signal(1, f, amp, idx=0.0, L=L)
+    f2, a2 = per_psr_signal(rng, offs, toas, 5)
+    ctx.batch_add_signal(0, f2, a2, idx=4.0)
+    segs = [O.Segment(1, 2 * np.pi * f, amp, 0.0, L=L), O.Segment(0, 2 * np.pi * f2, a2, 4.0)]
+    for real0, R in ((0, 130), (77, 5)):
+        got = ctx.batch_synth(31, real0, R)
+        want = O.batch_synth(offs, toas, nu, segs, 31, real0, R)
+        assert_parity(got, want, TOL)
+
+
 def test_checksums_device(ctx):
     rng = np.random.default_rng(9)
     _build(ctx, rng, P=4, white=True)
