@@ -44,6 +44,7 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=8, help="realizations timed for the CPU baseline (0: skip)")
     ap.add_argument("--path", type=int, default=0, help="synthesis path: 0 auto, 1 direct, 2 MFMA, 3 VALU")
     ap.add_argument("--anchor", type=int, default=0, help="recurrence re-anchor interval (0: library default)")
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL on ROCm) or gloo (CPU rehearsal)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-derived HBM bytes per synth launch (written by profiles/collect_pmc.py)")
     return ap.parse_args()
@@ -158,11 +159,16 @@ def cpu_baseline(sim, psrs, n_sample, seed):
 def main():
     args = parse()
     world, rank, local = dist_env()
-    comm = Comm(world, rank, local)
     from fakepta_amd import _capi
     from fakepta_amd.batch import BatchSimulator
 
-    ctx = _capi.Context(local)
+    # one process per GPU; local ranks beyond the visible devices wrap (rehearsal of several ranks on
+    # one card with --dist-backend gloo; the driver's N-GPU runs have one rank per device)
+    ndev = max(1, _capi.device_count())
+    device = local % ndev
+    os.environ["FAKEPTA_AMD_DEVICE"] = str(device)  # the drop-in calls of build_c2 use the same card
+    comm = Comm(world, rank, device, backend=args.dist_backend)
+    ctx = _capi.Context(device)
     psrs = build_c2(args.npsr, args.ntoa)
     sim = BatchSimulator(psrs, white=False, ctx=ctx)
     info = ctx.batch_info()
