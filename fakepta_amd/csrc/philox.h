@@ -36,8 +36,10 @@ __device__ __forceinline__ void box_muller(u32x4 v, double& z0, double& z1) {
   const double u1 = (double)((a >> 11) + 1ull) * 0x1.0p-53;
   const double u2 = (double)(b >> 11) * 0x1.0p-53;
   const double r = sqrt(-2.0 * log(u1));
+  // cos/sin(2 pi u2) as sincospi(2 u2): the argument is already reduced, so this skips the general
+  // range reduction; equal to the oracle's np.cos(2*pi*u2) to ~1 ulp of the unit-circle value
   double s, c;
-  sincos(6.283185307179586 * u2, &s, &c);
+  sincospi(2.0 * u2, &s, &c);
   z0 = r * c;
   z1 = r * s;
 }
