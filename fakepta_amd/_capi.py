@@ -33,6 +33,8 @@ _SIGS = [
     ("fpta_last_error", ctypes.c_char_p, [_ctx_p]),
     ("fpta_device_count", _c_int, [ctypes.POINTER(_c_int)]),
     ("fpta_gp_accumulate", _c_int, [_ctx_p, _i64, _vp, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _dbl, _vp]),
+    ("fpta_gp_accumulate_array", _c_int, [_ctx_p, _i32, _vp, _vp, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                          _dbl, _vp]),
     ("fpta_common_accumulate", _c_int, [_ctx_p, _i32, _vp, _vp, _vp, _i32, _vp, _vp, _dbl, _dbl, _vp, _vp, _vp,
                                         _vp]),
     ("fpta_white_accumulate", _c_int, [_ctx_p, _i64, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp]),
@@ -124,6 +126,31 @@ class Context:
         self._check(_lib.fpta_gp_accumulate(self._h, n, _ptr(toas), _ptr(nu), len(segments), _ptr(nm), _ptr(f),
                                             _ptr(cc), _ptr(cs), _ptr(idx), _ptr(ff), _ptr(m), float(sign),
                                             _ptr(residuals)), "fpta_gp_accumulate")
+
+    def gp_accumulate_array(self, offs, toas, nu, segments, residuals, sign=1.0, masks=None):
+        """Array form: segments = list of (f [P, N], ccos [P, N], csin [P, N], idx, freqf);
+        masks: None or list (per segment) of None / bool [n_toa_total]. residuals updated in place."""
+        offs = np.ascontiguousarray(offs, dtype=np.int64)
+        toas, nu = _f64(toas), _f64(nu)
+        P, n = len(offs) - 1, int(offs[-1])
+        assert residuals.dtype == np.float64 and residuals.flags.c_contiguous and len(residuals) == n
+        for s in segments:
+            assert np.shape(s[0]) == np.shape(s[1]) == np.shape(s[2]) and np.shape(s[0])[0] == P
+        nm = np.array([np.shape(s[0])[1] for s in segments], dtype=np.int32)
+        f = _f64(np.concatenate([np.asarray(s[0], float).ravel() for s in segments]))
+        cc = _f64(np.concatenate([np.asarray(s[1], float).ravel() for s in segments]))
+        cs = _f64(np.concatenate([np.asarray(s[2], float).ravel() for s in segments]))
+        idx = _f64([s[3] for s in segments])
+        ff = _f64([s[4] for s in segments])
+        m = None
+        if masks is not None and any(x is not None for x in masks):
+            m = np.ones((len(segments), n), dtype=np.uint8)
+            for i, x in enumerate(masks):
+                if x is not None:
+                    m[i] = np.asarray(x, dtype=bool)
+        self._check(_lib.fpta_gp_accumulate_array(self._h, P, _ptr(offs), _ptr(toas), _ptr(nu), len(segments),
+                                                  _ptr(nm), _ptr(f), _ptr(cc), _ptr(cs), _ptr(idx), _ptr(ff), _ptr(m),
+                                                  float(sign), _ptr(residuals)), "fpta_gp_accumulate_array")
 
     def common_accumulate(self, offs, toas, nu, f, amp, idx, freqf, L, z, residuals, want_x=True):
         offs = np.ascontiguousarray(offs, dtype=np.int64)

@@ -14,6 +14,7 @@ import numpy as np
 from . import _capi
 from . import spectrum as _spectrum_module
 from .fake_pta import Pulsar  # noqa: F401  (reference module namespace)
+from .fake_pta import reconstruct_array
 
 spec = {name: fn for name, fn in inspect.getmembers(_spectrum_module, inspect.isfunction)
         if name in _spectrum_module.__all__}
@@ -154,9 +155,12 @@ def add_common_correlated_noise(psrs, orf='hd', spectrum='powerlaw', name='gw', 
     else:
         raise ValueError(f'unknown spectrum {spectrum!r}')
     n_modes = len(f_psd)
+    # replace-on-reinject (correlated_noises.py:133-134), all pulsars in one GPU launch
+    if any(signal_name in p.signal_model for p in psrs):
+        old = reconstruct_array(psrs, [signal_name])
+        for p, r in zip(psrs, old):
+            p.residuals -= r
     for p in psrs:
-        if signal_name in p.signal_model:  # replace-on-reinject
-            p.residuals -= p.reconstruct_signal(signals=[signal_name])
         p.signal_model[signal_name] = {'orf': orf, 'spectrum': spectrum, 'hmap': h_map, 'f': f_psd, 'psd': psd,
                                        'fourier': np.zeros((2, n_modes)), 'nbin': n_modes, 'idx': idx}
     amp0 = np.sqrt(np.repeat(psd, 2))[0::2]           # coeffs[2i] of correlated_noises.py:147

@@ -584,35 +584,49 @@ int fpta_gp_accumulate(fpta_ctx* c, int64_t n_toa, const double* toas, const dou
                        const double* seg_idx, const double* seg_freqf, const uint8_t* mask, double sign,
                        double* residuals) {
   if (!c) return fail(nullptr, FPTA_EINVAL, "null ctx");
-  if (n_toa <= 0 || n_seg <= 0 || !toas || !nu || !seg_nmodes || !f || !ccos || !csin || !seg_idx ||
+  const int64_t offs[2] = {0, n_toa};
+  return fpta_gp_accumulate_array(c, 1, offs, toas, nu, n_seg, seg_nmodes, f, ccos, csin, seg_idx, seg_freqf, mask,
+                                  sign, residuals);
+}
+
+int fpta_gp_accumulate_array(fpta_ctx* c, int32_t n_psr, const int64_t* offs, const double* toas, const double* nu,
+                             int32_t n_seg, const int32_t* seg_nmodes, const double* f, const double* ccos,
+                             const double* csin, const double* seg_idx, const double* seg_freqf, const uint8_t* mask,
+                             double sign, double* residuals) {
+  if (!c) return fail(nullptr, FPTA_EINVAL, "null ctx");
+  if (n_psr <= 0 || !offs || n_seg <= 0 || !toas || !nu || !seg_nmodes || !f || !ccos || !csin || !seg_idx ||
       !seg_freqf || !residuals)
     return fail(c, FPTA_EINVAL, "gp_accumulate: bad arguments");
   HIPCHK(c, hipSetDevice(c->device), "hipSetDevice");
   Layout& L = c->scratch;
-  const int64_t offs[2] = {0, n_toa};
-  int rc = layout_set_toas(c, L, 1, offs, toas, nu);
+  int rc = layout_set_toas(c, L, n_psr, offs, toas, nu);
   if (rc) return rc;
+  const int64_t n_toa = offs[n_psr];
   int64_t m0 = 0, nmax = 0;
   for (int32_t s = 0; s < n_seg; ++s) {
     const int32_t nm = seg_nmodes[s];
     if (nm <= 0) return fail(c, FPTA_EINVAL, "gp_accumulate: segment with no modes");
-    std::vector<double> amp(nm, sign);  // coefficient = sign * (ccos, csin) through the from-z path
+    // coefficient = sign * (ccos, csin) through the from-z path (amplitude = sign, exact)
+    std::vector<double> amp((size_t)n_psr * nm, sign);
     rc = layout_add_signal(c, L, 0, nm, f + m0, amp.data(), seg_idx[s], seg_freqf[s], nullptr,
                            mask ? mask + (size_t)s * n_toa : nullptr);
     if (rc < 0) return rc;
-    m0 += nm;
+    m0 += (int64_t)n_psr * nm;
     nmax = std::max<int64_t>(nmax, nm + (nm & 1));
   }
   if ((rc = layout_finalize(c, L))) return rc;
-  // z [1][n_seg][1][nmax][2] = (ccos, csin)
-  std::vector<double> z((size_t)n_seg * nmax * 2, 0.0);
+  // z [1][n_seg][n_psr][nmax][2] = (ccos, csin)
+  std::vector<double> z((size_t)n_seg * n_psr * nmax * 2, 0.0);
   m0 = 0;
   for (int32_t s = 0; s < n_seg; ++s) {
-    for (int32_t k = 0; k < seg_nmodes[s]; ++k) {
-      z[((size_t)s * nmax + k) * 2] = ccos[m0 + k];
-      z[((size_t)s * nmax + k) * 2 + 1] = csin[m0 + k];
-    }
-    m0 += seg_nmodes[s];
+    const int32_t nm = seg_nmodes[s];
+    for (int32_t p = 0; p < n_psr; ++p)
+      for (int32_t k = 0; k < nm; ++k) {
+        const size_t dst = (((size_t)s * n_psr + p) * nmax + k) * 2;
+        z[dst] = ccos[m0 + (size_t)p * nm + k];
+        z[dst + 1] = csin[m0 + (size_t)p * nm + k];
+      }
+    m0 += (int64_t)n_psr * nm;
   }
   if ((rc = upload(c, c->zin, z.data(), sizeof(double) * z.size(), "gp_accumulate z"))) return rc;
   if ((rc = run_coefficients(c, L, 0, 0, 1, kRealPad, c->zin.as<double>(), (int32_t)nmax, nullptr))) return rc;

@@ -450,6 +450,60 @@ class Pulsar:
                 self.noisedict.pop(key)
 
 
+def reconstruct_array(psrs, signals=None, freqf=1400):
+    """reconstruct_signal (fake_pta.py:526-555, GP branches) for a whole array in ONE GPU launch.
+    Returns the list of per-pulsar time series. A pulsar that lacks a requested signal contributes
+    zero for it; pulsars may have different mode counts. (The CW branch is per pulsar: use
+    Pulsar.reconstruct_signal for 'cgw'.)"""
+    if signals is None:
+        signals = []
+        for p in psrs:
+            signals += [s for s in p.signal_model if s not in signals]
+    offs = np.concatenate([[0], np.cumsum([len(p.toas) for p in psrs])]).astype(np.int64)
+    P = len(psrs)
+    segs, masks = [], []
+    for signal in signals:
+        gp = signal in _GP_SIGNALS or 'common' in signal
+        sysn = 'system_noise' in signal
+        if not (gp or sysn):
+            continue
+        have = [p.signal_model[signal] if signal in p.signal_model else None for p in psrs]
+        nm = max((len(sm['f']) for sm in have if sm is not None), default=0)
+        if nm == 0:
+            continue
+        f = np.zeros((P, nm))
+        cc = np.zeros((P, nm))
+        cs = np.zeros((P, nm))
+        idx = None
+        for i, sm in enumerate(have):
+            if sm is None:
+                f[i] = np.arange(1, nm + 1) / max(psrs[i].Tspan, 1.0)
+                continue
+            fi = np.asarray(sm['f'], float)
+            df = _df(fi)
+            f[i, :len(fi)] = fi
+            if len(fi) < nm:  # zero-amplitude continuation of the grid
+                f[i, len(fi):] = fi[-1] + fi[0] * np.arange(1, nm - len(fi) + 1)
+            cc[i, :len(fi)] = df * sm['fourier'][0]
+            cs[i, :len(fi)] = df * sm['fourier'][1]
+            idx = float(sm['idx']) if idx is None else idx
+            if float(sm['idx']) != idx:
+                raise ValueError(f'signal {signal!r} has different chromatic indices across pulsars')
+        if gp:
+            segs.append((f, cc, cs, idx, float(freqf)))
+            masks.append(None)
+        if sysn:
+            backend = signal.split('system_noise_')[1]
+            segs.append((f, cc, cs, 0.0, float(freqf)))
+            masks.append(np.concatenate([p.backend_flags == backend for p in psrs]))
+    out = np.zeros(int(offs[-1]))
+    if segs:
+        _capi.get_context().gp_accumulate_array(offs, np.concatenate([p.toas for p in psrs]),
+                                                np.concatenate([p.freqs for p in psrs]), segs, out,
+                                                masks=masks if any(m is not None for m in masks) else None)
+    return [out[offs[i]:offs[i + 1]].copy() for i in range(P)]
+
+
 def make_fake_array(npsrs=25, Tobs=None, ntoas=None, gaps=True, toaerr=None, pdist=None, freqs=[1400],
                     isotropic=False, backends=None, noisedict=None, custom_model=None, ephem=None):
     """Build an array of fake pulsars and inject white, red, DM and chromatic noise

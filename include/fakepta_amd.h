@@ -65,6 +65,16 @@ int fpta_gp_accumulate(fpta_ctx* ctx, int64_t n_toa, const double* toas, const d
                        const double* seg_freqf, const uint8_t* mask, double sign,
                        double* residuals);
 
+/* Array form of fpta_gp_accumulate (one launch for a whole array): replaces the per-pulsar
+ * reconstruct_signal calls of correlated_noises.py:133-134 (replace-on-reinject) and of
+ * remove_signal (fake_pta.py:557-567) over many pulsars. n_psr pulsars (CSR offs[n_psr+1]);
+ * segment s has seg_nmodes[s] modes and contributes f/ccos/csin blocks of [n_psr][seg_nmodes[s]]
+ * (concatenated over segments). mask: NULL or uint8 [n_seg][n_toa_total]. residuals [n_toa_total]. */
+int fpta_gp_accumulate_array(fpta_ctx* ctx, int32_t n_psr, const int64_t* offs, const double* toas,
+                             const double* nu, int32_t n_seg, const int32_t* seg_nmodes, const double* f,
+                             const double* ccos, const double* csin, const double* seg_idx,
+                             const double* seg_freqf, const uint8_t* mask, double sign, double* residuals);
+
 /* Replaces fakepta/correlated_noises.py:146-160 (add_common_correlated_noise hot loop).
  * n_psr pulsars, CSR offsets offs[n_psr+1] into toas/nu (seconds / MHz).
  * For mode k: x_sin = L z[k][0], x_cos = L z[k][1] (z in the reference's draw order,

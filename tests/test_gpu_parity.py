@@ -124,6 +124,33 @@ def test_dropin_common_vs_reference(golden, orf):
                   TOL)
 
 
+def test_reconstruct_array_and_common_reinject():
+    """One-launch array reconstruct == per-pulsar reconstruct_signal; re-injecting a common signal
+    replaces it (correlated_noises.py:133-134)."""
+    from fakepta_amd import correlated_noises as cn
+    from fakepta_amd import fake_pta as fp
+    np.random.seed(12)
+    psrs = fp.make_fake_array(npsrs=9, Tobs=None, ntoas=80, gaps=True, toaerr=1e-7, isotropic=False,
+                              backends=["A.1400", "B.800"], custom_model={"RN": 20, "DM": 35, "Sv": None})
+    psrs[3].custom_model = {"RN": 7, "DM": None, "Sv": 12}
+    psrs[3].add_chromatic_noise(log10_A=-13.5, gamma=2.0)
+    psrs[4].add_system_noise(backend="B.800", components=9, log10_A=-13.2, gamma=3.0)
+    cn.add_common_correlated_noise(psrs, orf="hd", log10_A=-14.0, gamma=13 / 3, components=25)
+    sigs = ["red_noise", "dm_gp", "chrom_gp", "gw_common", "B.800_system_noise_B.800"]
+    arr = fp.reconstruct_array(psrs, sigs)
+    for p, r in zip(psrs, arr):
+        own = [s for s in sigs if s in p.signal_model]
+        assert_parity(r, p.reconstruct_signal(own), 1e-12)
+    for p in psrs:
+        p.make_ideal()
+    cn.add_common_correlated_noise(psrs, orf="dipole", log10_A=-14.0, gamma=13 / 3, components=10)
+    cn.add_common_correlated_noise(psrs, orf="hd", log10_A=-13.7, gamma=4.0, components=10)
+    rec = fp.reconstruct_array(psrs, ["gw_common"])
+    scale = max(np.abs(p.residuals).max() for p in psrs)
+    for p, r in zip(psrs, rec):
+        np.testing.assert_allclose(p.residuals, r, rtol=0, atol=1e-11 * scale)
+
+
 @pytest.mark.parametrize("fixture,kwargs", [
     ("g4_make_fake_array.npz", dict(seed=0, npsrs=25, Tobs=10, ntoas=1000, isotropic=True, gaps=True, toaerr=1e-7,
                                     backends="NUPPI.1400", custom_model={"RN": 30, "DM": None, "Sv": None})),
