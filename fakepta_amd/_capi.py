@@ -47,6 +47,7 @@ _SIGS = [
     ("fpta_batch_download", _c_int, [_ctx_p, _i32, _i32, _vp]),
     ("fpta_batch_device_out", _c_int, [_ctx_p, ctypes.POINTER(_vp), ctypes.POINTER(_i64), ctypes.POINTER(_i32)]),
     ("fpta_batch_checksums", _c_int, [_ctx_p, _vp]),
+    ("fpta_batch_correlations", _c_int, [_ctx_p, _i32, _vp]),
     ("fpta_batch_info", _c_int, [_ctx_p, _vp]),
     ("fpta_set_option", _c_int, [_ctx_p, _i32, _i64]),
     ("fpta_kernel_stats", _c_int, [_ctx_p, _i32, ctypes.POINTER(_i64), ctypes.POINTER(_dbl)]),
@@ -242,6 +243,16 @@ class Context:
         self._check(_lib.fpta_batch_device_out(self._h, ctypes.byref(p), ctypes.byref(ld), ctypes.byref(nr)),
                     "fpta_batch_device_out")
         return p.value, ld.value, nr.value
+
+    def batch_correlations(self, mode=2):
+        """0: [R, P, P] per realization; 1: [P, P] sum; 2: [P, P] sum of normalized; 3: [R, P] autos."""
+        info = self.batch_info()
+        _, _, R = self.batch_device_out()
+        P = info["n_psr"]
+        shape = {0: (R, P, P), 1: (P, P), 2: (P, P), 3: (R, P)}[mode]
+        out = np.empty(shape)
+        self._check(_lib.fpta_batch_correlations(self._h, int(mode), _ptr(out)), "fpta_batch_correlations")
+        return out
 
     def batch_checksums(self):
         _, _, nr = self.batch_device_out()

@@ -15,7 +15,7 @@ the oracle (oracle/fakepta_oracle.py: batch_synth) restates the exact semantics.
 import numpy as np
 
 from . import _capi
-from .correlated_noises import orf_factor, orf_matrix
+from .correlated_noises import bin_curve, orf_factor, orf_matrix
 
 GP_NAMES = ("red_noise", "dm_gp", "chrom_gp")
 
@@ -135,6 +135,29 @@ class BatchSimulator:
     def synth_from_z(self, z):
         """Validation mode: z [n_real, n_seg, P, N_max, 2] standard normals (cos, sin)."""
         return self.ctx.batch_synth_from_z(z)
+
+    def correlations(self, normalized=True):
+        """Mean over the last block's realizations of the zero-lag cross-correlation matrix
+        dot(res_a, res_b)/n (correlated_noises.py:14-19), normalized per realization by the
+        auto-correlations if `normalized`. Computed on device; pulsars must share the TOA count."""
+        _, _, R = self.ctx.batch_device_out()
+        return self.ctx.batch_correlations(2 if normalized else 1) / R
+
+    def hd_curve(self, bins=10, estimator="ratio"):
+        """(mean, std, bin centres) of the pairwise correlations against angular separation
+        (correlated_noises.py:21-47) for the last block. estimator "ratio": mean cross-power over
+        sqrt(mean auto-powers) (consistent); "per_realization": mean of per-realization normalized
+        correlations (biased toward 0 by O(1/n_eff) for red processes)."""
+        if estimator == "ratio":
+            C = self.correlations(normalized=False)
+            d = np.sqrt(np.diag(C))
+            C = C / np.outer(d, d)
+        else:
+            C = self.correlations(normalized=True)
+        pos = np.array([p.pos for p in self.psrs])
+        iu = np.triu_indices(len(self.psrs), 1)
+        angles = np.arccos(np.clip(pos @ pos.T, -1.0, 1.0))[iu]
+        return bin_curve(C[iu], angles, bins)
 
     def checksums(self):
         """Per-realization (sum, sum of squares) of the last block, computed on device."""

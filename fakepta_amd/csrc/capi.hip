@@ -93,7 +93,7 @@ struct fpta_ctx {
   std::string err;
   Layout batch, scratch;
   // batch white noise
-  DevBuf sigma, block_of, esig, zb_epochs;
+  DevBuf sigma, block_of, esig, zb_epochs, corr_autos, corr_parts, corr_dst;
   bool has_sigma = false, has_blocks = false;
   int64_t n_blocks = 0;
   // work buffers
@@ -863,6 +863,34 @@ int fpta_batch_checksums(fpta_ctx* c, double* sums) {
   HIPCHK(c, hipMemcpyAsync(sums, c->sums.p, sizeof(double) * 2 * c->out_R, hipMemcpyDeviceToHost, c->stream),
          "sums download");
   HIPCHK(c, hipStreamSynchronize(c->stream), "checksums sync");
+  return FPTA_OK;
+}
+
+int fpta_batch_correlations(fpta_ctx* c, int32_t mode, double* out) {
+  if (!c || !out || mode < 0 || mode > 3) return fail(c, FPTA_EINVAL, "correlations: bad arguments");
+  if (!c->out_R) return fail(c, FPTA_ESTATE, "correlations: nothing synthesized yet");
+  const Layout& L = c->batch;
+  const int32_t P = L.P;
+  const int64_t n = L.h_offs[1] - L.h_offs[0];
+  for (int32_t p = 0; p < P; ++p)
+    if (L.h_offs[p + 1] - L.h_offs[p] != n)
+      return fail(c, FPTA_EINVAL, "correlations: every pulsar must have the same number of TOAs");
+  if (n > 0x7FFFFFFF || c->out_R > 65535) return fail(c, FPTA_EINVAL, "correlations: block too large");
+  HIPCHK(c, hipSetDevice(c->device), "hipSetDevice");
+  const int32_t R = c->out_R;
+  const int32_t nparts = std::min<int32_t>(R, 256);
+  const size_t pp = (size_t)P * P;
+  size_t dst_len = mode == 0 ? (size_t)R * pp : mode == 3 ? (size_t)R * P : pp;
+  HIPCHK(c, c->corr_autos.ensure(sizeof(double) * (size_t)R * P), "autos alloc");
+  HIPCHK(c, c->corr_parts.ensure(sizeof(double) * (size_t)nparts * pp), "parts alloc");
+  HIPCHK(c, c->corr_dst.ensure(sizeof(double) * dst_len), "corr alloc");
+  double* dst = mode == 3 ? c->corr_autos.as<double>() : c->corr_dst.as<double>();
+  HIPCHK(c,
+         launch_correlations(c->stream, c->out.as<double>(), c->out_ld, (int32_t)n, P, R, mode,
+                             c->corr_autos.as<double>(), c->corr_parts.as<double>(), nparts, dst),
+         "k_xcorr launch");
+  HIPCHK(c, hipMemcpyAsync(out, dst, sizeof(double) * dst_len, hipMemcpyDeviceToHost, c->stream), "corr download");
+  HIPCHK(c, hipStreamSynchronize(c->stream), "corr sync");
   return FPTA_OK;
 }
 

@@ -83,6 +83,8 @@ hipError_t launch_white(hipStream_t st, const double* sigma, const int32_t* bloc
                         int32_t n_real, int64_t real0, uint32_t k0, uint32_t k1);
 hipError_t launch_checksums(hipStream_t st, const double* out, int64_t ldo, int64_t n_toa, int32_t n_real,
                             double* sums);
+hipError_t launch_correlations(hipStream_t st, const double* out, int64_t ldo, int32_t n, int32_t P, int32_t n_real,
+                               int32_t mode, double* autos, double* parts, int32_t nparts, double* dst);
 hipError_t launch_philox(hipStream_t st, int64_t n, const uint32_t* ctr, uint32_t k0, uint32_t k1,
                          uint32_t* out);
 

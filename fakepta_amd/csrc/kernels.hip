@@ -648,6 +648,127 @@ __global__ __launch_bounds__(256) void k_white_pairs(const double* __restrict__ 
   }
 }
 
+// ----------------------------------------------------------------------------- correlation statistics
+// The estimator of correlated_noises.py:14-34 on device, for arrays whose pulsars share the TOA
+// count n: C_r[a][b] = sum_t x_r[a][t] x_r[b][t] / n per realization r of the last block.
+// k_autos: auto[r][p] = C_r[p][p]. grid (P, n_real), one block per (pulsar, realization).
+__global__ __launch_bounds__(256) void k_autos(const double* __restrict__ out, int64_t ldo, int32_t n,
+                                               double* __restrict__ autos, int32_t P) {
+  __shared__ double red[256];
+  const int p = blockIdx.x, r = blockIdx.y;
+  const double* x = out + (int64_t)r * ldo + (int64_t)p * n;
+  double s = 0.0;
+  for (int t = threadIdx.x; t < n; t += 256) s = fma(x[t], x[t], s);
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) autos[(int64_t)r * P + p] = red[0] / n;
+}
+
+// k_xcorr: 64 x 64 tiles (ta <= tb) of C_r, 4 x 4 outputs per thread, TOA chunks of 32 staged in LDS.
+// mode 0: write C_r per realization [n_real][P][P]; mode 1: accumulate sum_r C_r; mode 2: accumulate
+// sum_r C_r[a][b] / sqrt(auto_r[a] auto_r[b]). Modes 1/2 loop over `rper` realizations per block and
+// write one partial [chunk][P][P] (summed in a fixed order afterwards: deterministic).
+constexpr int XC_T = 64, XC_K = 32;
+__global__ __launch_bounds__(256) void k_xcorr(const double* __restrict__ out, int64_t ldo, int32_t n, int32_t P,
+                                               int32_t n_real, int32_t mode, int32_t rper,
+                                               const double* __restrict__ autos, double* __restrict__ dst) {
+  __shared__ double Xa[XC_K][XC_T + 1];
+  __shared__ double Xb[XC_K][XC_T + 1];
+  // decode the upper-triangular tile pair
+  const int nt = (P + XC_T - 1) / XC_T;
+  int pair = blockIdx.x, ta = 0;
+  while (pair >= nt - ta) {
+    pair -= nt - ta;
+    ++ta;
+  }
+  const int tb = ta + pair;
+  const int a0 = ta * XC_T, b0 = tb * XC_T;
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  const int rbeg = blockIdx.y * rper, rend = min(n_real, rbeg + rper);
+  double tot[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) tot[i][j] = 0.0;
+  for (int r = rbeg; r < rend; ++r) {
+    const double* xr = out + (int64_t)r * ldo;
+    double acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = 0.0;
+    for (int t0 = 0; t0 < n; t0 += XC_K) {
+      __syncthreads();
+      for (int e = threadIdx.x; e < XC_T * XC_K; e += 256) {
+        const int row = e / XC_K, k = e % XC_K;
+        const int t = t0 + k;
+        Xa[k][row] = (a0 + row < P && t < n) ? xr[(int64_t)(a0 + row) * n + t] : 0.0;
+        Xb[k][row] = (b0 + row < P && t < n) ? xr[(int64_t)(b0 + row) * n + t] : 0.0;
+      }
+      __syncthreads();
+#pragma unroll 4
+      for (int k = 0; k < XC_K; ++k) {
+        double av[4], bv[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          av[i] = Xa[k][ty + 16 * i];
+          bv[i] = Xb[k][tx + 16 * i];
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = fma(av[i], bv[j], acc[i][j]);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int a = a0 + ty + 16 * i;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int b = b0 + tx + 16 * j;
+        if (a >= P || b >= P) continue;
+        const double c = acc[i][j] / n;
+        if (mode == 0) {
+          dst[((int64_t)r * P + a) * P + b] = c;
+          dst[((int64_t)r * P + b) * P + a] = c;
+        } else if (mode == 1) {
+          tot[i][j] += c;
+        } else {
+          tot[i][j] += c / sqrt(autos[(int64_t)r * P + a] * autos[(int64_t)r * P + b]);
+        }
+      }
+    }
+  }
+  if (mode != 0) {
+    double* part = dst + (int64_t)blockIdx.y * P * P;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int a = a0 + ty + 16 * i;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int b = b0 + tx + 16 * j;
+        if (a >= P || b >= P) continue;
+        part[(int64_t)a * P + b] = tot[i][j];
+        part[(int64_t)b * P + a] = tot[i][j];
+      }
+    }
+  }
+}
+
+// sum of `nparts` [P*P] partials in index order (deterministic)
+__global__ __launch_bounds__(256) void k_sum_parts(const double* __restrict__ parts, int32_t nparts, int64_t len,
+                                                   double* __restrict__ res) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= len) return;
+  double s = 0.0;
+  for (int c = 0; c < nparts; ++c) s += parts[(int64_t)c * len + i];
+  res[i] = s;
+}
+
 // ----------------------------------------------------------------------------- k_checksums
 __global__ __launch_bounds__(256) void k_checksums(const double* __restrict__ out, int64_t ldo, int64_t n_toa,
                                                    double* __restrict__ sums) {
@@ -794,6 +915,26 @@ hipError_t launch_white(hipStream_t st, const double* sigma, const int32_t* bloc
   dim3 grid((unsigned)((n_toa + 255) / 256), n_real);
   hipLaunchKernelGGL(k_white, grid, dim3(256), 0, st, sigma, block_of, esig, z, zb, out, ldo, n_toa, real0,
                      k0, k1);
+  return hipGetLastError();
+}
+
+hipError_t launch_correlations(hipStream_t st, const double* out, int64_t ldo, int32_t n, int32_t P, int32_t n_real,
+                               int32_t mode, double* autos, double* parts, int32_t nparts, double* dst) {
+  if (mode == 2 || mode == 3) {
+    hipLaunchKernelGGL(k_autos, dim3(P, n_real), dim3(256), 0, st, out, ldo, n, autos, P);
+    if (mode == 3) return hipGetLastError();
+  }
+  const int nt = (P + XC_T - 1) / XC_T;
+  const int npairs = nt * (nt + 1) / 2;
+  if (mode == 0) {
+    hipLaunchKernelGGL(k_xcorr, dim3(npairs, n_real), dim3(256), 0, st, out, ldo, n, P, n_real, 0, 1, autos, dst);
+  } else {
+    const int rper = (n_real + nparts - 1) / nparts;
+    hipLaunchKernelGGL(k_xcorr, dim3(npairs, nparts), dim3(256), 0, st, out, ldo, n, P, n_real, mode, rper, autos,
+                       parts);
+    const int64_t len = (int64_t)P * P;
+    hipLaunchKernelGGL(k_sum_parts, dim3((unsigned)((len + 255) / 256)), dim3(256), 0, st, parts, nparts, len, dst);
+  }
   return hipGetLastError();
 }
 

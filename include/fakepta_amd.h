@@ -142,6 +142,15 @@ int fpta_batch_device_out(fpta_ctx* ctx, double** dptr, int64_t* ld, int32_t* n_
 /* Per-realization sum and sum of squares of the last block, computed on device
  * (deterministic order). sums: host [n_real][2]. */
 int fpta_batch_checksums(fpta_ctx* ctx, double* sums);
+/* Correlation statistics of the last block, the estimator of
+ * fakepta/correlated_noises.py:14-34 (C_r[a][b] = dot(res_a, res_b) / n) for arrays whose pulsars
+ * all have n TOAs (FPTA_EINVAL otherwise):
+ *   mode 0: host out [n_real][P][P], C_r per realization
+ *   mode 1: host out [P][P], sum over realizations of C_r
+ *   mode 2: host out [P][P], sum over realizations of C_r[a][b] / sqrt(C_r[a][a] C_r[b][b])
+ *   mode 3: host out [n_real][P], auto-correlations C_r[p][p]
+ * Sums are formed in a fixed order (bitwise reproducible). */
+int fpta_batch_correlations(fpta_ctx* ctx, int32_t mode, double* out);
 /* info[0]=n_psr info[1]=n_toa_total info[2]=n_seg info[3]=K columns info[4]=max toas/pulsar */
 int fpta_batch_info(fpta_ctx* ctx, int64_t* info);
 

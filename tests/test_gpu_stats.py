@@ -80,6 +80,53 @@ def test_hellings_downs_recovered(ctx):
         assert abs(rho[iu][sel].mean() - gam[iu][sel].mean()) < 0.03
 
 
+def test_device_correlations_match_numpy(ctx):
+    """fpta_batch_correlations (all modes) == numpy on the same block (deterministic sums)."""
+    rng = np.random.default_rng(4)
+    P, n, R = 70, 150, 40
+    offs = np.arange(P + 1) * n
+    toas = np.tile(np.sort(rng.uniform(0, 3e8, n)), P)
+    ctx.batch_set_toas(offs, toas, np.full(P * n, 1400.0))
+    v = rng.normal(size=(P, 3))
+    f = O.freq_grid(20, 3e8)
+    ctx.batch_add_signal(1, f, np.sqrt(O.powerlaw(f, -14, 4.0) * O.delta_f(f)), L=O.mvn_factor(
+        O.orf_hd(v / np.linalg.norm(v, axis=1)[:, None])))
+    ctx.batch_set_white(np.full(P * n, 1e-7))
+    out = ctx.batch_synth(8, 0, R).reshape(R, P, n)
+    C = np.einsum("rat,rbt->rab", out, out) / n
+    scale = np.abs(C).max()
+    np.testing.assert_allclose(ctx.batch_correlations(0), C, rtol=1e-12, atol=1e-13 * scale)
+    np.testing.assert_allclose(ctx.batch_correlations(1), C.sum(0), rtol=1e-12, atol=1e-13 * scale * R)
+    d = np.sqrt(np.einsum("raa->ra", C))
+    np.testing.assert_allclose(ctx.batch_correlations(3), d ** 2, rtol=1e-12)
+    np.testing.assert_allclose(ctx.batch_correlations(2), (C / (d[:, :, None] * d[:, None, :])).sum(0),
+                               rtol=1e-11, atol=1e-12 * R)
+    np.testing.assert_array_equal(ctx.batch_correlations(2), ctx.batch_correlations(2))
+
+
+def test_hd_curve_on_device():
+    """BatchSimulator.hd_curve recovers Hellings-Downs from on-device statistics."""
+    from fakepta_amd import correlated_noises as cn
+    from fakepta_amd import fake_pta as fp
+    from fakepta_amd.batch import BatchSimulator
+    np.random.seed(2)
+    psrs = fp.make_fake_array(npsrs=50, Tobs=10, ntoas=300, gaps=False, isotropic=True, toaerr=1e-7,
+                              backends="X.1400", custom_model={"RN": None, "DM": None, "Sv": None})
+    cn.add_common_correlated_noise(psrs, orf="hd", log10_A=-14, gamma=13 / 3, components=30)
+    sim = BatchSimulator(psrs, white=False)
+    sim.synth(2048, seed=11, to_host=False)
+    mean, std, centres = sim.hd_curve(bins=8)
+    pos = np.array([p.pos for p in psrs])
+    gam = O.orf_hd(pos)
+    iu = np.triu_indices(len(psrs), 1)
+    ang = np.arccos(np.clip(pos @ pos.T, -1, 1))[iu]
+    edges = np.linspace(0, np.pi, 9)
+    for k in range(8):
+        sel = (ang > edges[k]) & (ang < edges[k + 1])
+        if sel.sum() >= 5:
+            assert abs(mean[k] - gam[iu][sel].mean()) < 0.03
+
+
 def test_white_and_ecorr_covariance(ctx):
     n, R = 400, 20000
     rng = np.random.default_rng(1)
