@@ -62,7 +62,7 @@ for _name, _res, _args in _SIGS:
 
 EXPORTED = [s[0] for s in _SIGS]
 
-OPT_SYNTH_PATH, OPT_MFMA_MIN_REAL, OPT_PROFILE, OPT_ANCHOR, OPT_VALU_VARIANT = 1, 2, 3, 4, 5
+OPT_SYNTH_PATH, OPT_MFMA_MIN_REAL, OPT_PROFILE, OPT_ANCHOR, OPT_VALU_VARIANT, OPT_FUSE_WHITE = 1, 2, 3, 4, 5, 6
 K_GEN, K_MIX, K_SYNTH, K_WHITE = 0, 1, 2, 3
 
 

@@ -107,6 +107,7 @@ struct fpta_ctx {
   int profile = 0;
   int anchor = 0;  // 0: phasor recurrence anchored once per segment
   int valu_variant = 1;  // seeded (MT 2, NT 16): fastest on C2 (profiles/r01_sweep_*.txt)
+  int fuse_white = 1;    // add white/ECORR in the seeded kernel's epilogue
   // profiling
   struct Pending {
     int which;
@@ -380,8 +381,22 @@ int build_tiles(fpta_ctx* c, Layout& L, int32_t R, int32_t tile_toa, int32_t til
   return FPTA_OK;
 }
 
+// White noise + ECORR to fuse into the synthesis epilogue (batch path).
+struct WhiteCfg {
+  int32_t on = 0;
+  const double* sigma = nullptr;
+  const int32_t* block_of = nullptr;
+  const double* esig = nullptr;
+  const double* zb = nullptr;
+  int64_t nblocks = 0;
+  int64_t real0 = 0;
+  uint32_t k0 = 0, k1 = 0;
+};
+
+// *fused is set when the kernel that ran also added `white` (only the seeded VALU kernel does).
 int run_synth(fpta_ctx* c, Layout& L, int32_t R, int32_t R_pad, double* out, int64_t ldo, int accumulate,
-              bool allow_mfma) {
+              bool allow_mfma, const WhiteCfg* white = nullptr, bool* fused = nullptr) {
+  if (fused) *fused = false;
   SynthArgs a{};
   a.offs = L.offs.as<int64_t>();
   a.psr_of = L.psr_of.as<int32_t>();
@@ -419,6 +434,18 @@ int run_synth(fpta_ctx* c, Layout& L, int32_t R, int32_t R_pad, double* out, int
     const ValuVariant v = kSeededVariants[c->valu_variant];
     int rc = build_tiles(c, L, R, 4 * 64 * v.mt, v.nt);
     if (rc) return rc;
+    if (white && white->on && c->fuse_white) {
+      a.w_on = 1;
+      a.w_sigma = white->sigma;
+      a.w_block_of = white->block_of;
+      a.w_esig = white->esig;
+      a.w_zb = white->zb;
+      a.w_nblocks = white->nblocks;
+      a.real0 = white->real0;
+      a.k0 = white->k0;
+      a.k1 = white->k1;
+      if (fused) *fused = true;
+    }
     KTimer kt(c, FPTA_K_SYNTH);
     HIPCHK(c,
            launch_synth_valu_seeded(c->stream, a, L.tiles.as<int4>(), L.n_tiles, L.seeds.as<double4>(),
@@ -523,6 +550,9 @@ int fpta_set_option(fpta_ctx* c, int32_t key, int64_t value) {
     case FPTA_OPT_SYNTH_PATH:
       if (value < 0 || value > 3) return fail(c, FPTA_EINVAL, "synth path must be 0, 1, 2 or 3");
       c->synth_path = (int)value;
+      return FPTA_OK;
+    case FPTA_OPT_FUSE_WHITE:
+      c->fuse_white = value ? 1 : 0;
       return FPTA_OK;
     case FPTA_OPT_VALU_VARIANT:
       if (value < 0 || value >= kNumValuVariants) return fail(c, FPTA_EINVAL, "unknown VALU variant");
@@ -783,22 +813,41 @@ static int batch_common(fpta_ctx* c, uint64_t seed, int64_t real0, int32_t n_rea
   HIPCHK(c, c->out.ensure(out_bytes), "out alloc");
   c->out_R = n_real;
   c->out_ld = L.n_toa;
+  const bool do_white = white && (c->has_sigma || c->has_blocks);
+  const uint32_t k0 = (uint32_t)(seed & 0xFFFFFFFFull), k1 = (uint32_t)(seed >> 32);
+  WhiteCfg wc{};
+  if (do_white) {
+    if (n_real > 65535) return fail(c, FPTA_EINVAL, "white: n_real > 65535 per call");
+    wc.on = 1;
+    wc.sigma = c->has_sigma ? c->sigma.as<double>() : nullptr;
+    wc.block_of = c->has_blocks ? c->block_of.as<int32_t>() : nullptr;
+    wc.esig = c->has_blocks ? c->esig.as<double>() : nullptr;
+    wc.nblocks = c->has_blocks ? c->n_blocks : 0;
+    wc.real0 = real0;
+    wc.k0 = k0;
+    wc.k1 = k1;
+    if (c->has_blocks) {  // ECORR epoch normals of this batch, needed by either white path
+      HIPCHK(c, c->zb_epochs.ensure(sizeof(double) * (size_t)n_real * c->n_blocks), "zb alloc");
+      wc.zb = c->zb_epochs.as<double>();
+      KTimer kt(c, FPTA_K_WHITE);
+      HIPCHK(c, launch_epoch_normals(c->stream, c->n_blocks, n_real, real0, k0, k1, c->zb_epochs.as<double>()),
+             "k_epoch_normals launch");
+    }
+  }
+  bool fused = false;
   if (L.segs.empty()) {
     HIPCHK(c, hipMemsetAsync(c->out.p, 0, out_bytes, c->stream), "out memset");
   } else {
     if ((rc = run_coefficients(c, L, seed, real0, n_real, R_pad, zin, zin_nm, nullptr))) return rc;
-    if ((rc = run_synth(c, L, n_real, R_pad, c->out.as<double>(), L.n_toa, 0, true))) return rc;
+    if ((rc = run_synth(c, L, n_real, R_pad, c->out.as<double>(), L.n_toa, 0, true, do_white ? &wc : nullptr,
+                        &fused)))
+      return rc;
   }
-  if (white && (c->has_sigma || c->has_blocks)) {
-    if (n_real > 65535) return fail(c, FPTA_EINVAL, "white: n_real > 65535 per call");
-    if (c->has_blocks) HIPCHK(c, c->zb_epochs.ensure(sizeof(double) * (size_t)n_real * c->n_blocks), "zb alloc");
+  if (do_white && !fused) {
     KTimer kt(c, FPTA_K_WHITE);
     HIPCHK(c,
-           launch_white_batch(c->stream, c->has_sigma ? c->sigma.as<double>() : nullptr,
-                              c->has_blocks ? c->block_of.as<int32_t>() : nullptr,
-                              c->has_blocks ? c->esig.as<double>() : nullptr, c->has_blocks ? c->n_blocks : 0,
-                              c->zb_epochs.as<double>(), c->out.as<double>(), L.n_toa, L.n_toa, n_real, real0,
-                              (uint32_t)(seed & 0xFFFFFFFFull), (uint32_t)(seed >> 32)),
+           launch_white_pairs(c->stream, wc.sigma, wc.block_of, wc.esig, wc.nblocks, wc.zb, c->out.as<double>(),
+                              L.n_toa, L.n_toa, n_real, real0, k0, k1),
            "k_white_pairs launch");
   }
   if (out) HIPCHK(c, hipMemcpyAsync(out, c->out.p, out_bytes, hipMemcpyDeviceToHost, c->stream), "out download");

@@ -38,6 +38,15 @@ struct SynthArgs {
   int32_t n_real;
   int32_t accumulate;
   int32_t anchor;
+  // white noise + ECORR fused into the epilogue of the seeded VALU kernel (w_on = 1)
+  int32_t w_on;
+  const double* w_sigma;       // [n_toa] or null
+  const int32_t* w_block_of;   // [n_toa] epoch of each TOA (-1: none) or null
+  const double* w_esig;        // [n_blocks]
+  const double* w_zb;          // [n_real][n_blocks] epoch normals of this batch
+  int64_t w_nblocks;
+  int64_t real0;               // global index of realization 0 of the batch
+  uint32_t k0, k1;             // Philox key (seed)
 };
 
 // MFMA tile geometry
@@ -72,9 +81,11 @@ hipError_t launch_mix(hipStream_t st, const SegDesc& sd, int32_t P, int32_t R_pa
                       double* coef, int32_t K, double* x_out);
 hipError_t launch_mix_tiled(hipStream_t st, const SegDesc& sd, int32_t P, int32_t R_pad, const double* zbuf,
                             double* coef, int32_t K, double* x_out);
-hipError_t launch_white_batch(hipStream_t st, const double* sigma, const int32_t* block_of, const double* esig,
-                              int64_t n_blocks, double* zb, double* out, int64_t ldo, int64_t n_toa, int32_t n_real,
-                              int64_t real0, uint32_t k0, uint32_t k1);
+hipError_t launch_epoch_normals(hipStream_t st, int64_t n_blocks, int32_t n_real, int64_t real0, uint32_t k0,
+                                uint32_t k1, double* zb);
+hipError_t launch_white_pairs(hipStream_t st, const double* sigma, const int32_t* block_of, const double* esig,
+                              int64_t n_blocks, const double* zb, double* out, int64_t ldo, int64_t n_toa,
+                              int32_t n_real, int64_t real0, uint32_t k0, uint32_t k1);
 hipError_t launch_synth_direct(hipStream_t st, const SynthArgs& a);
 hipError_t launch_synth_mfma(hipStream_t st, const SynthArgs& a, const int4* tiles, int32_t n_tiles);
 hipError_t launch_synth_valu(hipStream_t st, const SynthArgs& a, const int4* tiles, int32_t n_tiles, int variant);

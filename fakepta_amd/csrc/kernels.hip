@@ -460,13 +460,23 @@ __global__ __launch_bounds__(256) void k_seeds(const SegDesc* __restrict__ segs,
   seeds[(int64_t)s * n_toa + t] = make_double4(ch * cn, ch * sn, 2.0 * cn, ch);
 }
 
+// White-noise normal of (TOA t, global realization g): stream paired over realizations,
+// ctr = (t, 0xFFFFFFFF, 0xFFFFFFF0, g >> 1) -> (z for g even, z for g odd) (oracle:
+// white_normals_rpairs). A lane that owns TOA t uses both outputs of one Box-Muller.
+__device__ __forceinline__ void white_pair(int64_t t, int64_t g, uint32_t k0, uint32_t k1, double& z0, double& z1) {
+  const u32x4 c = {(uint32_t)t, kWhitePsrWord, kWhiteStream, (uint32_t)(g >> 1)};
+  box_muller(philox4x32_10(c, k0, k1), z0, z1);
+}
+
 // ----------------------------------------------------------------------------- k_synth_valu_seeded
 // The production fused kernel for harmonic grids (every f_k = k/T signal of fake_pta.py:264 and
 // correlated_noises.py:120). No transcendental in the kernel: each lane loads its TOA's seed and
 // advances the phasor one mode per complex multiply. Workgroup = 4 waves on 4 consecutive TOA
 // blocks (64*MT TOAs each) sharing the same NT realizations, so the wave-uniform coefficient
 // stream (scalar loads into v_fma_f64 SGPR operands) is shared through the scalar cache.
-template <int MT, int NT>
+// WHITE: the epilogue adds sigma*z + ECORR (fake_pta.py:201-230) before the single store, so the
+// block is written once instead of re-read and re-written by a separate white-noise pass.
+template <int MT, int NT, bool WHITE>
 __global__ __launch_bounds__(256) void k_synth_valu_seeded(SynthArgs a, const int4* __restrict__ tiles,
                                                            const double4* __restrict__ seeds) {
   const int4 tl = tiles[blockIdx.x];
@@ -546,6 +556,36 @@ __global__ __launch_bounds__(256) void k_synth_valu_seeded(SynthArgs a, const in
     }
   }
 
+  if constexpr (WHITE) {
+    double sg[MT], es[MT];
+    int ep[MT];
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      const int64_t tg = base + tc[m];
+      sg[m] = a.w_sigma ? a.w_sigma[tg] : 0.0;
+      ep[m] = a.w_block_of ? a.w_block_of[tg] : -1;
+      es[m] = ep[m] >= 0 ? a.w_esig[ep[m]] : 0.0;
+    }
+    double z0[MT], z1[MT];
+#pragma unroll
+    for (int n = 0; n < NT; ++n) {
+      const int r = r0 + n;
+      if (r >= a.n_real) break;
+      const int64_t g = a.real0 + r;  // wave-uniform: the branches below do not diverge
+      if (a.w_sigma && (n == 0 || (g & 1) == 0)) {
+#pragma unroll
+        for (int m = 0; m < MT; ++m) white_pair(base + tc[m], g, a.k0, a.k1, z0[m], z1[m]);
+      }
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        double v = acc[m][n];
+        if (a.w_sigma) v = fma(sg[m], (g & 1) ? z1[m] : z0[m], v);
+        if (ep[m] >= 0) v = fma(es[m], a.w_zb[(int64_t)r * a.w_nblocks + ep[m]], v);
+        acc[m][n] = v;
+      }
+    }
+  }
+
 #pragma unroll
   for (int n = 0; n < NT; ++n) {
     const int r = r0 + n;
@@ -617,34 +657,29 @@ __global__ __launch_bounds__(256) void k_epoch_normals(int64_t n_blocks, int64_t
   if (2 * i + 1 < n_blocks) row[2 * i + 1] = z1;
 }
 
-// k_white_pairs: out[r][t] += sigma[t] z(t, r) + ecorr[b(t)] zb[r][b(t)], one Philox call and
-// one Box-Muller per TOA pair (t even -> z0, t odd -> z1). grid (ceil(ceil(n_toa/2)/256), n_real).
+// k_white_pairs: out[r][t] += sigma[t] z(t, real0 + r) + ecorr[b(t)] zb[r][b(t)], one thread per
+// (TOA, global realization pair). grid (ceil(n_toa/256), number of realization pairs touched).
 __global__ __launch_bounds__(256) void k_white_pairs(const double* __restrict__ sigma,
                                                      const int32_t* __restrict__ block_of,
                                                      const double* __restrict__ esig, const double* __restrict__ zb,
                                                      int64_t n_blocks, double* __restrict__ out, int64_t ldo,
-                                                     int64_t n_toa, int64_t real0, uint32_t k0, uint32_t k1) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int r = blockIdx.y;
-  const int64_t t = 2 * i;
+                                                     int64_t n_toa, int32_t n_real, int64_t real0, uint32_t k0,
+                                                     uint32_t k1) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (t >= n_toa) return;
+  const int64_t g0 = ((real0 >> 1) + blockIdx.y) * 2;  // even global realization of this pair
   double z[2] = {0.0, 0.0};
-  if (sigma) {
-    const u32x4 c = {(uint32_t)i, kWhitePsrWord, kWhiteStream, (uint32_t)(real0 + r)};
-    box_muller(philox4x32_10(c, k0, k1), z[0], z[1]);
-  }
-  double* orow = out + (int64_t)r * ldo;
-  const double* zbr = zb ? zb + (int64_t)r * n_blocks : nullptr;
+  if (sigma) white_pair(t, g0, k0, k1, z[0], z[1]);
+  const double s = sigma ? sigma[t] : 0.0;
+  const int b = block_of ? block_of[t] : -1;
+  const double e = b >= 0 ? esig[b] : 0.0;
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
-    const int64_t tt = t + h;
-    if (tt >= n_toa) break;
-    double v = sigma ? sigma[tt] * z[h] : 0.0;
-    if (block_of) {
-      const int b = block_of[tt];
-      if (b >= 0) v = fma(esig[b], zbr[b], v);
-    }
-    orow[tt] += v;
+    const int64_t r = g0 + h - real0;
+    if (r < 0 || r >= n_real) continue;
+    double v = s * z[h];
+    if (b >= 0) v = fma(e, zb[r * n_blocks + b], v);
+    out[r * ldo + t] += v;
   }
 }
 
@@ -837,16 +872,20 @@ hipError_t launch_mix_tiled(hipStream_t st, const SegDesc& sd, int32_t P, int32_
   return hipGetLastError();
 }
 
-hipError_t launch_white_batch(hipStream_t st, const double* sigma, const int32_t* block_of, const double* esig,
-                              int64_t n_blocks, double* zb, double* out, int64_t ldo, int64_t n_toa, int32_t n_real,
-                              int64_t real0, uint32_t k0, uint32_t k1) {
-  if (block_of && n_blocks > 0) {
-    hipLaunchKernelGGL(k_epoch_normals, dim3((unsigned)(((n_blocks + 1) / 2 + 255) / 256), n_real), dim3(256), 0, st,
-                       n_blocks, real0, k0, k1, zb);
-  }
-  hipLaunchKernelGGL(k_white_pairs, dim3((unsigned)(((n_toa + 1) / 2 + 255) / 256), n_real), dim3(256), 0, st,
-                     sigma, n_blocks > 0 ? block_of : nullptr, esig, n_blocks > 0 ? zb : nullptr, n_blocks, out, ldo,
-                     n_toa, real0, k0, k1);
+hipError_t launch_epoch_normals(hipStream_t st, int64_t n_blocks, int32_t n_real, int64_t real0, uint32_t k0,
+                                uint32_t k1, double* zb) {
+  hipLaunchKernelGGL(k_epoch_normals, dim3((unsigned)(((n_blocks + 1) / 2 + 255) / 256), n_real), dim3(256), 0, st,
+                     n_blocks, real0, k0, k1, zb);
+  return hipGetLastError();
+}
+
+hipError_t launch_white_pairs(hipStream_t st, const double* sigma, const int32_t* block_of, const double* esig,
+                              int64_t n_blocks, const double* zb, double* out, int64_t ldo, int64_t n_toa,
+                              int32_t n_real, int64_t real0, uint32_t k0, uint32_t k1) {
+  const int64_t npairs = ((real0 + n_real - 1) >> 1) - (real0 >> 1) + 1;
+  hipLaunchKernelGGL(k_white_pairs, dim3((unsigned)((n_toa + 255) / 256), (unsigned)npairs), dim3(256), 0, st, sigma,
+                     n_blocks > 0 ? block_of : nullptr, esig, n_blocks > 0 ? zb : nullptr, n_blocks, out, ldo, n_toa,
+                     n_real, real0, k0, k1);
   return hipGetLastError();
 }
 
@@ -891,10 +930,14 @@ hipError_t launch_seeds(hipStream_t st, const SegDesc* segs, int32_t n_seg, cons
 hipError_t launch_synth_valu_seeded(hipStream_t st, const SynthArgs& a, const int4* tiles, int32_t n_tiles,
                                     const double4* seeds, int variant) {
   switch (variant) {
-#define FPTA_SEEDED_CASE(i)                                                                               \
-  case i:                                                                                                 \
-    hipLaunchKernelGGL((k_synth_valu_seeded<kSeededVariants[i].mt, kSeededVariants[i].nt>), dim3(n_tiles), \
-                       dim3(256), 0, st, a, tiles, seeds);                                                \
+#define FPTA_SEEDED_CASE(i)                                                                                     \
+  case i:                                                                                                       \
+    if (a.w_on)                                                                                                 \
+      hipLaunchKernelGGL((k_synth_valu_seeded<kSeededVariants[i].mt, kSeededVariants[i].nt, true>), dim3(n_tiles), \
+                         dim3(256), 0, st, a, tiles, seeds);                                                    \
+    else                                                                                                        \
+      hipLaunchKernelGGL((k_synth_valu_seeded<kSeededVariants[i].mt, kSeededVariants[i].nt, false>),             \
+                         dim3(n_tiles), dim3(256), 0, st, a, tiles, seeds);                                     \
     break;
     FPTA_SEEDED_CASE(0)
     FPTA_SEEDED_CASE(1)

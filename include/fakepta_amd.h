@@ -104,7 +104,7 @@ int fpta_white_accumulate(fpta_ctx* ctx, int64_t n_toa, const double* sigma, con
  * Philox4x32-10 draws -> ORF mixing -> fused basis/contraction -> white/ECORR.
  * Draw streams (invariant to batching and to the number of GPUs):
  *   GP   : ctr = (mode, pulsar, segment, realization), key = seed -> (z_cos, z_sin)
- *   white: ctr = (toa>>1, 0xFFFFFFFF, 0xFFFFFFF0, realization), pick [toa&1]
+ *   white: ctr = (toa, 0xFFFFFFFF, 0xFFFFFFF0, realization>>1), pick [realization&1]
  *   ECORR: ctr = (block>>1, 0xFFFFFFFF, 0xFFFFFFF1, realization), pick [block&1]
  * Replaces the Python loop of fakepta/fake_pta.py:648-668 + correlated_noises.py:153-160
  * when many realizations of one array are needed. */
@@ -160,6 +160,7 @@ int fpta_batch_info(fpta_ctx* ctx, int64_t* info);
 #define FPTA_OPT_PROFILE 3        /* 1: time every batch kernel with HIP events on the ctx stream */
 #define FPTA_OPT_ANCHOR 4         /* recurrence re-anchor interval in K-steps of 2 modes (0 = once per signal, default) */
 #define FPTA_OPT_VALU_VARIANT 5   /* tile variant of the VALU fused kernel (0..5) */
+#define FPTA_OPT_FUSE_WHITE 6     /* 1 (default): white/ECORR added in the synthesis epilogue; 0: separate pass */
 int fpta_set_option(fpta_ctx* ctx, int32_t key, int64_t value);
 /* Kernel ids for fpta_kernel_stats */
 #define FPTA_K_GEN 0

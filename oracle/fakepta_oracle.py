@@ -334,8 +334,25 @@ def gp_normals(seed, reals, p, seg, n_modes):
     return box_muller(philox4x32_10(ctr, seed_key(seed)))
 
 
+def white_normals_rpairs(seed, reals, n_toa):
+    """White-noise stream: one normal per (realization, TOA), paired over REALIZATIONS so a GPU lane
+    owning a TOA uses both outputs of one Box-Muller: ctr = (t, 0xFFFFFFFF, 0xFFFFFFF0, g >> 1),
+    pick [g & 1] for global realization g. Returns [len(reals), n_toa]."""
+    reals = np.asarray(reals, dtype=np.uint64)
+    t = np.arange(n_toa, dtype=np.uint64)
+    ctr = np.zeros((len(reals), n_toa, 4), dtype=np.uint32)
+    ctr[..., 0] = t.astype(np.uint32)[None, :]
+    ctr[..., 1] = WHITE_PSR_WORD
+    ctr[..., 2] = WHITE_STREAM
+    ctr[..., 3] = (reals >> np.uint64(1)).astype(np.uint32)[:, None]
+    z = box_muller(philox4x32_10(ctr, seed_key(seed)))
+    pick = (reals & np.uint64(1)).astype(np.int64)[:, None, None]
+    return np.take_along_axis(z, np.broadcast_to(pick, z.shape[:-1] + (1,)), axis=-1)[..., 0]
+
+
 def white_normals(seed, reals, n_toa, stream=WHITE_STREAM):
-    """one normal per (realization, TOA): ctr = (t >> 1, 0xFFFFFFFF, stream, r), pick [t & 1]."""
+    """one normal per (realization, index), paired over the index: ctr = (i >> 1, 0xFFFFFFFF,
+    stream, r), pick [i & 1]. Used for the ECORR epoch stream (index = epoch)."""
     reals = np.asarray(reals, dtype=np.uint32)
     t = np.arange(n_toa, dtype=np.uint64)
     ctr = np.zeros((len(reals), n_toa, 4), dtype=np.uint32)
@@ -400,7 +417,7 @@ def batch_synth(offs, toas, freqs, segments, seed, real0, n_real, sigma=None, bl
             out[:, sl] += ch[None, :] * (a[:, p, :, 0] @ np.cos(ph).T + a[:, p, :, 1] @ np.sin(ph).T)
     reals = np.arange(real0, real0 + n_real)
     if sigma is not None:
-        out += sigma[None, :] * white_normals(seed, reals, offs[-1], WHITE_STREAM)
+        out += sigma[None, :] * white_normals_rpairs(seed, reals, offs[-1])
     if block_of is not None and ecorr_sigma is not None and len(ecorr_sigma):
         zb = white_normals(seed, reals, len(ecorr_sigma), ECORR_STREAM)
         has = block_of >= 0

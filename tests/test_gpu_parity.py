@@ -244,11 +244,13 @@ PATHS = [(1, 0), (2, 0)] + [(3, v) for v in range(6)]  # (synth path, VALU varia
 
 
 @pytest.mark.parametrize("path,variant", PATHS)
-@pytest.mark.parametrize("case", ["basic", "masked_odd_modes", "white_ecorr", "common_only", "tiny_pulsars"])
+@pytest.mark.parametrize("case", ["basic", "masked_odd_modes", "white_ecorr", "white_only", "ecorr_only",
+                                  "common_only", "tiny_pulsars"])
 def test_batch_vs_oracle(ctx, capi, path, variant, case):
     rng = np.random.default_rng(zlib.crc32(case.encode()))
     kw = dict(basic={}, masked_odd_modes=dict(per_psr=((7, 4.0), (1, 0.0)), masked=True),
-              white_ecorr=dict(white=True, ecorr=True), common_only=dict(per_psr=(), common=((30, 0.0), (13, 2.0))),
+              white_ecorr=dict(white=True, ecorr=True), white_only=dict(white=True, P=3),
+              ecorr_only=dict(ecorr=True, per_psr=((12, 0.0),), common=()), common_only=dict(per_psr=(), common=((30, 0.0), (13, 2.0))),
               tiny_pulsars=dict(P=5, n_range=(1, 18)))[case]
     offs, toas, nu, segs, sigma, block_of, es = _build(ctx, rng, **kw)
     ctx.set_option(capi.OPT_SYNTH_PATH, path)
@@ -297,6 +299,23 @@ def test_recurrence_anchor_accuracy(ctx, capi, path, anchor):
         ctx.set_option(capi.OPT_ANCHOR, 0)
     want = O.batch_synth(offs, toas, nu, [O.Segment(0, 2 * np.pi * f, a, 2.0)], 5, 0, 64)
     assert_parity(got, want, TOL)
+
+
+@pytest.mark.parametrize("white,ecorr", [(True, False), (False, True), (True, True)])
+def test_white_fused_matches_separate_pass(ctx, capi, white, ecorr):
+    """The seeded kernel's white/ECORR epilogue and the separate k_white_pairs pass draw the same
+    normals: the two agree to rounding (only the order of the final additions differs)."""
+    rng = np.random.default_rng(31)
+    _build(ctx, rng, P=5, white=white, ecorr=ecorr)
+    try:
+        ctx.set_option(capi.OPT_SYNTH_PATH, 3)
+        fused = ctx.batch_synth(77, 9, 131)
+        ctx.set_option(capi.OPT_FUSE_WHITE, 0)
+        separate = ctx.batch_synth(77, 9, 131)
+    finally:
+        ctx.set_option(capi.OPT_FUSE_WHITE, 1)
+        ctx.set_option(capi.OPT_SYNTH_PATH, 0)
+    assert_parity(fused, separate, 1e-13)
 
 
 def test_batch_split_invariance_bitwise(ctx):
