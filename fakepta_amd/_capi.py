@@ -38,6 +38,10 @@ _SIGS = [
     ("fpta_common_accumulate", _c_int, [_ctx_p, _i32, _vp, _vp, _vp, _i32, _vp, _vp, _dbl, _dbl, _vp, _vp, _vp,
                                         _vp]),
     ("fpta_white_accumulate", _c_int, [_ctx_p, _i64, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp]),
+    ("fpta_gp_covariance", _c_int, [_ctx_p, _i64, _vp, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    ("fpta_noise_wiener", _c_int, [_ctx_p, _i64, _vp, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    ("fpta_noise_draw", _c_int, [_ctx_p, _i64, _vp, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _u64, _i64, _i32,
+                                 _vp]),
     ("fpta_batch_set_toas", _c_int, [_ctx_p, _i32, _vp, _vp, _vp]),
     ("fpta_batch_add_signal", _c_int, [_ctx_p, _i32, _i32, _vp, _vp, _dbl, _dbl, _vp, _vp]),
     ("fpta_batch_set_white", _c_int, [_ctx_p, _vp, _i64, _vp, _vp, _vp]),
@@ -63,7 +67,7 @@ for _name, _res, _args in _SIGS:
 EXPORTED = [s[0] for s in _SIGS]
 
 OPT_SYNTH_PATH, OPT_MFMA_MIN_REAL, OPT_PROFILE, OPT_ANCHOR, OPT_VALU_VARIANT, OPT_FUSE_WHITE = 1, 2, 3, 4, 5, 6
-K_GEN, K_MIX, K_SYNTH, K_WHITE = 0, 1, 2, 3
+K_GEN, K_MIX, K_SYNTH, K_WHITE, K_DENSE = 0, 1, 2, 3, 4
 
 
 class FptaError(RuntimeError):
@@ -127,6 +131,54 @@ class Context:
         self._check(_lib.fpta_gp_accumulate(self._h, n, _ptr(toas), _ptr(nu), len(segments), _ptr(nm), _ptr(f),
                                             _ptr(cc), _ptr(cs), _ptr(idx), _ptr(ff), _ptr(m), float(sign),
                                             _ptr(residuals)), "fpta_gp_accumulate")
+
+    # ------------------------------------------------------------------ dense covariance
+    @staticmethod
+    def _dense_args(toas, nu, segments, white_var):
+        """segments: list of (f [N], w = psd * df [N], idx, freqf)."""
+        toas, nu = _f64(toas), _f64(nu)
+        n = len(toas)
+        assert len(nu) == n and len(segments) > 0
+        nm = np.array([len(s[0]) for s in segments], dtype=np.int32)
+        for s in segments:
+            assert len(s[1]) == len(s[0])
+        f = _f64(np.concatenate([np.asarray(s[0], float) for s in segments]))
+        w = _f64(np.concatenate([np.asarray(s[1], float) for s in segments]))
+        idx = _f64([s[2] for s in segments])
+        ff = _f64([s[3] for s in segments])
+        wv = None if white_var is None else _f64(white_var)
+        if wv is not None:
+            assert len(wv) == n
+        keep = (toas, nu, nm, f, w, idx, ff, wv)
+        args = (n, _ptr(toas), _ptr(nu), len(segments), _ptr(nm), _ptr(f), _ptr(w), _ptr(idx), _ptr(ff), _ptr(wv))
+        return n, keep, args
+
+    def gp_covariance(self, toas, nu, segments, white_var=None):
+        """sum_s B_s diag(psd df) B_s^T (+ diag(white_var)) as a [n, n] float64 array."""
+        n, keep, args = self._dense_args(toas, nu, segments, white_var)
+        cov = np.empty((n, n), dtype=np.float64)
+        self._check(_lib.fpta_gp_covariance(self._h, *args, _ptr(cov)), "fpta_gp_covariance")
+        del keep
+        return cov
+
+    def noise_wiener(self, toas, nu, segments, white_var, residuals):
+        """red_cov C^-1 residuals with C = red_cov + diag(white_var) (device Cholesky)."""
+        n, keep, args = self._dense_args(toas, nu, segments, white_var)
+        r = _f64(residuals)
+        assert len(r) == n
+        out = np.empty(n, dtype=np.float64)
+        self._check(_lib.fpta_noise_wiener(self._h, *args, _ptr(r), _ptr(out)), "fpta_noise_wiener")
+        del keep
+        return out
+
+    def noise_draw(self, toas, nu, segments, white_var, seed, real0, n_real):
+        """[n_real, n] draws of N(0, red_cov + diag(white_var)) (Philox stream, device Cholesky)."""
+        n, keep, args = self._dense_args(toas, nu, segments, white_var)
+        out = np.empty((n_real, n), dtype=np.float64)
+        self._check(_lib.fpta_noise_draw(self._h, *args, int(seed) & 0xFFFFFFFFFFFFFFFF, int(real0), int(n_real),
+                                         _ptr(out)), "fpta_noise_draw")
+        del keep
+        return out
 
     def gp_accumulate_array(self, offs, toas, nu, segments, residuals, sign=1.0, masks=None):
         """Array form: segments = list of (f [P, N], ccos [P, N], csin [P, N], idx, freqf);

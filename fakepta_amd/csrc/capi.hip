@@ -115,8 +115,11 @@ struct fpta_ctx {
   };
   std::vector<Pending> pending;
   std::vector<hipEvent_t> pool;
-  int64_t kcount[FPTA_K_N] = {0, 0, 0, 0};
-  double kms[FPTA_K_N] = {0, 0, 0, 0};
+  int64_t kcount[FPTA_K_N] = {};
+  double kms[FPTA_K_N] = {};
+  // dense-covariance path: inputs, basis G^T [k_pad][n_pad], matrix C [n_pad][n_pad], panel, draws
+  DevBuf dn_toas, dn_nu, dn_f, dn_sw, dn_segof, dn_segidx, dn_segff, dn_white, dn_GT, dn_C, dn_PT, dn_info, dn_r,
+      dn_y, dn_out, dn_Z;
 };
 
 namespace {
@@ -321,7 +324,7 @@ int layout_finalize(fpta_ctx* c, Layout& L) {
   return FPTA_OK;
 }
 
-int32_t round_up(int32_t x, int32_t m) { return (x + m - 1) / m * m; }
+int32_t pad_to(int32_t x, int32_t m) { return (x + m - 1) / m * m; }
 
 // Draw + mix every segment into c->coef [P][K][R_pad].
 int run_coefficients(fpta_ctx* c, Layout& L, uint64_t seed, int64_t real0, int32_t R, int32_t R_pad,
@@ -481,6 +484,97 @@ int blocks_to_owner(fpta_ctx* c, int64_t n_toa, int64_t n_blocks, const int64_t*
       owner[t] = (int32_t)b;
     }
   }
+  return FPTA_OK;
+}
+
+// ----------------------------------------------------------------------------- dense covariance
+inline int64_t pad_i64(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
+
+struct DenseDims {
+  int64_t n = 0, n_pad = 0;
+  int32_t n_modes = 0, k_pad = 0;
+};
+
+// Basis + Gram: C [n_pad][n_pad] on device = sum_s B_s diag(w_s) B_s^T (+ diag white), full symmetric,
+// padding rows/columns zero (the factor and the draws read them).
+int dense_build(fpta_ctx* c, int64_t n, const double* toas, const double* nu, int32_t n_seg,
+                const int32_t* seg_nmodes, const double* f, const double* w, const double* seg_idx,
+                const double* seg_freqf, const double* white_var, DenseDims& d) {
+  if (n <= 0 || !toas || !nu || n_seg <= 0 || !seg_nmodes || !f || !w || !seg_idx || !seg_freqf)
+    return fail(c, FPTA_EINVAL, "dense: bad arguments");
+  if (n > (int64_t)1 << 17) return fail(c, FPTA_EINVAL, "dense: more than 131072 TOAs");
+  HIPCHK(c, hipSetDevice(c->device), "hipSetDevice");
+  int64_t M = 0;
+  for (int32_t s = 0; s < n_seg; ++s) {
+    if (seg_nmodes[s] <= 0) return fail(c, FPTA_EINVAL, "dense: segment with no modes");
+    M += seg_nmodes[s];
+  }
+  if (M > (1 << 20)) return fail(c, FPTA_EINVAL, "dense: too many modes");
+  std::vector<double> sw((size_t)M);
+  std::vector<int32_t> seg_of((size_t)M);
+  for (int32_t s = 0, m = 0; s < n_seg; ++s)
+    for (int32_t k = 0; k < seg_nmodes[s]; ++k, ++m) {
+      if (!(w[m] >= 0.0)) return fail(c, FPTA_EINVAL, "dense: psd * df must be >= 0");
+      sw[m] = std::sqrt(w[m]);
+      seg_of[m] = s;
+    }
+  d.n = n;
+  d.n_pad = pad_i64(n, 256);
+  d.n_modes = (int32_t)M;
+  d.k_pad = (int32_t)pad_i64(2 * M, 4);
+  int rc;
+  if ((rc = upload(c, c->dn_toas, toas, sizeof(double) * n, "dense toas"))) return rc;
+  if ((rc = upload(c, c->dn_nu, nu, sizeof(double) * n, "dense nu"))) return rc;
+  if ((rc = upload(c, c->dn_f, f, sizeof(double) * M, "dense f"))) return rc;
+  if ((rc = upload(c, c->dn_sw, sw.data(), sizeof(double) * M, "dense w"))) return rc;
+  if ((rc = upload(c, c->dn_segof, seg_of.data(), sizeof(int32_t) * M, "dense segments"))) return rc;
+  if ((rc = upload(c, c->dn_segidx, seg_idx, sizeof(double) * n_seg, "dense idx"))) return rc;
+  if ((rc = upload(c, c->dn_segff, seg_freqf, sizeof(double) * n_seg, "dense freqf"))) return rc;
+  if (white_var && (rc = upload(c, c->dn_white, white_var, sizeof(double) * n, "dense white"))) return rc;
+  HIPCHK(c, c->dn_GT.ensure(sizeof(double) * (size_t)d.k_pad * d.n_pad), "dense basis alloc");
+  HIPCHK(c, c->dn_C.ensure(sizeof(double) * (size_t)d.n_pad * d.n_pad), "dense matrix alloc");
+  HIPCHK(c, hipMemsetAsync(c->dn_C.p, 0, sizeof(double) * (size_t)d.n_pad * d.n_pad, c->stream), "dense memset");
+  KTimer kt(c, FPTA_K_DENSE);
+  HIPCHK(c,
+         launch_cov_basis(c->stream, c->dn_toas.as<double>(), c->dn_nu.as<double>(), n, c->dn_f.as<double>(),
+                          c->dn_sw.as<double>(), c->dn_segof.as<int32_t>(), c->dn_segidx.as<double>(),
+                          c->dn_segff.as<double>(), d.n_modes, d.k_pad, c->dn_GT.as<double>(), d.n_pad),
+         "k_cov_basis launch");
+  HIPCHK(c,
+         launch_gemm_tn(c->stream, c->dn_GT.as<double>(), d.n_pad, c->dn_GT.as<double>(), d.n_pad, false, false,
+                        c->dn_C.as<double>(), d.n_pad, n, n, d.k_pad / 4, 1, 0, 2,
+                        white_var ? c->dn_white.as<double>() : nullptr),
+         "k_gemm_tn (gram) launch");
+  return FPTA_OK;
+}
+
+// In-place lower Cholesky of C (right-looking, 64-wide panels: diagonal block in LDS, panel solve,
+// MFMA trailing update). Fails with FPTA_EINVAL when C is not numerically positive definite.
+int dense_cholesky(fpta_ctx* c, const DenseDims& d) {
+  double* C = c->dn_C.as<double>();
+  const int64_t ld = d.n_pad;
+  HIPCHK(c, c->dn_PT.ensure(sizeof(double) * 64 * (size_t)d.n_pad), "dense panel alloc");
+  HIPCHK(c, c->dn_info.ensure(sizeof(int)), "dense info alloc");
+  HIPCHK(c, hipMemsetAsync(c->dn_info.p, 0, sizeof(int), c->stream), "dense info memset");
+  {
+    KTimer kt(c, FPTA_K_DENSE);
+    const int32_t T = (int32_t)((d.n + 63) / 64);
+    for (int32_t kb = 0; kb < T; ++kb) {
+      const int64_t k0 = (int64_t)kb * 64;
+      HIPCHK(c, launch_potrf_block(c->stream, C, ld, d.n, k0, c->dn_info.as<int>()), "k_potrf_block launch");
+      if (k0 + 64 >= d.n) break;
+      HIPCHK(c, launch_trsm_panel(c->stream, C, ld, d.n, k0, c->dn_PT.as<double>(), d.n_pad), "k_trsm_panel launch");
+      HIPCHK(c,
+             launch_gemm_tn(c->stream, c->dn_PT.as<double>(), d.n_pad, c->dn_PT.as<double>(), d.n_pad, false, false, C,
+                            ld, d.n, d.n, 16, 1, kb + 1, 1, nullptr),
+             "k_gemm_tn (update) launch");
+    }
+  }
+  int info = 0;
+  HIPCHK(c, hipMemcpyAsync(&info, c->dn_info.p, sizeof(int), hipMemcpyDeviceToHost, c->stream), "dense info");
+  HIPCHK(c, hipStreamSynchronize(c->stream), "dense cholesky sync");
+  if (info)
+    return fail(c, FPTA_EINVAL, "dense: covariance not positive definite (pivot " + std::to_string(info - 1) + ")");
   return FPTA_OK;
 }
 
@@ -753,6 +847,81 @@ int fpta_white_accumulate(fpta_ctx* c, int64_t n_toa, const double* sigma, const
 }
 
 // ------------------------------------------------------------------------------------ batch
+// ----------------------------------------------------------------------------- dense covariance
+int fpta_gp_covariance(fpta_ctx* c, int64_t n_toa, const double* toas, const double* nu, int32_t n_seg,
+                       const int32_t* seg_nmodes, const double* f, const double* w, const double* seg_idx,
+                       const double* seg_freqf, const double* white_var, double* cov) {
+  if (!c) return fail(nullptr, FPTA_EINVAL, "null ctx");
+  if (!cov) return fail(c, FPTA_EINVAL, "gp_covariance: null output");
+  DenseDims d;
+  int rc = dense_build(c, n_toa, toas, nu, n_seg, seg_nmodes, f, w, seg_idx, seg_freqf, white_var, d);
+  if (rc) return rc;
+  HIPCHK(c,
+         hipMemcpy2DAsync(cov, sizeof(double) * n_toa, c->dn_C.p, sizeof(double) * d.n_pad, sizeof(double) * n_toa,
+                          n_toa, hipMemcpyDeviceToHost, c->stream),
+         "gp_covariance download");
+  HIPCHK(c, hipStreamSynchronize(c->stream), "gp_covariance sync");
+  return FPTA_OK;
+}
+
+int fpta_noise_wiener(fpta_ctx* c, int64_t n_toa, const double* toas, const double* nu, int32_t n_seg,
+                      const int32_t* seg_nmodes, const double* f, const double* w, const double* seg_idx,
+                      const double* seg_freqf, const double* white_var, const double* residuals, double* out) {
+  if (!c) return fail(nullptr, FPTA_EINVAL, "null ctx");
+  if (!white_var || !residuals || !out) return fail(c, FPTA_EINVAL, "noise_wiener: bad arguments");
+  DenseDims d;
+  int rc = dense_build(c, n_toa, toas, nu, n_seg, seg_nmodes, f, w, seg_idx, seg_freqf, white_var, d);
+  if (rc) return rc;
+  if ((rc = upload(c, c->dn_r, residuals, sizeof(double) * n_toa, "noise_wiener residuals"))) return rc;
+  if ((rc = dense_cholesky(c, d))) return rc;
+  HIPCHK(c, c->dn_y.ensure(sizeof(double) * n_toa), "noise_wiener scratch");
+  HIPCHK(c, c->dn_out.ensure(sizeof(double) * n_toa), "noise_wiener out");
+  {
+    KTimer kt(c, FPTA_K_DENSE);
+    HIPCHK(c,
+           launch_chol_solve(c->stream, c->dn_C.as<double>(), d.n_pad, n_toa, c->dn_r.as<double>(),
+                             c->dn_white.as<double>(), c->dn_y.as<double>(), c->dn_out.as<double>()),
+           "k_chol_solve launch");
+  }
+  HIPCHK(c, hipMemcpyAsync(out, c->dn_out.p, sizeof(double) * n_toa, hipMemcpyDeviceToHost, c->stream),
+         "noise_wiener download");
+  HIPCHK(c, hipStreamSynchronize(c->stream), "noise_wiener sync");
+  return FPTA_OK;
+}
+
+int fpta_noise_draw(fpta_ctx* c, int64_t n_toa, const double* toas, const double* nu, int32_t n_seg,
+                    const int32_t* seg_nmodes, const double* f, const double* w, const double* seg_idx,
+                    const double* seg_freqf, const double* white_var, uint64_t seed, int64_t real0, int32_t n_real,
+                    double* out) {
+  if (!c) return fail(nullptr, FPTA_EINVAL, "null ctx");
+  if (!out || n_real <= 0 || real0 < 0) return fail(c, FPTA_EINVAL, "noise_draw: bad arguments");
+  if (real0 + n_real > ((int64_t)1 << 33)) return fail(c, FPTA_EINVAL, "noise_draw: realization index overflow");
+  DenseDims d;
+  int rc = dense_build(c, n_toa, toas, nu, n_seg, seg_nmodes, f, w, seg_idx, seg_freqf, white_var, d);
+  if (rc) return rc;
+  if ((rc = dense_cholesky(c, d))) return rc;
+  const int64_t ldz = pad_i64(n_real, 256);
+  HIPCHK(c, c->dn_Z.ensure(sizeof(double) * (size_t)d.n_pad * ldz), "noise_draw normals alloc");
+  HIPCHK(c, c->dn_out.ensure(sizeof(double) * (size_t)n_real * n_toa), "noise_draw out alloc");
+  {
+    KTimer kt(c, FPTA_K_DENSE);
+    HIPCHK(c,
+           launch_dense_normals(c->stream, n_toa, d.n_pad, n_real, real0, (uint32_t)(seed & 0xFFFFFFFFull),
+                                (uint32_t)(seed >> 32), c->dn_Z.as<double>(), ldz),
+           "k_dense_normals launch");
+    // X [n_real][n_toa] = Z L^T: A = Z (k-major: ZT[t][r]), B^T = L (rows), L lower-triangular
+    HIPCHK(c,
+           launch_gemm_tn(c->stream, c->dn_Z.as<double>(), ldz, c->dn_C.as<double>(), d.n_pad, true, true,
+                          c->dn_out.as<double>(), n_toa, n_real, n_toa, (int32_t)(d.n_pad / 4), 0, 0, 0, nullptr),
+           "k_gemm_tn (draws) launch");
+  }
+  HIPCHK(c, hipMemcpyAsync(out, c->dn_out.p, sizeof(double) * (size_t)n_real * n_toa, hipMemcpyDeviceToHost,
+                           c->stream),
+         "noise_draw download");
+  HIPCHK(c, hipStreamSynchronize(c->stream), "noise_draw sync");
+  return FPTA_OK;
+}
+
 int fpta_batch_set_toas(fpta_ctx* c, int32_t n_psr, const int64_t* offs, const double* toas, const double* nu) {
   if (!c) return fail(nullptr, FPTA_EINVAL, "null ctx");
   HIPCHK(c, hipSetDevice(c->device), "hipSetDevice");
@@ -808,7 +977,7 @@ static int batch_common(fpta_ctx* c, uint64_t seed, int64_t real0, int32_t n_rea
   HIPCHK(c, hipSetDevice(c->device), "hipSetDevice");
   int rc = layout_finalize(c, L);
   if (rc) return rc;
-  const int32_t R_pad = round_up(n_real, kRealPad);
+  const int32_t R_pad = pad_to(n_real, kRealPad);
   const size_t out_bytes = sizeof(double) * (size_t)n_real * L.n_toa;
   HIPCHK(c, c->out.ensure(out_bytes), "out alloc");
   c->out_R = n_real;

@@ -99,4 +99,19 @@ hipError_t launch_correlations(hipStream_t st, const double* out, int64_t ldo, i
 hipError_t launch_philox(hipStream_t st, int64_t n, const uint32_t* ctr, uint32_t k0, uint32_t k1,
                          uint32_t* out);
 
+// dense-covariance path (dense.hip)
+hipError_t launch_cov_basis(hipStream_t st, const double* toas, const double* nu, int64_t n, const double* f,
+                            const double* sw, const int32_t* seg_of, const double* seg_idx, const double* seg_freqf,
+                            int32_t n_modes, int32_t k_pad, double* GT, int64_t ldn);
+hipError_t launch_gemm_tn(hipStream_t st, const double* a, int64_t lda, const double* b, int64_t ldb, bool b_rows,
+                          bool b_tri, double* c, int64_t ldc, int64_t m, int64_t n, int32_t k4, int32_t lower,
+                          int32_t tile0, int32_t mode, const double* diag);
+hipError_t launch_potrf_block(hipStream_t st, double* C, int64_t ldc, int64_t n, int64_t k0, int* info);
+hipError_t launch_trsm_panel(hipStream_t st, double* C, int64_t ldc, int64_t n, int64_t k0, double* PT,
+                             int64_t ldp);
+hipError_t launch_chol_solve(hipStream_t st, const double* C, int64_t ldc, int64_t n, const double* r,
+                             const double* white, double* y, double* out);
+hipError_t launch_dense_normals(hipStream_t st, int64_t n, int64_t rows, int32_t n_real, int64_t real0, uint32_t k0,
+                                uint32_t k1, double* ZT, int64_t ldz);
+
 }  // namespace fpta

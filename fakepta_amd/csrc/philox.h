@@ -48,5 +48,6 @@ __device__ __forceinline__ void box_muller(u32x4 v, double& z0, double& z1) {
 constexpr uint32_t kWhitePsrWord = 0xFFFFFFFFu;
 constexpr uint32_t kWhiteStream = 0xFFFFFFF0u;
 constexpr uint32_t kEcorrStream = 0xFFFFFFF1u;
+constexpr uint32_t kDenseStream = 0xFFFFFFF2u;  // dense-covariance draws (fpta_noise_draw)
 
 }  // namespace fpta

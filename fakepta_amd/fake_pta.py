@@ -322,9 +322,14 @@ class Pulsar:
                                           self.residuals, masks=None if mask is None else [mask])
 
     # ------------------------------------------------------------------ dense covariance (host)
+    def _dense_segment(self, signal, freqf):
+        sm = self.signal_model[signal]
+        f = np.asarray(sm['f'], dtype=float)
+        return (f, np.asarray(sm['psd'], dtype=float) * np.diff(np.append(0, f)), float(sm['idx']), float(freqf))
+
     def make_time_correlated_noise_cov(self, signal='', freqf=1400):
-        """F diag(S df) F^T of one stored GP (fake_pta.py:389-420). Host numpy: the dense
-        O(N_toa^2) path is outside the accelerated scope ('next')."""
+        """F diag(psd df) F^T of one stored GP (fake_pta.py:389-420), built on the GPU
+        (fpta_gp_covariance: basis kernel + fp64 MFMA Gram). System noise uses the backend's TOAs."""
         backend = signal.split('system_noise_')[1] if 'system_noise' in signal else None
         if backend is not None:
             signal = backend + '_' + signal
@@ -334,34 +339,51 @@ class Pulsar:
                 return
         else:
             mask = np.ones(len(self.toas), dtype=bool)
-        sm = self.signal_model[signal]
-        f, psd, idx = sm['f'], sm['psd'], sm['idx']
-        w = np.repeat(psd * np.diff(np.append(0, f)), 2)
-        t = self.toas[mask]
-        ch = ((freqf / self.freqs[mask]) ** idx)[:, None]
-        ph = 2 * np.pi * np.outer(t, f)
-        F = np.empty((len(t), 2 * len(f)))
-        F[:, 0::2] = ch * np.cos(ph)
-        F[:, 1::2] = ch * np.sin(ph)
-        return (F * w) @ F.T
+        seg = self._dense_segment(signal, freqf)
+        return _capi.get_context().gp_covariance(self.toas[mask], self.freqs[mask], [seg])
+
+    def _red_segments(self, freqf=1400):
+        return [self._dense_segment(sig, freqf) for key, sig in (('RN', 'red_noise'), ('DM', 'dm_gp'),
+                                                                  ('Sv', 'chrom_gp'))
+                if self.custom_model[key] is not None]
 
     def make_noise_covariance_matrix(self):
-        """(white variances, red covariance) (fake_pta.py:493-513)."""
+        """(white variances, red covariance) (fake_pta.py:493-513); the red part of every GP in
+        custom_model in one device call."""
         white_cov = self._white_sigma2()
-        red_cov = np.zeros((len(self.toas), len(self.toas)))
-        for key, sig in (('RN', 'red_noise'), ('DM', 'dm_gp'), ('Sv', 'chrom_gp')):
-            if self.custom_model[key] is not None:
-                red_cov += self.make_time_correlated_noise_cov(signal=sig)
-        return white_cov, red_cov
+        segs = self._red_segments()
+        if not segs:
+            return white_cov, np.zeros((len(self.toas), len(self.toas)))
+        return white_cov, _capi.get_context().gp_covariance(self.toas, self.freqs, segs)
 
     def draw_noise_model(self, residuals=None):
-        """MVN draw from the dense covariance, or the Wiener-filter reconstruction
-        (fake_pta.py:515-524). Host numpy (not accelerated)."""
-        white_cov, red_cov = self.make_noise_covariance_matrix()
-        cov = np.diag(white_cov) + red_cov
+        """draw_noise_model (fake_pta.py:515-524). With residuals: the Wiener estimate
+        red_cov C^-1 residuals on the GPU (device Cholesky, fpta_noise_wiener). Without: one draw
+        of N(0, C) with numpy's multivariate_normal on the GPU-built C, as the reference does
+        (same np.random stream; its SVD factor is the reference's)."""
+        white_cov = self._white_sigma2()
+        segs = self._red_segments()
+        ctx = _capi.get_context()
         if residuals is None:
+            if segs:
+                cov = ctx.gp_covariance(self.toas, self.freqs, segs, white_var=white_cov)
+            else:
+                cov = np.diag(white_cov)
             return np.random.multivariate_normal(mean=np.zeros(len(self.toas)), cov=cov)
-        return red_cov.T @ (np.linalg.inv(cov) @ residuals)
+        if not segs:
+            return np.zeros(len(self.toas))
+        return ctx.noise_wiener(self.toas, self.freqs, segs, white_cov, residuals)
+
+    def draw_noise_model_batch(self, n_real, seed=0, real0=0):
+        """n_real draws of N(0, C), C = red_cov + diag(white) (the distribution of
+        draw_noise_model()), on the GPU: device Cholesky + Philox normals + MFMA triangular
+        product. Realization g uses its own Philox counter, so any split of [real0, real0 + n_real)
+        gives the same draws. Returns [n_real, n_toa]."""
+        segs = self._red_segments()
+        white_cov = self._white_sigma2()
+        if not segs:
+            raise ValueError('draw_noise_model_batch: no time-correlated signal in custom_model')
+        return _capi.get_context().noise_draw(self.toas, self.freqs, segs, white_cov, seed, real0, n_real)
 
     # ------------------------------------------------------------------ deterministic signals
     def add_cgw(self, costheta, phi, cosinc, log10_mc, log10_fgw, log10_h, phase0, psi, psrterm=False):

@@ -99,6 +99,46 @@ int fpta_white_accumulate(fpta_ctx* ctx, int64_t n_toa, const double* sigma, con
                           int64_t n_blocks, const int64_t* block_offs, const int64_t* block_idx,
                           const double* ecorr_sigma, const double* zb, double* residuals);
 
+/* ------------------------------------------------------------------ dense covariance
+ * The reference's covariance-matrix route (fakepta/fake_pta.py:389-420, :493-524). Signals are
+ * given as segments like fpta_gp_accumulate: seg_nmodes[n_seg]; f and w hold sum(seg_nmodes)
+ * values with w = psd * df (the reference's np.repeat(psd * df, 2)); seg_idx / seg_freqf give
+ * each segment's chromatic factor (freqf/nu)^idx. For a backend's system noise pass only that
+ * backend's TOAs (the reference builds the covariance of the masked TOAs, :398-405).
+ * white_var: NULL or [n_toa] white-noise variances, added on the diagonal. */
+
+/* Replaces make_time_correlated_noise_cov (fakepta/fake_pta.py:389-420) and, summed over
+ * segments, the red part of make_noise_covariance_matrix (:493-513); with white_var, the
+ * total covariance np.diag(white_cov) + red_cov of draw_noise_model (:517):
+ *   cov[i][j] = sum_s ch_s(i) ch_s(j) sum_k w[k] (cos(2 pi f_k t_i) cos(2 pi f_k t_j)
+ *                                                + sin(2 pi f_k t_i) sin(2 pi f_k t_j))
+ *               + (i == j ? white_var[i] : 0)
+ * Basis generation + fp64 MFMA Gram (lower tiles, mirrored). cov: host [n_toa][n_toa]. */
+int fpta_gp_covariance(fpta_ctx* ctx, int64_t n_toa, const double* toas, const double* nu,
+                       int32_t n_seg, const int32_t* seg_nmodes, const double* f, const double* w,
+                       const double* seg_idx, const double* seg_freqf, const double* white_var,
+                       double* cov);
+
+/* Replaces draw_noise_model(residuals) (fakepta/fake_pta.py:520-523), the Wiener estimate
+ *   out = red_cov^T C^-1 residuals,  C = red_cov + diag(white_var),
+ * evaluated as residuals - white_var * C^-1 residuals (red_cov is symmetric) through a device
+ * Cholesky factorisation of C instead of the reference's explicit inverse. white_var is
+ * required. FPTA_EINVAL if C is not positive definite. out may alias residuals. */
+int fpta_noise_wiener(fpta_ctx* ctx, int64_t n_toa, const double* toas, const double* nu,
+                      int32_t n_seg, const int32_t* seg_nmodes, const double* f, const double* w,
+                      const double* seg_idx, const double* seg_freqf, const double* white_var,
+                      const double* residuals, double* out);
+
+/* Batched draw_noise_model() (fakepta/fake_pta.py:518-519): n_real realizations of N(0, C),
+ * C = red_cov + diag(white_var), as x = L z with L the device Cholesky factor of C and z
+ * Philox normals ctr = (toa, 0xFFFFFFFF, 0xFFFFFFF2, g >> 1), pick [g & 1], g = real0 + r.
+ * Same distribution as the reference's np.random.multivariate_normal (which factors C by SVD);
+ * the draws themselves follow this library's stream. out: host [n_real][n_toa]. */
+int fpta_noise_draw(fpta_ctx* ctx, int64_t n_toa, const double* toas, const double* nu,
+                    int32_t n_seg, const int32_t* seg_nmodes, const double* f, const double* w,
+                    const double* seg_idx, const double* seg_freqf, const double* white_var,
+                    uint64_t seed, int64_t real0, int32_t n_real, double* out);
+
 /* ------------------------------------------------------------------ batched realizations
  * Many independent realizations of the whole array on device (north-star steps 1-4):
  * Philox4x32-10 draws -> ORF mixing -> fused basis/contraction -> white/ECORR.
@@ -167,7 +207,8 @@ int fpta_set_option(fpta_ctx* ctx, int32_t key, int64_t value);
 #define FPTA_K_MIX 1
 #define FPTA_K_SYNTH 2
 #define FPTA_K_WHITE 3
-#define FPTA_K_N 4
+#define FPTA_K_DENSE 4 /* dense covariance: basis + Gram, Cholesky, solves, draws */
+#define FPTA_K_N 5
 /* Accumulated launches and HIP-event milliseconds of kernel `which` since the last reset. */
 int fpta_kernel_stats(fpta_ctx* ctx, int32_t which, int64_t* count, double* total_ms);
 int fpta_reset_stats(fpta_ctx* ctx);

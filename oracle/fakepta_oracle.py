@@ -314,6 +314,7 @@ def box_muller(x):
 WHITE_PSR_WORD = 0xFFFFFFFF
 WHITE_STREAM = 0xFFFFFFF0
 ECORR_STREAM = 0xFFFFFFF1
+DENSE_STREAM = 0xFFFFFFF2
 
 
 def seed_key(seed):
@@ -334,7 +335,7 @@ def gp_normals(seed, reals, p, seg, n_modes):
     return box_muller(philox4x32_10(ctr, seed_key(seed)))
 
 
-def white_normals_rpairs(seed, reals, n_toa):
+def white_normals_rpairs(seed, reals, n_toa, stream=WHITE_STREAM):
     """White-noise stream: one normal per (realization, TOA), paired over REALIZATIONS so a GPU lane
     owning a TOA uses both outputs of one Box-Muller: ctr = (t, 0xFFFFFFFF, 0xFFFFFFF0, g >> 1),
     pick [g & 1] for global realization g. Returns [len(reals), n_toa]."""
@@ -343,7 +344,7 @@ def white_normals_rpairs(seed, reals, n_toa):
     ctr = np.zeros((len(reals), n_toa, 4), dtype=np.uint32)
     ctr[..., 0] = t.astype(np.uint32)[None, :]
     ctr[..., 1] = WHITE_PSR_WORD
-    ctr[..., 2] = WHITE_STREAM
+    ctr[..., 2] = stream
     ctr[..., 3] = (reals >> np.uint64(1)).astype(np.uint32)[:, None]
     z = box_muller(philox4x32_10(ctr, seed_key(seed)))
     pick = (reals & np.uint64(1)).astype(np.int64)[:, None, None]
@@ -423,3 +424,39 @@ def batch_synth(offs, toas, freqs, segments, seed, real0, n_real, sigma=None, bl
         has = block_of >= 0
         out[:, has] += ecorr_sigma[block_of[has]][None, :] * zb[:, block_of[has]]
     return out
+
+
+# ----------------------------------------------------------------------------- dense covariance
+def dense_cov_signal(toas, freqs, f, psd, idx, freqf=1400.0):
+    """make_time_correlated_noise_cov (fake_pta.py:389-420): basis [n, 2N] with the chromatic
+    factor, cov = basis diag(repeat(psd df, 2)) basis^T."""
+    df = np.diff(np.append(0, f))
+    w = np.repeat(psd * df, 2)
+    basis = np.zeros((len(toas), 2 * len(f)))
+    ch = (freqf / freqs) ** idx
+    for i in range(len(f)):
+        basis[:, 2 * i] = ch * np.cos(2 * np.pi * f[i] * toas)
+        basis[:, 2 * i + 1] = ch * np.sin(2 * np.pi * f[i] * toas)
+    return np.dot(basis, np.dot(np.diag(w), basis.T))
+
+
+def dense_cov(toas, freqs, signals, freqf=1400.0):
+    """red part of make_noise_covariance_matrix (fake_pta.py:505-512): sum over (f, psd, idx)."""
+    red = np.zeros((len(toas), len(toas)))
+    for f, psd, idx in signals:
+        red += dense_cov_signal(toas, freqs, f, psd, idx, freqf)
+    return red
+
+
+def wiener_reference(white_cov, red_cov, residuals):
+    """draw_noise_model(residuals) (fake_pta.py:516-523), the reference's explicit-inverse form."""
+    cov = np.diag(white_cov) + red_cov
+    return np.dot(red_cov.T, np.dot(np.linalg.inv(cov), residuals))
+
+
+def dense_draws(cov, seed, real0, n_real):
+    """Batched N(0, cov) draws of this build: x_r = L z_r with L = cholesky(cov) and z the
+    DENSE_STREAM normals (ctr = (toa, 0xFFFFFFFF, 0xFFFFFFF2, g >> 1), pick [g & 1])."""
+    L = np.linalg.cholesky(cov)
+    z = white_normals_rpairs(seed, np.arange(real0, real0 + n_real), cov.shape[0], stream=DENSE_STREAM)
+    return z @ L.T

@@ -152,3 +152,33 @@ def test_batch_semantics_match_reference_loop():
                                  [freqs[offs[i]:offs[i + 1]] for i in range(P)], fc, psdc, zc, L, 0.0)
     ref += np.concatenate(res)
     assert_parity(out, ref, 1e-12)
+
+
+def test_dense_covariance_oracle_vs_g6(golden):
+    """make_time_correlated_noise_cov / make_noise_covariance_matrix / draw_noise_model(residuals)
+    restated in oracle.dense_* reproduce the reference's outputs (fake_pta.py:389-420, :493-524)."""
+    g = golden("g6_dense_cov.npz")
+    sigs = []
+    for lab in ("rn", "dm", "sv"):
+        f, psd, idx = g[f"{lab}_f"], g[f"{lab}_psd"], float(g[f"{lab}_idx"])
+        assert_parity(O.dense_cov_signal(g["toas"], g["freqs"], f, psd, idx), g[f"{lab}_cov"], 1e-14)
+        sigs.append((f, psd, idx))
+    red = O.dense_cov(g["toas"], g["freqs"], sigs)
+    assert_parity(red, g["red_cov"], 1e-14)
+    flags = g["backend_flags"]
+    sig = np.zeros(len(g["toas"]))
+    for b, ef, tq in zip(("A.1400", "B.800"), g["efac"], g["tnequad"]):
+        m = flags == b
+        sig[m] = np.sqrt(ef ** 2 * g["toaerrs"][m] ** 2 + 10 ** (2 * tq))
+    assert_parity(sig ** 2, g["white_cov"], 1e-15)
+    assert_parity(O.wiener_reference(g["white_cov"], red, g["residuals"]), g["wiener"], 1e-12)
+
+
+def test_dense_draws_oracle_distribution():
+    """dense_draws = cholesky(C) z with the DENSE_STREAM normals: x x^T / R -> C."""
+    rng = np.random.default_rng(1)
+    A = rng.normal(size=(6, 6))
+    C = A @ A.T + 6 * np.eye(6)
+    x = O.dense_draws(C, 5, 0, 40000)
+    S = x.T @ x / len(x)
+    assert np.max(np.abs(S - C) / np.sqrt(np.outer(np.diag(C), np.diag(C)))) < 0.03

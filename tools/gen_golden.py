@@ -19,6 +19,8 @@ Fixture map:
   g4_make_fake_array.npz + g4_noisedict.json
                       config 1 (BASELINE configs[0]) end-to-end with np.random.seed(0)
   g5_tutorial.json    known answers printed in examples/tutorial.ipynb
+  g6_dense_cov.npz    one 2-backend pulsar: make_time_correlated_noise_cov per GP,
+                      make_noise_covariance_matrix, draw_noise_model(residuals) (Wiener)
 """
 import json
 import os
@@ -239,6 +241,39 @@ def gen_g5():
                   fh, indent=1)
 
 
+def gen_g6(fp):
+    rng = np.random.default_rng(17)
+    yr = 365.25 * 24 * 3600
+    epochs = _ragged_epochs(rng, 80, 0.2 * yr, 30.1 * 24 * 3600)
+    np.random.seed(23)
+    psr = fp.Pulsar(epochs, 2e-7, 0.4, 2.2, pdist=(1.0, 0.2), freqs=[1400],
+                    backends=["A.1400", "B.800"],
+                    custom_model={"RN": 30, "DM": 100, "Sv": 30})
+    for b in psr.backends:
+        psr.noisedict[f"{psr.name}_{b}_efac"] = {"A.1400": 1.2, "B.800": 0.9}[b]
+        psr.noisedict[f"{psr.name}_{b}_log10_tnequad"] = {"A.1400": -6.8, "B.800": -7.1}[b]
+    psr.add_red_noise(spectrum="powerlaw", log10_A=-13.9, gamma=3.1)
+    psr.add_dm_noise(spectrum="powerlaw", log10_A=-13.5, gamma=2.2)
+    psr.add_chromatic_noise(spectrum="powerlaw", log10_A=-13.8, gamma=1.8)
+    psr.add_white_noise()
+    d = dict(toas=psr.toas.copy(), freqs=psr.freqs.copy(), toaerrs=psr.toaerrs.copy(),
+             backend_flags=psr.backend_flags.astype("U"), name=np.array(psr.name),
+             residuals=psr.residuals.copy(),
+             efac=np.array([psr.noisedict[f"{psr.name}_{b}_efac"] for b in ("A.1400", "B.800")]),
+             tnequad=np.array([psr.noisedict[f"{psr.name}_{b}_log10_tnequad"] for b in ("A.1400", "B.800")]))
+    for sig, lab in (("red_noise", "rn"), ("dm_gp", "dm"), ("chrom_gp", "sv")):
+        sm = psr.signal_model[sig]
+        d[f"{lab}_f"] = sm["f"]
+        d[f"{lab}_psd"] = sm["psd"]
+        d[f"{lab}_idx"] = float(sm["idx"])
+        d[f"{lab}_cov"] = psr.make_time_correlated_noise_cov(signal=sig)
+    white_cov, red_cov = psr.make_noise_covariance_matrix()
+    d["white_cov"] = white_cov
+    d["red_cov"] = red_cov
+    d["wiener"] = psr.draw_noise_model(residuals=psr.residuals)
+    np.savez_compressed(os.path.join(OUT, "g6_dense_cov.npz"), **d)
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
     fp, cn, sp = ref_shim.load_reference()
@@ -247,6 +282,7 @@ def main():
     gen_g3(fp, cn)
     gen_g4(fp)
     gen_g5()
+    gen_g6(fp)
     for fn in sorted(os.listdir(OUT)):
         print(fn, os.path.getsize(os.path.join(OUT, fn)))
 
