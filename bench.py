@@ -29,7 +29,8 @@ METRIC = "residual samples/sec (TOA×realization) for 100-psr HD GWB; % FP64 pea
 FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 matrix (= vector) peak, AMD datasheet (MI355X_MICROARCH.md lists none)
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 SYNTH_KERNELS = {0: ("k_synth_valu_seeded<2,16>", "fp64-valu"), 3: ("k_synth_valu_seeded<2,16>", "fp64-valu"),
-                 2: ("k_synth_mfma<4,2>", "fp64-mfma"), 1: ("k_synth_direct", "fp64-valu")}
+                 2: ("k_synth_mfma<4,2>", "fp64-mfma"), 1: ("k_synth_direct", "fp64-valu"),
+                 4: ("k_grid_interp", "fp64-valu")}
 
 
 def parse():
@@ -42,7 +43,7 @@ def parse():
     ap.add_argument("--ntoa", type=int, default=2000)
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--cpu-sample", type=int, default=8, help="realizations timed for the CPU baseline (0: skip)")
-    ap.add_argument("--path", type=int, default=0, help="synthesis path: 0 auto, 1 direct, 2 MFMA, 3 VALU")
+    ap.add_argument("--path", type=int, default=0, help="synthesis path: 0 auto, 1 direct, 2 MFMA, 3 VALU, 4 gridded")
     ap.add_argument("--anchor", type=int, default=0, help="recurrence re-anchor interval (0: library default)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL on ROCm) or gloo (CPU rehearsal)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
@@ -198,7 +199,8 @@ def main():
 
     ctx.set_option(_capi.OPT_PROFILE, 0)
     kstats = {name: ctx.kernel_stats(k) for name, k in
-              (("gen", _capi.K_GEN), ("mix", _capi.K_MIX), ("synth", _capi.K_SYNTH), ("white", _capi.K_WHITE))}
+              (("gen", _capi.K_GEN), ("mix", _capi.K_MIX), ("grid", _capi.K_GRID), ("synth", _capi.K_SYNTH),
+               ("white", _capi.K_WHITE))}
     sums = ctx.batch_checksums()  # last step's realizations
     all_sums = comm.gather(sums)
     n_samples_total = info["n_toa"] * R * args.steps * world

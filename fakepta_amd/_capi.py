@@ -53,6 +53,7 @@ _SIGS = [
     ("fpta_batch_checksums", _c_int, [_ctx_p, _vp]),
     ("fpta_batch_correlations", _c_int, [_ctx_p, _i32, _vp]),
     ("fpta_batch_info", _c_int, [_ctx_p, _vp]),
+    ("fpta_batch_grid_info", _c_int, [_ctx_p, _vp]),
     ("fpta_set_option", _c_int, [_ctx_p, _i32, _i64]),
     ("fpta_kernel_stats", _c_int, [_ctx_p, _i32, ctypes.POINTER(_i64), ctypes.POINTER(_dbl)]),
     ("fpta_reset_stats", _c_int, [_ctx_p]),
@@ -67,7 +68,8 @@ for _name, _res, _args in _SIGS:
 EXPORTED = [s[0] for s in _SIGS]
 
 OPT_SYNTH_PATH, OPT_MFMA_MIN_REAL, OPT_PROFILE, OPT_ANCHOR, OPT_VALU_VARIANT, OPT_FUSE_WHITE = 1, 2, 3, 4, 5, 6
-K_GEN, K_MIX, K_SYNTH, K_WHITE, K_DENSE = 0, 1, 2, 3, 4
+OPT_GRID_WIDTH, OPT_GRID_SIGMA = 7, 8
+K_GEN, K_MIX, K_SYNTH, K_WHITE, K_DENSE, K_GRID = 0, 1, 2, 3, 4, 5
 
 
 class FptaError(RuntimeError):
@@ -264,6 +266,16 @@ class Context:
         info = np.zeros(5, dtype=np.int64)
         self._check(_lib.fpta_batch_info(self._h, _ptr(info)), "fpta_batch_info")
         return dict(n_psr=int(info[0]), n_toa=int(info[1]), n_seg=int(info[2]), K=int(info[3]), max_np=int(info[4]))
+
+    def batch_grid_info(self):
+        """Gridded-path plan figures and the path of the last batch (fpta_batch_grid_info)."""
+        g = np.zeros(8, dtype=np.float64)
+        self._check(_lib.fpta_batch_grid_info(self._h, _ptr(g)), "fpta_batch_grid_info")
+        keys = ("last_path", "ok", "n_chunks", "fma_dft", "fma_interp", "fma_direct", "grid_vals", "weight_bytes")
+        d = dict(zip(keys, g.tolist()))
+        d["last_path"] = int(d["last_path"])
+        d["ok"] = bool(d["ok"])
+        return d
 
     def batch_synth(self, seed, real0, n_real, to_host=True, coeffs=False):
         info = self.batch_info()

@@ -54,7 +54,41 @@ struct DevBuf {
 struct Seg {
   SegDesc d{};
   int32_t nm_orig = 0;
+  std::vector<double> h_w0;  // first angular frequency per row ([P] for kind 0, [1] for kind 1)
   DevBuf w, amp, L, mask;
+};
+
+// Gridded-synthesis tables of one signal (grid.hip): real-DFT table E, interpolation weights.
+struct GridSeg {
+  int32_t nf = 0, half = 0, lde = 0, rmax = 0;
+  DevBuf ecos, esin, wd, js, g;
+};
+
+// Gridded-synthesis plan of a layout (built once per layout, reused by every batch).
+struct GridPlan {
+  bool built = false;
+  bool ok = false;           // usable for this layout (harmonic, <= kGridMaxSeg signals)
+  std::string why;           // reason when !ok
+  int32_t w = 0;             // kernel width (grid cells)
+  double sigma = 0.0;        // oversampling
+  int32_t n_chunks = 0;
+  DevBuf chunks;             // int4 {pulsar, first TOA (pulsar-local), count, 0}
+  std::vector<GridSeg*> segs;
+  double fma_grid = 0.0;     // FMAs per realization: DFT + interpolation
+  double fma_dft = 0.0;      // FMAs per realization in k_grid_dft
+  double fma_interp = 0.0;   // FMAs per realization in k_grid_interp (dense band, padded TOA slots)
+  double grid_vals = 0.0;    // grid values per realization (sum over signals of P nf)
+  double weight_bytes = 0.0; // interpolation weight tables
+  double fma_direct = 0.0;   // FMAs per realization of the direct contraction
+  int64_t g_rpad = 0;        // R_pad the grid buffers are sized for
+  ~GridPlan() { clear(); }
+  void clear() {
+    for (GridSeg* g : segs) delete g;
+    segs.clear();
+    built = ok = false;
+    n_chunks = 0;
+    g_rpad = 0;
+  }
 };
 
 // A device-resident pulsar array plus its GP signals.
@@ -63,6 +97,7 @@ struct Layout {
   int64_t n_toa = 0;
   int64_t max_np = 0;
   std::vector<int64_t> h_offs;
+  std::vector<double> h_toas;
   DevBuf offs, toas, nu, psr_of;
   std::vector<Seg*> segs;
   DevBuf segdesc;
@@ -75,6 +110,7 @@ struct Layout {
   DevBuf tiles;
   int32_t n_tiles = 0;
   int64_t tiles_R = -1;
+  GridPlan grid;
   ~Layout() { clear_signals(); }
   void clear_signals() {
     for (Seg* s : segs) delete s;
@@ -82,6 +118,7 @@ struct Layout {
     K = 0;
     dirty = true;
     tiles_R = -1;
+    grid.clear();
   }
 };
 
@@ -108,6 +145,9 @@ struct fpta_ctx {
   int anchor = 0;  // 0: phasor recurrence anchored once per segment
   int valu_variant = 1;  // seeded (MT 2, NT 16): fastest on C2 (profiles/r01_sweep_*.txt)
   int fuse_white = 1;    // add white/ECORR in the seeded kernel's epilogue
+  int last_path = 0;     // synthesis path of the last batch (1 direct, 2 MFMA, 3 VALU, 4 gridded)
+  int grid_w = 13;       // gridded path: kernel width in grid cells
+  int grid_sigma100 = 200;  // gridded path: oversampling x 100
   // profiling
   struct Pending {
     int which;
@@ -207,6 +247,7 @@ int layout_set_toas(fpta_ctx* c, Layout& L, int32_t P, const int64_t* offs, cons
   L.n_toa = N;
   L.max_np = mx;
   L.h_offs.assign(offs, offs + P + 1);
+  L.h_toas.assign(toas, toas + N);
   std::vector<int32_t> psr_of(N);
   for (int32_t p = 0; p < P; ++p)
     for (int64_t t = offs[p]; t < offs[p + 1]; ++t) psr_of[t] = p;
@@ -257,6 +298,7 @@ int layout_add_signal(fpta_ctx* c, Layout& L, int32_t kind, int32_t nm, const do
   }
   Seg* s = new Seg();
   s->nm_orig = nm;
+  for (int32_t r = 0; r < rows; ++r) s->h_w0.push_back(w[(size_t)r * nmp]);
   int rc;
   if ((rc = upload(c, s->w, w.data(), sizeof(double) * w.size(), "add_signal w")) ||
       (rc = upload(c, s->amp, a.data(), sizeof(double) * a.size(), "add_signal amp"))) {
@@ -303,6 +345,7 @@ int layout_add_signal(fpta_ctx* c, Layout& L, int32_t kind, int32_t nm, const do
 
 int layout_finalize(fpta_ctx* c, Layout& L) {
   if (!L.dirty) return FPTA_OK;
+  L.grid.clear();
   std::vector<SegDesc> d;
   bool harm = !L.segs.empty();
   for (Seg* s : L.segs) {
@@ -384,6 +427,226 @@ int build_tiles(fpta_ctx* c, Layout& L, int32_t R, int32_t tile_toa, int32_t til
   return FPTA_OK;
 }
 
+
+// ------------------------------------------------------------------------------- gridded plan
+// Gauss-Legendre nodes/weights on [-1, 1] (Newton on P_n; host, once per plan).
+void gauss_legendre(int n, std::vector<double>& x, std::vector<double>& wt) {
+  x.assign(n, 0.0);
+  wt.assign(n, 0.0);
+  for (int i = 0; i < (n + 1) / 2; ++i) {
+    double z = std::cos(M_PI * (i + 0.75) / (n + 0.5)), dp = 1.0;
+    for (int it = 0; it < 100; ++it) {
+      double p0 = 1.0, p1 = z;
+      for (int k = 2; k <= n; ++k) {
+        const double p2 = ((2.0 * k - 1.0) * z * p1 - (k - 1.0) * p0) / k;
+        p0 = p1;
+        p1 = p2;
+      }
+      dp = n * (z * p1 - p0) / (z * z - 1.0);
+      const double dz = p1 / dp;
+      z -= dz;
+      if (std::fabs(dz) < 1e-16) break;
+    }
+    x[i] = -z;
+    x[n - 1 - i] = z;
+    wt[i] = wt[n - 1 - i] = 2.0 / ((1.0 - z * z) * dp * dp);
+  }
+}
+
+// Build the gridded plan (grid.hip) of layout L: per signal the grid size nf, the deconvolved real-DFT
+// table, the chunking of every pulsar's TOAs into runs of <= kGridTT whose interpolation rows span at
+// most kGridRowCap cells, and the dense banded weights (device). Not usable -> ok = false + why.
+constexpr int kGridRowCap = 48;
+constexpr double kGridAutoRatio = 0.5;  // auto path: gridded when it needs < half the direct FMAs
+int grid_build(fpta_ctx* c, Layout& L) {
+  GridPlan& G = L.grid;
+  if (G.built && G.w == c->grid_w && G.sigma == c->grid_sigma100 / 100.0) return FPTA_OK;
+  G.clear();
+  G.built = true;
+  G.w = c->grid_w;
+  G.sigma = c->grid_sigma100 / 100.0;
+  const int32_t n_seg = (int32_t)L.segs.size();
+  if (n_seg == 0 || n_seg > kGridMaxSeg) {
+    G.why = "gridded path: needs 1.." + std::to_string(kGridMaxSeg) + " signals";
+    return FPTA_OK;
+  }
+  for (Seg* sg : L.segs)
+    if (!sg->d.harmonic) {
+      G.why = "gridded path: every signal needs a harmonic grid f_k = k f_1";
+      return FPTA_OK;
+    }
+  const int32_t w = G.w;
+  // shape parameter of the exponential-of-semicircle kernel for oversampling sigma (2.31 w at sigma = 2)
+  const double beta = 0.98 * M_PI * w * (1.0 - 0.5 / G.sigma), hw = 0.5 * w;
+  const int64_t N = L.n_toa;
+  // per (segment, TOA): first interpolation row J (unwrapped) and offset d = u - J, u = theta / h
+  std::vector<std::vector<int64_t>> J(n_seg, std::vector<int64_t>(N));
+  std::vector<std::vector<double>> D(n_seg, std::vector<double>(N));
+  std::vector<int32_t> nf(n_seg);
+  for (int32_t s = 0; s < n_seg; ++s) {
+    const SegDesc& d = L.segs[s]->d;
+    int32_t n = (int32_t)std::ceil(G.sigma * (2.0 * d.nm + 1.0));
+    n += n & 1;
+    nf[s] = std::max(n, 2 * w + 2);
+    const double h = 2.0 * M_PI / nf[s];
+    for (int32_t p = 0; p < L.P; ++p) {
+      const double w0 = L.segs[s]->h_w0[d.kind == 0 ? p : 0];
+      for (int64_t t = L.h_offs[p]; t < L.h_offs[p + 1]; ++t) {
+        const double u = (w0 * L.h_toas[t]) / h;
+        if (!std::isfinite(u) || std::fabs(u) > 1e15) {
+          G.why = "gridded path: phase out of range";
+          return FPTA_OK;
+        }
+        const int64_t j = (int64_t)std::floor(u - hw) + 1;
+        J[s][t] = j;
+        D[s][t] = u - (double)j;
+      }
+    }
+  }
+  // chunks: <= kGridTT consecutive TOAs of one pulsar, every signal's band <= kGridRowCap rows
+  std::vector<int4> chunks;
+  std::vector<int32_t> chunk_of(N), tt_of(N);
+  std::vector<std::vector<int2>> js(n_seg);
+  std::vector<int32_t> rmax(n_seg, 0);
+  std::vector<int64_t> lo(n_seg), hi(n_seg);
+  for (int32_t p = 0; p < L.P; ++p) {
+    int64_t t = L.h_offs[p];
+    const int64_t t_end = L.h_offs[p + 1];
+    while (t < t_end) {
+      const int64_t t0 = t;
+      for (int32_t s = 0; s < n_seg; ++s) lo[s] = hi[s] = J[s][t];
+      ++t;
+      // chunks end on multiples of kGridTT in the global TOA index: every full chunk then writes whole
+      // 128-byte lines of each realization row
+      const int64_t t_lim = std::min(t_end, (t0 / kGridTT + 1) * kGridTT);
+      while (t < t_lim) {
+        bool fits = true;
+        for (int32_t s = 0; s < n_seg && fits; ++s)
+          fits = std::max(hi[s], J[s][t]) - std::min(lo[s], J[s][t]) + w + 1 <= kGridRowCap;
+        if (!fits) break;
+        for (int32_t s = 0; s < n_seg; ++s) {
+          lo[s] = std::min(lo[s], J[s][t]);
+          hi[s] = std::max(hi[s], J[s][t]);
+        }
+        ++t;
+      }
+      const int32_t ci = (int32_t)chunks.size();
+      chunks.push_back(make_int4(p, (int)(t0 - L.h_offs[p]), (int)(t - t0), 0));
+      for (int64_t u = t0; u < t; ++u) {
+        chunk_of[u] = ci;
+        tt_of[u] = (int32_t)(u - t0);
+      }
+      for (int32_t s = 0; s < n_seg; ++s) {
+        int32_t rows = (int32_t)(hi[s] - lo[s]) + w;
+        rows += rows & 1;  // k_grid_interp consumes rows in pairs (the pad row has zero weights)
+        const int64_t m = ((lo[s] % nf[s]) + nf[s]) % nf[s];
+        js[s].push_back(make_int2((int)m, rows));
+        rmax[s] = std::max(rmax[s], rows);
+        for (int64_t u = t0; u < t; ++u) J[s][u] -= lo[s];  // row of the TOA's first weight in the chunk
+      }
+    }
+  }
+  if (chunks.size() > (size_t)0x7FFFFFFF / 8) {
+    G.why = "gridded path: too many chunks";
+    return FPTA_OK;
+  }
+  G.n_chunks = (int32_t)chunks.size();
+  int rc;
+  if ((rc = upload(c, G.chunks, chunks.data(), sizeof(int4) * chunks.size(), "grid chunks"))) return rc;
+  DevBuf d_chunk_of, d_tt_of, d_row, d_d;
+  if ((rc = upload(c, d_chunk_of, chunk_of.data(), sizeof(int32_t) * N, "grid chunk_of")) ||
+      (rc = upload(c, d_tt_of, tt_of.data(), sizeof(int32_t) * N, "grid tt_of")))
+    return rc;
+  std::vector<double> gx, gw;
+  gauss_legendre(256, gx, gw);
+  G.fma_direct = 0.0;
+  G.fma_grid = 0.0;
+  for (int32_t s = 0; s < n_seg; ++s) {
+    const SegDesc& d = L.segs[s]->d;
+    GridSeg* gs = new GridSeg();
+    G.segs.push_back(gs);
+    gs->nf = nf[s];
+    gs->half = nf[s] / 2;
+    gs->lde = gs->half + 1 + kGridMI;
+    gs->rmax = rmax[s];
+    // q_k = (2 pi / nf) / phi_hat(k), phi_hat(k) = alpha int_{-1}^{1} phi(z) cos(k alpha z) dz, alpha = pi w / nf
+    const double alpha = M_PI * w / nf[s];
+    std::vector<double> ec((size_t)d.nm * gs->lde, 0.0), es((size_t)d.nm * gs->lde, 0.0);
+    for (int32_t m = 0; m < d.nm; ++m) {
+      const int64_t k = m + 1;
+      double ph = 0.0;
+      for (size_t q = 0; q < gx.size(); ++q)
+        ph += gw[q] * std::exp(beta * (std::sqrt(1.0 - gx[q] * gx[q]) - 1.0)) * std::cos(k * alpha * gx[q]);
+      const double qk = (2.0 * M_PI / nf[s]) / (alpha * ph);
+      for (int32_t j = 0; j <= gs->half; ++j) {
+        const double a = 2.0 * M_PI * (double)((k * j) % nf[s]) / nf[s];  // exact argument reduction
+        ec[(size_t)m * gs->lde + j] = qk * std::cos(a);
+        es[(size_t)m * gs->lde + j] = qk * std::sin(a);
+      }
+    }
+    if ((rc = upload(c, gs->ecos, ec.data(), sizeof(double) * ec.size(), "grid ecos")) ||
+        (rc = upload(c, gs->esin, es.data(), sizeof(double) * es.size(), "grid esin")) ||
+        (rc = upload(c, gs->js, js[s].data(), sizeof(int2) * js[s].size(), "grid js")))
+      return rc;
+    std::vector<int32_t> row(J[s].begin(), J[s].end());
+    if ((rc = upload(c, d_row, row.data(), sizeof(int32_t) * N, "grid rows")) ||
+        (rc = upload(c, d_d, D[s].data(), sizeof(double) * N, "grid offsets")))
+      return rc;
+    const size_t wbytes = sizeof(double) * ((size_t)G.n_chunks * gs->rmax + 1) * kGridTT;
+    HIPCHK(c, gs->wd.ensure(wbytes), "grid weights alloc");
+    HIPCHK(c, hipMemsetAsync(gs->wd.p, 0, wbytes, c->stream), "grid weights memset");
+    HIPCHK(c,
+           launch_grid_weights(c->stream, d, N, L.nu.as<double>(), d_chunk_of.as<int32_t>(), d_tt_of.as<int32_t>(),
+                               d_row.as<int32_t>(), d_d.as<double>(), w, beta, gs->rmax, gs->wd.as<double>()),
+           "k_grid_weights launch");
+    HIPCHK(c, hipStreamSynchronize(c->stream), "grid weights sync");  // d_row / d_d are reused
+    double rows_sum = 0.0;
+    for (const int2& q : js[s]) rows_sum += q.y;
+    G.fma_direct += 2.0 * d.nm * (double)N;
+    G.fma_dft += (double)L.P * (gs->half + 1) * 2.0 * d.nm;
+    G.fma_interp += rows_sum * kGridTT;
+    G.grid_vals += (double)L.P * gs->nf;
+    G.weight_bytes += (double)wbytes;
+    G.fma_grid = G.fma_dft + G.fma_interp;
+  }
+  G.ok = true;
+  return FPTA_OK;
+}
+
+// Run the gridded synthesis: one DFT launch per signal, then one interpolation launch for all.
+int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad) {
+  GridPlan& G = L.grid;
+  GridSegs gsegs{};
+  gsegs.n = (int32_t)G.segs.size();
+  if (G.g_rpad != R_pad) {
+    for (GridSeg* gs : G.segs) HIPCHK(c, gs->g.ensure(sizeof(double) * (size_t)L.P * gs->nf * R_pad), "grid alloc");
+    G.g_rpad = R_pad;
+  }
+  {
+    KTimer kt(c, FPTA_K_GRID);
+    for (size_t s = 0; s < G.segs.size(); ++s) {
+      GridSeg* gs = G.segs[s];
+      const SegDesc& d = L.segs[s]->d;
+      GridSegDev& g = gsegs.s[s];
+      g.ecos = gs->ecos.as<double>();
+      g.esin = gs->esin.as<double>();
+      g.wd = gs->wd.as<double>();
+      g.js = gs->js.as<int2>();
+      g.g = gs->g.as<double>();
+      g.nf = gs->nf;
+      g.half = gs->half;
+      g.lde = gs->lde;
+      g.rmax = gs->rmax;
+      g.nm = d.nm;
+      g.col0 = d.col0;
+    }
+    HIPCHK(c, launch_grid_dft(c->stream, gsegs, L.P, a.coef, a.K, R_pad), "k_grid_dft launch");
+  }
+  KTimer kt(c, FPTA_K_SYNTH);
+  HIPCHK(c, launch_grid_interp(c->stream, a, G.chunks.as<int4>(), G.n_chunks, gsegs, R_pad), "k_grid_interp launch");
+  return FPTA_OK;
+}
+
 // White noise + ECORR to fuse into the synthesis epilogue (batch path).
 struct WhiteCfg {
   int32_t on = 0;
@@ -417,10 +680,26 @@ int run_synth(fpta_ctx* c, Layout& L, int32_t R, int32_t R_pad, double* out, int
   a.n_real = R;
   a.accumulate = accumulate;
   a.anchor = c->anchor;
-  // path: 1 direct, 2 MFMA, 3 VALU; auto (0) = VALU for R >= mfma_min_real, direct below
+  // path: 1 direct, 2 MFMA, 3 VALU, 4 gridded; auto (0) = gridded when its plan needs fewer than
+  // kGridAutoRatio of the direct FMAs, else VALU, for R >= mfma_min_real; direct below
   int path = c->synth_path;
-  if (path == 0) path = R >= c->mfma_min_real ? 3 : 1;
   if (!allow_mfma) path = 1;
+  if (path == 0 || path == 4) {
+    const bool want = path == 4;
+    if ((want || R >= c->mfma_min_real) && L.all_harmonic && c->anchor == 0) {
+      int rc = grid_build(c, L);
+      if (rc) return rc;
+    }
+    const bool ok = L.grid.built && L.grid.ok;
+    if (want && !ok)
+      return fail(c, FPTA_EINVAL,
+                  L.grid.why.empty() ? std::string("gridded path: needs harmonic grids and anchor 0")
+                                     : L.grid.why);
+    if (ok && (want || L.grid.fma_grid < kGridAutoRatio * L.grid.fma_direct))
+      path = 4;
+    else if (path == 0)
+      path = R >= c->mfma_min_real ? 3 : 1;
+  }
   // host-side guards of what the tiled kernels assume (every tile's realization block lies inside
   // the coefficient padding; the coefficient buffer holds P*K*R_pad values)
   if (R_pad % kRealPad != 0 || R > R_pad || kRealPad % kTileReal != 0 ||
@@ -428,7 +707,22 @@ int run_synth(fpta_ctx* c, Layout& L, int32_t R, int32_t R_pad, double* out, int
     return fail(c, FPTA_EINVAL, "synth: realization padding inconsistent with the tile geometry");
   if (c->coef.cap < sizeof(double) * (size_t)L.P * std::max(L.K, 1) * R_pad)
     return fail(c, FPTA_ESTATE, "synth: coefficient buffer smaller than P*K*R_pad");
-  if (path == 2) {
+  c->last_path = path;
+  if (path == 4) {
+    if (white && white->on && c->fuse_white) {
+      a.w_on = 1;
+      a.w_sigma = white->sigma;
+      a.w_block_of = white->block_of;
+      a.w_esig = white->esig;
+      a.w_zb = white->zb;
+      a.w_nblocks = white->nblocks;
+      a.real0 = white->real0;
+      a.k0 = white->k0;
+      a.k1 = white->k1;
+      if (fused) *fused = true;
+    }
+    return grid_run(c, L, a, R_pad);
+  } else if (path == 2) {
     int rc = build_tiles(c, L, R, kTileToa, kTileReal);
     if (rc) return rc;
     KTimer kt(c, FPTA_K_SYNTH);
@@ -642,8 +936,18 @@ int fpta_set_option(fpta_ctx* c, int32_t key, int64_t value) {
   if (!c) return fail(nullptr, FPTA_EINVAL, "set_option: null ctx");
   switch (key) {
     case FPTA_OPT_SYNTH_PATH:
-      if (value < 0 || value > 3) return fail(c, FPTA_EINVAL, "synth path must be 0, 1, 2 or 3");
+      if (value < 0 || value > 4) return fail(c, FPTA_EINVAL, "synth path must be 0, 1, 2, 3 or 4");
       c->synth_path = (int)value;
+      return FPTA_OK;
+    case FPTA_OPT_GRID_WIDTH:
+      if (value < 4 || value > 24) return fail(c, FPTA_EINVAL, "grid width must be in [4, 24]");
+      c->grid_w = (int)value;
+      c->batch.grid.clear();
+      return FPTA_OK;
+    case FPTA_OPT_GRID_SIGMA:
+      if (value < 125 || value > 400) return fail(c, FPTA_EINVAL, "grid oversampling (x100) must be in [125, 400]");
+      c->grid_sigma100 = (int)value;
+      c->batch.grid.clear();
       return FPTA_OK;
     case FPTA_OPT_FUSE_WHITE:
       c->fuse_white = value ? 1 : 0;
@@ -1119,6 +1423,21 @@ int fpta_batch_info(fpta_ctx* c, int64_t* info) {
   info[2] = (int64_t)c->batch.segs.size();
   info[3] = c->batch.K;
   info[4] = c->batch.max_np;
+  return FPTA_OK;
+}
+
+int fpta_batch_grid_info(fpta_ctx* c, double* out) {
+  if (!c || !out) return fail(c, FPTA_EINVAL, "grid_info: bad arguments");
+  const GridPlan& G = c->batch.grid;
+  const bool ok = G.built && G.ok;
+  out[0] = c->last_path;
+  out[1] = ok ? 1.0 : 0.0;
+  out[2] = ok ? G.n_chunks : 0.0;
+  out[3] = ok ? G.fma_dft : 0.0;
+  out[4] = ok ? G.fma_interp : 0.0;
+  out[5] = ok ? G.fma_direct : 0.0;
+  out[6] = ok ? G.grid_vals : 0.0;
+  out[7] = ok ? G.weight_bytes : 0.0;
   return FPTA_OK;
 }
 

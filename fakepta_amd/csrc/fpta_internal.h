@@ -69,6 +69,31 @@ constexpr int kNumValuVariants = sizeof(kValuVariants) / sizeof(kValuVariants[0]
 constexpr ValuVariant kSeededVariants[] = {{1, 16}, {2, 16}, {1, 8}, {2, 8}, {1, 32}, {4, 16}};
 static_assert(sizeof(kSeededVariants) == sizeof(kValuVariants), "one variant index selects both tables");
 
+// Gridded synthesis (grid.hip): one signal's tables as the kernels see them.
+constexpr int kGridTT = 16;  // TOAs per interpolation chunk
+constexpr int kGridMI = 8;   // grid rows per wave in k_grid_dft
+struct GridSegDev {
+  const double* ecos;  // [nm][lde] q_k cos(2 pi k j / nf), k = m + 1 (zero-padded columns)
+  const double* esin;  // [nm][lde] q_k sin(2 pi k j / nf)
+  const double* wd;    // [n_chunks][rmax][kGridTT] interpolation weights (chromatic factor, mask folded in)
+  const int2* js;      // [n_chunks] {first grid row mod nf, rows}
+  double* g;           // [P][nf][R_pad] grid values of the batch
+  int32_t nf, half, lde, rmax, nm, col0;
+  int32_t nblk;        // k_grid_dft row blocks of this signal (set by launch_grid_dft)
+};
+constexpr int kGridMaxSeg = 16;  // signals per layout on the gridded path (passed by value as kernel arguments)
+struct GridSegs {
+  GridSegDev s[kGridMaxSeg];
+  int32_t n;
+};
+
+hipError_t launch_grid_weights(hipStream_t st, const SegDesc& sd, int64_t n_toa, const double* nu,
+                               const int32_t* chunk_of, const int32_t* tt_of, const int32_t* row_of,
+                               const double* d_of, int32_t w, double beta, int32_t rmax, double* wd);
+hipError_t launch_grid_dft(hipStream_t st, GridSegs gsegs, int32_t P, const double* coef, int32_t K, int32_t R_pad);
+hipError_t launch_grid_interp(hipStream_t st, const SynthArgs& a, const int4* chunks, int32_t n_chunks,
+                              const GridSegs& gsegs, int32_t R_pad);
+
 hipError_t launch_seeds(hipStream_t st, const SegDesc* segs, int32_t n_seg, const int32_t* psr_of,
                         const double* toas, const double* nu, int64_t n_toa, double4* seeds);
 hipError_t launch_synth_valu_seeded(hipStream_t st, const SynthArgs& a, const int4* tiles, int32_t n_tiles,

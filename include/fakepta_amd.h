@@ -194,13 +194,24 @@ int fpta_batch_correlations(fpta_ctx* ctx, int32_t mode, double* out);
 /* info[0]=n_psr info[1]=n_toa_total info[2]=n_seg info[3]=K columns info[4]=max toas/pulsar */
 int fpta_batch_info(fpta_ctx* ctx, int64_t* info);
 
+/* Gridded-path plan of the batch layout and the path the last batch took (for rooflines):
+ * out[0] synthesis path of the last batch (1 direct, 2 MFMA, 3 VALU, 4 gridded), out[1] plan usable,
+ * out[2] interpolation chunks, out[3] k_grid_dft FMAs per realization, out[4] k_grid_interp FMAs per
+ * realization, out[5] direct-contraction FMAs per realization, out[6] grid values per realization,
+ * out[7] interpolation-weight bytes. out: host double[8]. */
+int fpta_batch_grid_info(fpta_ctx* ctx, double* out);
+
 /* ------------------------------------------------------------------ tuning / profiling */
-#define FPTA_OPT_SYNTH_PATH 1     /* 0 auto, 1 direct (sincos per basis element), 2 fp64 MFMA, 3 fp64 VALU fused */
+#define FPTA_OPT_SYNTH_PATH 1     /* 0 auto, 1 direct (sincos per basis element), 2 fp64 MFMA, 3 fp64 VALU fused,
+                                     4 gridded (real DFT to an oversampled phase grid + banded interpolation,
+                                     harmonic grids only; aliasing error ~1e-12 relative at the defaults) */
 #define FPTA_OPT_MFMA_MIN_REAL 2  /* auto: MFMA path when n_real >= this (default 16) */
 #define FPTA_OPT_PROFILE 3        /* 1: time every batch kernel with HIP events on the ctx stream */
 #define FPTA_OPT_ANCHOR 4         /* recurrence re-anchor interval in K-steps of 2 modes (0 = once per signal, default) */
 #define FPTA_OPT_VALU_VARIANT 5   /* tile variant of the VALU fused kernel (0..5) */
 #define FPTA_OPT_FUSE_WHITE 6     /* 1 (default): white/ECORR added in the synthesis epilogue; 0: separate pass */
+#define FPTA_OPT_GRID_WIDTH 7     /* gridded path: interpolation kernel width in grid cells (default 13) */
+#define FPTA_OPT_GRID_SIGMA 8     /* gridded path: grid oversampling x 100 (default 200) */
 int fpta_set_option(fpta_ctx* ctx, int32_t key, int64_t value);
 /* Kernel ids for fpta_kernel_stats */
 #define FPTA_K_GEN 0
@@ -208,7 +219,8 @@ int fpta_set_option(fpta_ctx* ctx, int32_t key, int64_t value);
 #define FPTA_K_SYNTH 2
 #define FPTA_K_WHITE 3
 #define FPTA_K_DENSE 4 /* dense covariance: basis + Gram, Cholesky, solves, draws */
-#define FPTA_K_N 5
+#define FPTA_K_GRID 5  /* gridded path: real-DFT grid values (k_grid_dft); its interpolation counts as SYNTH */
+#define FPTA_K_N 6
 /* Accumulated launches and HIP-event milliseconds of kernel `which` since the last reset. */
 int fpta_kernel_stats(fpta_ctx* ctx, int32_t which, int64_t* count, double* total_ms);
 int fpta_reset_stats(fpta_ctx* ctx);

@@ -460,3 +460,55 @@ def dense_draws(cov, seed, real0, n_real):
     L = np.linalg.cholesky(cov)
     z = white_normals_rpairs(seed, np.arange(real0, real0 + n_real), cov.shape[0], stream=DENSE_STREAM)
     return z @ L.T
+
+
+# ----------------------------------------------------------------------------- gridded synthesis model
+# Numpy model of the library's gridded path (grid.hip, FPTA_OPT_SYNTH_PATH 4): the same sum as
+# gp_synth_vec on a harmonic grid f_k = k f_1 (fake_pta.py:264, correlated_noises.py:120),
+# factored as a type-2 non-uniform FFT. Not a reference function: it documents the approximation
+# and lets the CPU suite check its error bound (tests/test_oracle_golden.py).
+def es_kernel(z, beta):
+    """Exponential of semicircle phi(z) = exp(beta (sqrt(1 - z^2) - 1)) on |z| < 1, else 0."""
+    z = np.asarray(z, dtype=float)
+    s = 1.0 - z * z
+    return np.where(s > 0, np.exp(beta * (np.sqrt(np.maximum(s, 0.0)) - 1.0)), 0.0)
+
+
+def grid_params(n_modes, w=13, sigma=2.0):
+    """Grid size nf >= sigma (2N + 1) (even, >= 2w + 2) and kernel shape beta for width w."""
+    nf = int(np.ceil(sigma * (2 * n_modes + 1)))
+    nf += nf & 1
+    nf = max(nf, 2 * w + 2)
+    beta = 0.98 * np.pi * w * (1.0 - 0.5 / sigma)
+    return nf, beta
+
+
+def grid_deconvolution(n_modes, nf, w, beta, n_quad=256):
+    """q_k = (2 pi / nf) / phi_hat(k), phi_hat(k) = alpha int_{-1}^{1} phi(z) cos(k alpha z) dz with
+    alpha = pi w / nf (Gauss-Legendre quadrature), k = 1..N."""
+    alpha = np.pi * w / nf
+    x, wt = np.polynomial.legendre.leggauss(n_quad)
+    k = np.arange(1, n_modes + 1)
+    ph = alpha * (np.cos(np.outer(k, alpha * x)) @ (wt * es_kernel(x, beta)))
+    return (2.0 * np.pi / nf) / ph
+
+
+def grid_synth(toas, freqs, w0, amp_cos, amp_sin, idx, freqf=1400.0, w=13, sigma=2.0):
+    """sum_k chrom(t) (amp_cos_k cos(k w0 t) + amp_sin_k sin(k w0 t)) through the grid:
+    g_j = sum_k q_k (amp_cos_k cos(2 pi k j / nf) + amp_sin_k sin(2 pi k j / nf)), then
+    r(t) = chrom(t) sum_{i<w} phi((u - J - i) / (w/2)) g_{(J + i) mod nf}, u = w0 t / h, h = 2 pi / nf,
+    J = floor(u - w/2) + 1. amp_* of shape [N] or [R, N]."""
+    amp_cos = np.atleast_2d(amp_cos)
+    amp_sin = np.atleast_2d(amp_sin)
+    N = amp_cos.shape[-1]
+    nf, beta = grid_params(N, w, sigma)
+    q = grid_deconvolution(N, nf, w, beta)
+    k = np.arange(1, N + 1)
+    ang = TWO_PI * ((np.outer(np.arange(nf), k)) % nf) / nf
+    g = (amp_cos * q) @ np.cos(ang).T + (amp_sin * q) @ np.sin(ang).T  # [R, nf]
+    u = (w0 * np.asarray(toas)) / (TWO_PI / nf)
+    J = np.floor(u - 0.5 * w).astype(np.int64) + 1
+    out = np.zeros((amp_cos.shape[0], len(toas)))
+    for i in range(w):
+        out += es_kernel((u - (J + i)) / (0.5 * w), beta)[None, :] * g[:, (J + i) % nf]
+    return chromatic(freqs, idx, freqf)[None, :] * out

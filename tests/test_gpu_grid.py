@@ -1,0 +1,200 @@
+"""Gridded synthesis path (FPTA_OPT_SYNTH_PATH 4, grid.hip) against the CPU oracle.
+
+The gridded path evaluates the same Fourier sums as the direct kernels through an oversampled
+phase grid (real DFT) and a banded exponential-of-semicircle interpolation.
+It is an approximation with a bounded aliasing error: at the defaults (width 13, oversampling 2)
+the error is ~1e-12 relative for a FLAT spectrum (every mode weighs equally, the worst case)
+and smaller for red spectra. Tolerance: the suite's 1e-10; the accuracy tests
+below also check the tighter bound GRID_TOL the defaults are designed for.
+"""
+import numpy as np
+import pytest
+
+from oracle import fakepta_oracle as O
+from tests.conftest import assert_parity, rel_err
+from tests.helpers import common_signal, oracle_segments, per_psr_signal, random_layout
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-10
+GRID_TOL = 2e-11
+
+
+@pytest.fixture(scope="module")
+def capi():
+    from fakepta_amd import _capi
+    return _capi
+
+
+@pytest.fixture(scope="module")
+def ctx(capi):
+    c = capi.Context(0)
+    yield c
+    c.close()
+
+
+@pytest.fixture
+def gridded(ctx, capi):
+    ctx.set_option(capi.OPT_SYNTH_PATH, 4)
+    yield ctx
+    ctx.set_option(capi.OPT_SYNTH_PATH, 0)
+    ctx.set_option(capi.OPT_GRID_WIDTH, 13)
+    ctx.set_option(capi.OPT_GRID_SIGMA, 200)
+    ctx.set_option(capi.OPT_FUSE_WHITE, 1)
+
+
+def _flat_layout(ctx, rng, P=4, n_range=(100, 300), n_modes=100, idx=2.0, t0=4.5e9):
+    offs, toas, nu = random_layout(rng, P, n_range, t_max=1.6e8)
+    toas = toas + t0
+    ctx.batch_set_toas(offs, toas, nu)
+    f, _ = per_psr_signal(rng, offs, toas, n_modes)
+    a = np.full_like(f, 1e-7)
+    ctx.batch_add_signal(0, f, a, idx=idx)
+    return offs, toas, nu, [O.Segment(0, 2 * np.pi * f, a, idx)]
+
+
+@pytest.mark.parametrize("n_modes", [1, 30, 100, 257])
+def test_flat_spectrum_real_epochs(gridded, n_modes):
+    """Worst case for the aliasing error: flat spectrum, real-MJD-like epochs (t ~ 5e9 s)."""
+    rng = np.random.default_rng(n_modes)
+    offs, toas, nu, segs = _flat_layout(gridded, rng, n_modes=n_modes)
+    got = gridded.batch_synth(5, 0, 64)
+    want = O.batch_synth(offs, toas, nu, segs, 5, 0, 64)
+    assert rel_err(got, want) <= GRID_TOL
+    assert_parity(got, want, TOL)
+
+
+def test_width_and_oversampling_options(gridded, capi):
+    """The kernel width sets the error (a narrow kernel is measurably worse); a lower oversampling
+    with a wider kernel stays within tolerance."""
+    rng = np.random.default_rng(3)
+    offs, toas, nu, segs = _flat_layout(gridded, rng, n_modes=60)
+    want = O.batch_synth(offs, toas, nu, segs, 8, 0, 32)
+    gridded.set_option(capi.OPT_GRID_WIDTH, 6)
+    coarse = rel_err(gridded.batch_synth(8, 0, 32), want)
+    gridded.set_option(capi.OPT_GRID_WIDTH, 16)
+    gridded.set_option(capi.OPT_GRID_SIGMA, 150)
+    fine = rel_err(gridded.batch_synth(8, 0, 32), want)
+    assert 1e-9 < coarse < 1e-3
+    assert fine <= GRID_TOL
+
+
+def test_unsorted_and_clustered_toas(gridded):
+    """TOAs in any order (chunks shrink where the band would exceed the row cap) and clustered
+    epochs with long gaps (make_fake_array gaps=True)."""
+    rng = np.random.default_rng(17)
+    P = 6
+    n = rng.integers(50, 400, size=P)
+    offs = np.concatenate([[0], np.cumsum(n)]).astype(np.int64)
+    parts = []
+    for p, k in enumerate(n):
+        centers = rng.uniform(0, 3e8, 5)
+        t = np.concatenate([c + rng.uniform(0, 3e5, k // 5 + 1) for c in centers])[:k]
+        if p % 2:
+            rng.shuffle(t)
+        parts.append(t)
+    toas = np.concatenate(parts)
+    nu = rng.uniform(700, 3000, offs[-1])
+    gridded.batch_set_toas(offs, toas, nu)
+    segs = []
+    for nm, idx in ((30, 0.0), (100, 2.0)):
+        f, a = per_psr_signal(rng, offs, toas, nm)
+        gridded.batch_add_signal(0, f, a, idx=idx)
+        segs.append(O.Segment(0, 2 * np.pi * f, a, idx))
+    f, a, L, _ = common_signal(rng, offs, toas, 30)
+    gridded.batch_add_signal(1, f, a, L=L)
+    segs.append(O.Segment(1, 2 * np.pi * f, a, 0.0, L=L))
+    for real0, R in ((0, 130), (3, 17)):
+        got = gridded.batch_synth(42, real0, R)
+        want = O.batch_synth(offs, toas, nu, segs, 42, real0, R)
+        assert_parity(got, want, TOL)
+
+
+@pytest.mark.parametrize("real0", [0, 7])
+def test_fused_white_matches_separate_pass(gridded, capi, real0):
+    rng = np.random.default_rng(23)
+    offs, toas, nu = random_layout(rng, 5, (30, 200))
+    gridded.batch_set_toas(offs, toas, nu)
+    f, a = per_psr_signal(rng, offs, toas, 30)
+    gridded.batch_add_signal(0, f, a, idx=0.0)
+    sigma = rng.uniform(1e-7, 1e-6, offs[-1])
+    blocks = [np.arange(s, min(s + 3, offs[-1])) for s in range(0, offs[-1], 4)]
+    es = rng.uniform(1e-8, 1e-7, len(blocks))
+    gridded.batch_set_white(sigma, blocks, es)
+    fused = gridded.batch_synth(77, real0, 131)
+    gridded.set_option(capi.OPT_FUSE_WHITE, 0)
+    separate = gridded.batch_synth(77, real0, 131)
+    assert_parity(fused, separate, 1e-13)
+    block_of = -np.ones(offs[-1], dtype=np.int64)
+    for b, q in enumerate(blocks):
+        block_of[q] = b
+    want = O.batch_synth(offs, toas, nu, [O.Segment(0, 2 * np.pi * f, a, 0.0)], 77, real0, 131, sigma=sigma,
+                         block_of=block_of, ecorr_sigma=es)
+    assert_parity(fused, want, TOL)
+
+
+def test_split_invariance_bitwise(gridded):
+    rng = np.random.default_rng(8)
+    offs, toas, nu = random_layout(rng, 6, (40, 300))
+    gridded.batch_set_toas(offs, toas, nu)
+    f, a = per_psr_signal(rng, offs, toas, 41)
+    gridded.batch_add_signal(0, f, a, idx=2.0)
+    full = gridded.batch_synth(2024, 0, 200)
+    parts = np.concatenate([gridded.batch_synth(2024, r0, n) for r0, n in ((0, 64), (64, 100), (164, 36))])
+    np.testing.assert_array_equal(full, parts)
+
+
+def test_non_harmonic_grid_is_refused(gridded, capi):
+    rng = np.random.default_rng(2)
+    offs, toas, nu = random_layout(rng, 3, (20, 50))
+    gridded.batch_set_toas(offs, toas, nu)
+    f = np.sort(rng.uniform(1e-9, 1e-7, (3, 10)), axis=1)
+    gridded.batch_add_signal(0, f, np.full_like(f, 1e-7))
+    with pytest.raises(capi.FptaError, match="harmonic"):
+        gridded.batch_synth(1, 0, 32)
+
+
+def test_c2_full_size_gridded_vs_seeded(ctx, capi):
+    """BASELINE configs[1] (100 psr x 2000 TOAs, RN30 + DM100 + HD30, R = 1024): the gridded path and
+    the exact seeded VALU path agree over the whole block (size-independent cross-check of two
+    different algorithms on the same device coefficients)."""
+    from fakepta_amd import correlated_noises as cn
+    from fakepta_amd import fake_pta as fp
+    from fakepta_amd.batch import BatchSimulator
+    np.random.seed(0)
+    psrs = fp.make_fake_array(npsrs=100, Tobs=10, ntoas=2000, gaps=False, isotropic=True, toaerr=1e-7,
+                              backends="NUPPI.1400", custom_model={"RN": 30, "DM": 100, "Sv": None})
+    cn.add_common_correlated_noise(psrs, orf="hd", log10_A=-15, gamma=13 / 3)
+    sim = BatchSimulator(psrs, white=False, ctx=ctx)
+    try:
+        ctx.set_option(capi.OPT_SYNTH_PATH, 4)
+        grid = sim.synth(1024, seed=1234)
+        ctx.set_option(capi.OPT_SYNTH_PATH, 3)
+        exact = sim.synth(1024, seed=1234)
+    finally:
+        ctx.set_option(capi.OPT_SYNTH_PATH, 0)
+    assert np.all(np.isfinite(grid))
+    assert rel_err(grid, exact) <= GRID_TOL
+    per_real = np.linalg.norm(grid - exact, axis=1) / np.linalg.norm(exact, axis=1)
+    assert per_real.max() <= 5 * GRID_TOL
+    # one realization against the oracle restatement on the device's coefficients
+    segs = oracle_segments(sim)
+    _, co = sim.synth(2, seed=1234, coeffs=True)
+    ctx.set_option(capi.OPT_SYNTH_PATH, 4)
+    try:
+        g2 = sim.synth(2, seed=1234)
+    finally:
+        ctx.set_option(capi.OPT_SYNTH_PATH, 0)
+    np.testing.assert_array_equal(g2, grid[:2])
+    want = np.zeros(sim.n_toa)
+    col = 0
+    for s in segs:
+        for p in range(len(psrs)):
+            sl = slice(sim.offs[p], sim.offs[p + 1])
+            w = s.w[p] if s.kind == 0 else s.w
+            ph = np.outer(sim.toas[sl], w)
+            ch = (s.freqf / sim.freqs[sl]) ** s.idx
+            a = co[p, col:col + 2 * s.n_modes, 1]
+            want[sl] += ch * (np.cos(ph) @ a[0::2] + np.sin(ph) @ a[1::2])
+        col += 2 * s.n_modes
+    assert_parity(grid[1], want, TOL)

@@ -240,7 +240,7 @@ def _build(ctx, rng, P=7, n_range=(20, 260), per_psr=((30, 0.0), (41, 2.0)), com
     return offs, toas, nu, segs, sigma, block_of, es
 
 
-PATHS = [(1, 0), (2, 0)] + [(3, v) for v in range(6)]  # (synth path, VALU variant)
+PATHS = [(1, 0), (2, 0)] + [(3, v) for v in range(6)] + [(4, 0)]  # (synth path, VALU variant); 4 = gridded
 
 
 @pytest.mark.parametrize("path,variant", PATHS)

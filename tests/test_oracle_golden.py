@@ -182,3 +182,24 @@ def test_dense_draws_oracle_distribution():
     x = O.dense_draws(C, 5, 0, 40000)
     S = x.T @ x / len(x)
     assert np.max(np.abs(S - C) / np.sqrt(np.outer(np.diag(C), np.diag(C)))) < 0.03
+
+
+# ----------------------------------------------------------------------------- gridded-path model
+@pytest.mark.parametrize("n_modes,spectrum", [(30, "flat"), (100, "flat"), (100, "red"), (7, "flat")])
+def test_grid_model_error_bound(n_modes, spectrum):
+    """The gridded factorisation (grid.hip) at its defaults (width 13, oversampling 2) reproduces the
+    direct sum to <= 2e-11 relative on real-MJD-like epochs, flat spectrum being the worst case."""
+    rng = np.random.default_rng(n_modes)
+    T = 3.15e8
+    toas = np.sort(rng.uniform(0, T, 1500)) + 4.8e9
+    freqs = rng.uniform(700, 3000, toas.size)
+    f = np.arange(1, n_modes + 1) / T
+    amp = np.ones(n_modes) if spectrum == "flat" else np.arange(1, n_modes + 1) ** (-13 / 6)
+    c = rng.normal(size=(3, n_modes)) * amp
+    s = rng.normal(size=(3, n_modes)) * amp
+    want = O.gp_synth_vec(toas, freqs, f, c, s, 2.0)
+    got = O.grid_synth(toas, freqs, 2 * np.pi * f[0], c, s, 2.0)
+    err = np.linalg.norm(got - want) / np.linalg.norm(want)
+    assert err <= 2e-11, err
+    coarse = O.grid_synth(toas, freqs, 2 * np.pi * f[0], c, s, 2.0, w=6)
+    assert np.linalg.norm(coarse - want) / np.linalg.norm(want) > 1e-9  # the width controls the error
