@@ -28,9 +28,10 @@ sys.path.insert(0, ROOT)
 METRIC = "residual samples/sec (TOA×realization) for 100-psr HD GWB; % FP64 peak"
 FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 matrix (= vector) peak, AMD datasheet (MI355X_MICROARCH.md lists none)
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-SYNTH_KERNELS = {0: ("k_synth_valu_seeded<2,16>", "fp64-valu"), 3: ("k_synth_valu_seeded<2,16>", "fp64-valu"),
-                 2: ("k_synth_mfma<4,2>", "fp64-mfma"), 1: ("k_synth_direct", "fp64-valu"),
-                 4: ("k_grid_interp", "fp64-valu")}
+SYNTH_KERNELS = {3: ("k_synth_valu_seeded<2,16>", "fp64-valu"), 2: ("k_synth_mfma<4,2>", "fp64-mfma"),
+                 1: ("k_synth_direct", "fp64-valu")}
+GRID_INTERP = {True: ("k_grid_interp_mfma<8>", "fp64-mfma"), False: ("k_grid_interp<16>", "fp64-valu")}
+GRID_DFT = {True: "k_grid_dft_mfma<2,2>", False: "k_grid_dft<8>"}
 
 
 def parse():
@@ -45,6 +46,8 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=8, help="realizations timed for the CPU baseline (0: skip)")
     ap.add_argument("--path", type=int, default=0, help="synthesis path: 0 auto, 1 direct, 2 MFMA, 3 VALU, 4 gridded")
     ap.add_argument("--anchor", type=int, default=0, help="recurrence re-anchor interval (0: library default)")
+    ap.add_argument("--grid-mfma", type=int, default=-1,
+                    help="gridded path kernels on MFMA: bit 0 DFT, bit 1 interpolation (-1: library default)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL on ROCm) or gloo (CPU rehearsal)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-derived HBM bytes per synth launch (written by profiles/collect_pmc.py)")
@@ -177,6 +180,8 @@ def main():
         ctx.set_option(_capi.OPT_SYNTH_PATH, args.path)
     if args.anchor:
         ctx.set_option(_capi.OPT_ANCHOR, args.anchor)
+    if args.grid_mfma >= 0:
+        ctx.set_option(_capi.OPT_GRID_MFMA, args.grid_mfma)
     R = args.real
 
     for s in range(args.warmup):
@@ -209,16 +214,49 @@ def main():
     synth_n, synth_ms = kstats["synth"]
     synth_avg_s = synth_ms / max(synth_n, 1) / 1e3
     flops = 2.0 * info["K"] * info["n_toa"] * R
-    achieved = flops / synth_avg_s / 1e12
+    gi = ctx.batch_grid_info()
+    path = gi["last_path"]
+    if path == 4:
+        kernel, pipe = GRID_INTERP[bool(gi["grid_mfma"] & 2)]
+    else:
+        kernel, pipe = SYNTH_KERNELS[path]
     traffic = None
     if os.path.exists(args.traffic):
         try:
             with open(args.traffic) as fh:
                 tr = json.load(fh)
-            if tr.get("K") == info["K"] and tr.get("n_real") == R and tr.get("n_toa") == info["n_toa"]:
+            if (tr.get("K") == info["K"] and tr.get("n_real") == R and tr.get("n_toa") == info["n_toa"]
+                    and kernel.startswith(tr.get("kernel", "?"))):
                 traffic = tr.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             traffic = None
+    out_bytes = 8.0 * info["n_toa"] * R
+    if path == 4:
+        # gridded path: the dominant kernel is the interpolation, an HBM-bound stream:
+        # algorithmic bytes = residual block written once + grid values read once + interpolation weights
+        R_pad = -(-R // 128) * 128
+        alg_bytes = out_bytes + 8.0 * gi["grid_vals"] * R_pad + gi["weight_bytes"]
+        achieved = alg_bytes / synth_avg_s / 1e9
+        grid_n, grid_ms = kstats["grid"]
+        grid_avg_s = grid_ms / max(grid_n, 1) / 1e3
+        dft_flops = 2.0 * gi["fma_dft"] * R_pad
+        roofline = {"bound": "hbm", "pipe": pipe, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": kernel,
+                    "bytes_per_launch": alg_bytes, "avg_launch_ms": synth_avg_s * 1e3,
+                    "write_GBps": out_bytes / synth_avg_s / 1e9,
+                    "interp_fp64_TFLOPs": 2.0 * gi["fma_interp"] * R_pad / synth_avg_s / 1e12,
+                    "dft": {"kernel": GRID_DFT[bool(gi["grid_mfma"] & 1)], "avg_launch_ms": grid_avg_s * 1e3,
+                            "flops_per_launch": dft_flops, "TFLOPs": dft_flops / max(grid_avg_s, 1e-12) / 1e12,
+                            "frac_fp64_peak": dft_flops / max(grid_avg_s, 1e-12) / 1e12 / FP64_PEAK_TFLOPS},
+                    "direct_equivalent_TFLOPs": flops / (synth_avg_s + grid_avg_s) / 1e12}
+    else:
+        # exact paths: compute (FP64) bound, 2K FLOP per 8-byte sample = 80 FLOP/B at K = 320. The peak is
+        # the MI355X FP64 datasheet figure, equal for the vector and matrix pipes (DESIGN.md §5 Calibration)
+        achieved = flops / synth_avg_s / 1e12
+        roofline = {"bound": "mfma", "pipe": pipe, "achieved": achieved, "peak": FP64_PEAK_TFLOPS,
+                    "unit": "TFLOP/s", "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic, "kernel": kernel,
+                    "flops_per_launch": flops, "avg_launch_ms": synth_avg_s * 1e3,
+                    "write_GBps": out_bytes / synth_avg_s / 1e9}
 
     if rank == 0:
         line = {
@@ -229,15 +267,8 @@ def main():
                                    "%d realizations/GPU/step, Philox seed %d" % (args.npsr, args.ntoa, R, args.seed),
                        "n_psr": args.npsr, "n_toa_total": info["n_toa"], "K": info["K"], "realizations_per_gpu": R,
                        "parallelism": "realization-sharded x%d" % world},
-            # compute (FP64) bound: 2K FLOP per 8-byte sample = 80 FLOP/B at K = 320. The peak is the
-            # MI355X FP64 datasheet figure, equal for the vector and matrix pipes; the default kernel
-            # issues v_fma_f64 (DESIGN.md §5 Calibration), the MFMA kernel is --path 2.
-            "roofline": {"bound": "mfma", "pipe": SYNTH_KERNELS[args.path][1], "achieved": achieved,
-                         "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
-                         "kernel": SYNTH_KERNELS[args.path][0], "flops_per_launch": flops,
-                         "avg_launch_ms": synth_avg_s * 1e3,
-                         "write_GBps": 8.0 * info["n_toa"] * R / synth_avg_s / 1e9},
+            "synth_path": {1: "direct", 2: "mfma", 3: "valu-seeded", 4: "gridded"}.get(path, str(path)),
+            "roofline": roofline,
             "kernels_ms_per_step": {k: (v[1] / max(v[0], 1)) * (v[0] / max(args.steps, 1)) for k, v in kstats.items()},
             "checksum": float(np.sum(all_sums[..., 1])),
         }

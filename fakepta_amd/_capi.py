@@ -68,7 +68,7 @@ for _name, _res, _args in _SIGS:
 EXPORTED = [s[0] for s in _SIGS]
 
 OPT_SYNTH_PATH, OPT_MFMA_MIN_REAL, OPT_PROFILE, OPT_ANCHOR, OPT_VALU_VARIANT, OPT_FUSE_WHITE = 1, 2, 3, 4, 5, 6
-OPT_GRID_WIDTH, OPT_GRID_SIGMA = 7, 8
+OPT_GRID_WIDTH, OPT_GRID_SIGMA, OPT_GRID_MFMA = 7, 8, 9
 K_GEN, K_MIX, K_SYNTH, K_WHITE, K_DENSE, K_GRID = 0, 1, 2, 3, 4, 5
 
 
@@ -269,12 +269,14 @@ class Context:
 
     def batch_grid_info(self):
         """Gridded-path plan figures and the path of the last batch (fpta_batch_grid_info)."""
-        g = np.zeros(8, dtype=np.float64)
+        g = np.zeros(9, dtype=np.float64)
         self._check(_lib.fpta_batch_grid_info(self._h, _ptr(g)), "fpta_batch_grid_info")
-        keys = ("last_path", "ok", "n_chunks", "fma_dft", "fma_interp", "fma_direct", "grid_vals", "weight_bytes")
+        keys = ("last_path", "ok", "n_chunks", "fma_dft", "fma_interp", "fma_direct", "grid_vals", "weight_bytes",
+                "grid_mfma")
         d = dict(zip(keys, g.tolist()))
         d["last_path"] = int(d["last_path"])
         d["ok"] = bool(d["ok"])
+        d["grid_mfma"] = int(d["grid_mfma"])
         return d
 
     def batch_synth(self, seed, real0, n_real, to_host=True, coeffs=False):

@@ -60,7 +60,7 @@ struct Seg {
 
 // Gridded-synthesis tables of one signal (grid.hip): real-DFT table E, interpolation weights.
 struct GridSeg {
-  int32_t nf = 0, half = 0, lde = 0, rmax = 0;
+  int32_t nf = 0, half = 0, lde = 0, rmax = 0, ntab = 0;
   DevBuf ecos, esin, wd, js, g;
 };
 
@@ -148,6 +148,7 @@ struct fpta_ctx {
   int last_path = 0;     // synthesis path of the last batch (1 direct, 2 MFMA, 3 VALU, 4 gridded)
   int grid_w = 13;       // gridded path: kernel width in grid cells
   int grid_sigma100 = 200;  // gridded path: oversampling x 100
+  int grid_mfma = 3;     // gridded path on fp64 MFMA: bit 0 k_grid_dft_mfma, bit 1 k_grid_interp_mfma
   // profiling
   struct Pending {
     int which;
@@ -538,7 +539,7 @@ int grid_build(fpta_ctx* c, Layout& L) {
       }
       for (int32_t s = 0; s < n_seg; ++s) {
         int32_t rows = (int32_t)(hi[s] - lo[s]) + w;
-        rows += rows & 1;  // k_grid_interp consumes rows in pairs (the pad row has zero weights)
+        rows = (rows + 3) & ~3;  // k_grid_interp_mfma: 4 rows per MFMA; k_grid_interp: pairs (pad rows weigh 0)
         const int64_t m = ((lo[s] % nf[s]) + nf[s]) % nf[s];
         js[s].push_back(make_int2((int)m, rows));
         rmax[s] = std::max(rmax[s], rows);
@@ -567,11 +568,12 @@ int grid_build(fpta_ctx* c, Layout& L) {
     G.segs.push_back(gs);
     gs->nf = nf[s];
     gs->half = nf[s] / 2;
-    gs->lde = gs->half + 1 + kGridMI;
+    gs->lde = (gs->half + 32) / 32 * 32;  // row tiles of k_grid_dft_mfma (32) and k_grid_dft (kGridMI)
+    gs->ntab = (d.nm + 7) / 8 * 8;         // whole pairs of 4-mode MFMA k-steps (zero rows)
     gs->rmax = rmax[s];
     // q_k = (2 pi / nf) / phi_hat(k), phi_hat(k) = alpha int_{-1}^{1} phi(z) cos(k alpha z) dz, alpha = pi w / nf
     const double alpha = M_PI * w / nf[s];
-    std::vector<double> ec((size_t)d.nm * gs->lde, 0.0), es((size_t)d.nm * gs->lde, 0.0);
+    std::vector<double> ec((size_t)gs->ntab * gs->lde, 0.0), es((size_t)gs->ntab * gs->lde, 0.0);
     for (int32_t m = 0; m < d.nm; ++m) {
       const int64_t k = m + 1;
       double ph = 0.0;
@@ -639,11 +641,18 @@ int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad) {
       g.rmax = gs->rmax;
       g.nm = d.nm;
       g.col0 = d.col0;
+      g.ntab = gs->ntab;
     }
-    HIPCHK(c, launch_grid_dft(c->stream, gsegs, L.P, a.coef, a.K, R_pad), "k_grid_dft launch");
+    HIPCHK(c,
+           (c->grid_mfma & 1) ? launch_grid_dft_mfma(c->stream, gsegs, L.P, a.coef, a.K, R_pad)
+                              : launch_grid_dft(c->stream, gsegs, L.P, a.coef, a.K, R_pad),
+           "k_grid_dft launch");
   }
   KTimer kt(c, FPTA_K_SYNTH);
-  HIPCHK(c, launch_grid_interp(c->stream, a, G.chunks.as<int4>(), G.n_chunks, gsegs, R_pad), "k_grid_interp launch");
+  HIPCHK(c,
+         (c->grid_mfma & 2) ? launch_grid_interp_mfma(c->stream, a, G.chunks.as<int4>(), G.n_chunks, gsegs, R_pad)
+                            : launch_grid_interp(c->stream, a, G.chunks.as<int4>(), G.n_chunks, gsegs, R_pad),
+         "k_grid_interp launch");
   return FPTA_OK;
 }
 
@@ -951,6 +960,10 @@ int fpta_set_option(fpta_ctx* c, int32_t key, int64_t value) {
       return FPTA_OK;
     case FPTA_OPT_FUSE_WHITE:
       c->fuse_white = value ? 1 : 0;
+      return FPTA_OK;
+    case FPTA_OPT_GRID_MFMA:
+      if (value < 0 || value > 3) return fail(c, FPTA_EINVAL, "grid MFMA mask must be in [0, 3]");
+      c->grid_mfma = (int)value;
       return FPTA_OK;
     case FPTA_OPT_VALU_VARIANT:
       if (value < 0 || value >= kNumValuVariants) return fail(c, FPTA_EINVAL, "unknown VALU variant");
@@ -1438,6 +1451,7 @@ int fpta_batch_grid_info(fpta_ctx* c, double* out) {
   out[5] = ok ? G.fma_direct : 0.0;
   out[6] = ok ? G.grid_vals : 0.0;
   out[7] = ok ? G.weight_bytes : 0.0;
+  out[8] = c->grid_mfma;
   return FPTA_OK;
 }
 

@@ -79,7 +79,8 @@ struct GridSegDev {
   const int2* js;      // [n_chunks] {first grid row mod nf, rows}
   double* g;           // [P][nf][R_pad] grid values of the batch
   int32_t nf, half, lde, rmax, nm, col0;
-  int32_t nblk;        // k_grid_dft row blocks of this signal (set by launch_grid_dft)
+  int32_t ntab;        // mode rows of ecos/esin (nm zero-padded to a multiple of 8)
+  int32_t nblk;        // k_grid_dft row blocks of this signal (set by launch_grid_dft*)
 };
 constexpr int kGridMaxSeg = 16;  // signals per layout on the gridded path (passed by value as kernel arguments)
 struct GridSegs {
@@ -93,6 +94,11 @@ hipError_t launch_grid_weights(hipStream_t st, const SegDesc& sd, int64_t n_toa,
 hipError_t launch_grid_dft(hipStream_t st, GridSegs gsegs, int32_t P, const double* coef, int32_t K, int32_t R_pad);
 hipError_t launch_grid_interp(hipStream_t st, const SynthArgs& a, const int4* chunks, int32_t n_chunks,
                               const GridSegs& gsegs, int32_t R_pad);
+// the same two steps on v_mfma_f64_16x16x4_f64 (grid_mfma.hip)
+hipError_t launch_grid_dft_mfma(hipStream_t st, GridSegs gsegs, int32_t P, const double* coef, int32_t K,
+                                int32_t R_pad);
+hipError_t launch_grid_interp_mfma(hipStream_t st, const SynthArgs& a, const int4* chunks, int32_t n_chunks,
+                                   const GridSegs& gsegs, int32_t R_pad);
 
 hipError_t launch_seeds(hipStream_t st, const SegDesc* segs, int32_t n_seg, const int32_t* psr_of,
                         const double* toas, const double* nu, int64_t n_toa, double4* seeds);

@@ -305,7 +305,7 @@ hipError_t launch_grid_dft(hipStream_t st, GridSegs gsegs, int32_t P, const doub
   int64_t gx = 0;
   for (int s = 0; s < gsegs.n; ++s) {
     GridSegDev& g = gsegs.s[s];
-    if (g.lde < g.half + 1 + kGridMI || g.nm % 2) return hipErrorInvalidValue;
+    if (g.lde < (g.half + kGridMI) / kGridMI * kGridMI || g.nm % 2) return hipErrorInvalidValue;
     g.nblk = (g.half + 1 + kGridMI - 1) / kGridMI;
     gx += g.nblk;
   }

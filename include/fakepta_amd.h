@@ -198,7 +198,7 @@ int fpta_batch_info(fpta_ctx* ctx, int64_t* info);
  * out[0] synthesis path of the last batch (1 direct, 2 MFMA, 3 VALU, 4 gridded), out[1] plan usable,
  * out[2] interpolation chunks, out[3] k_grid_dft FMAs per realization, out[4] k_grid_interp FMAs per
  * realization, out[5] direct-contraction FMAs per realization, out[6] grid values per realization,
- * out[7] interpolation-weight bytes. out: host double[8]. */
+ * out[7] interpolation-weight bytes, out[8] the FPTA_OPT_GRID_MFMA mask in force. out: host double[9]. */
 int fpta_batch_grid_info(fpta_ctx* ctx, double* out);
 
 /* ------------------------------------------------------------------ tuning / profiling */
@@ -212,6 +212,8 @@ int fpta_batch_grid_info(fpta_ctx* ctx, double* out);
 #define FPTA_OPT_FUSE_WHITE 6     /* 1 (default): white/ECORR added in the synthesis epilogue; 0: separate pass */
 #define FPTA_OPT_GRID_WIDTH 7     /* gridded path: interpolation kernel width in grid cells (default 13) */
 #define FPTA_OPT_GRID_SIGMA 8     /* gridded path: grid oversampling x 100 (default 200) */
+#define FPTA_OPT_GRID_MFMA 9      /* gridded path kernels on fp64 MFMA: bit 0 the DFT, bit 1 the interpolation
+                                     (default 3; 0 = both on the fp64 VALU) */
 int fpta_set_option(fpta_ctx* ctx, int32_t key, int64_t value);
 /* Kernel ids for fpta_kernel_stats */
 #define FPTA_K_GEN 0

@@ -33,10 +33,13 @@ def ctx(capi):
     c.close()
 
 
-@pytest.fixture
-def gridded(ctx, capi):
+@pytest.fixture(params=[3, 0, 1, 2], ids=["mfma", "valu", "dft_mfma", "interp_mfma"])
+def gridded(ctx, capi, request):
+    """Gridded path with the DFT / interpolation on fp64 MFMA (mask bits 0 / 1) or the fp64 VALU."""
     ctx.set_option(capi.OPT_SYNTH_PATH, 4)
+    ctx.set_option(capi.OPT_GRID_MFMA, request.param)
     yield ctx
+    ctx.set_option(capi.OPT_GRID_MFMA, 3)
     ctx.set_option(capi.OPT_SYNTH_PATH, 0)
     ctx.set_option(capi.OPT_GRID_WIDTH, 13)
     ctx.set_option(capi.OPT_GRID_SIGMA, 200)
