@@ -23,7 +23,8 @@ sys.path.insert(0, ROOT)
 
 def kernel_times(ctx, capi, steps):
     return {n: ctx.kernel_stats(k)[1] / steps for n, k in
-            (("gen", capi.K_GEN), ("mix", capi.K_MIX), ("synth", capi.K_SYNTH), ("white", capi.K_WHITE))}
+            (("gen", capi.K_GEN), ("mix", capi.K_MIX), ("grid", capi.K_GRID), ("synth", capi.K_SYNTH),
+             ("white", capi.K_WHITE))}
 
 
 def timed(ctx, capi, fn, steps, warmup=2):
@@ -87,7 +88,7 @@ def c3(total):
     sums = ctx.batch_checksums()
     info = ctx.batch_info()
     del cn
-    return dict(config="c3", K=info["K"], realizations=total, batch=B, wall_s=dt,
+    return dict(config="c3", K=info["K"], realizations=total, batch=B, wall_s=dt, path=ctx.batch_grid_info()["last_path"],
                 samples_per_s=info["n_toa"] * total / dt, kernels_ms_per_batch={k: v for k, v in kt.items()},
                 last_checksum=float(sums[:, 1].sum()))
 
@@ -115,8 +116,8 @@ def c4():
     dt, kt = timed(ctx, _capi, lambda s: ctx.batch_synth(7, s * R, R, to_host=False), 5, warmup=1)
     flops = 2.0 * 2 * N * P * n_p * R
     return dict(config="c4", K=2 * N, n_toa=P * n_p, realizations=R, ms_per_step=dt / 5 * 1e3,
-                samples_per_s=P * n_p * R * 5 / dt, kernels_ms_per_step=kt,
-                synth_tflops=flops / (kt["synth"] / 1e3) / 1e12,
+                samples_per_s=P * n_p * R * 5 / dt, kernels_ms_per_step=kt, path=ctx.batch_grid_info()["last_path"],
+                synth_direct_equiv_tflops=flops / ((kt["synth"] + kt["grid"]) / 1e3) / 1e12,
                 mix_tflops=2.0 * P * P * 2 * N * R / (kt["mix"] / 1e3) / 1e12 if kt["mix"] else None)
 
 
@@ -149,8 +150,8 @@ def c5():
     info = ctx.batch_info()
     return dict(config="c5", K=info["K"], n_toa=info["n_toa"], realizations=R, ms_per_step=dt / 10 * 1e3,
                 samples_per_s=info["n_toa"] * R * 10 / dt, kernels_ms_per_step=kt,
-                synth_tflops=2.0 * info["K"] * info["n_toa"] * R / (kt["synth"] / 1e3) / 1e12,
-                n_ecorr_blocks=len(sim.blocks))
+                synth_direct_equiv_tflops=2.0 * info["K"] * info["n_toa"] * R / ((kt["synth"] + kt["grid"]) / 1e3) / 1e12,
+                path=ctx.batch_grid_info()["last_path"], n_ecorr_blocks=len(sim.blocks))
 
 
 def main():

@@ -28,4 +28,5 @@ def main(d, out, K, n_toa, n_real, kernel="k_synth_valu_seeded"):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4]), int(sys.argv[5]))
+    main(sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4]), int(sys.argv[5]),
+         *(sys.argv[6:7] or []))
