@@ -15,6 +15,7 @@ realizations (step * G + g) * R ...); RCCL is used for the barrier, the max-over
 a gather of per-realization checksums to rank 0.
 """
 import argparse
+import glob
 import json
 import os
 import sys
@@ -49,8 +50,9 @@ def parse():
     ap.add_argument("--grid-mfma", type=int, default=-1,
                     help="gridded path kernels on MFMA: bit 0 DFT, bit 1 interpolation (-1: library default)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL on ROCm) or gloo (CPU rehearsal)")
-    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
-                    help="PMC-derived HBM bytes per synth launch (written by profiles/collect_pmc.py)")
+    ap.add_argument("--traffic", default="",
+                    help="PMC-derived HBM bytes per synth launch (written by profiles/collect_pmc.py); "
+                         "default: the profiles/*traffic.json record matching the kernel and shape")
     return ap.parse_args()
 
 
@@ -221,15 +223,19 @@ def main():
     else:
         kernel, pipe = SYNTH_KERNELS[path]
     traffic = None
-    if os.path.exists(args.traffic):
+    candidates = ([args.traffic] if args.traffic else
+                  sorted(glob.glob(os.path.join(ROOT, "profiles", "*traffic.json"))))
+    for cand in candidates:
         try:
-            with open(args.traffic) as fh:
+            with open(cand) as fh:
                 tr = json.load(fh)
-            if (tr.get("K") == info["K"] and tr.get("n_real") == R and tr.get("n_toa") == info["n_toa"]
-                    and kernel.startswith(tr.get("kernel", "?"))):
-                traffic = tr.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
-            traffic = None
+            continue
+        # a PMC record only counts for the same kernel on the same shape (same launch)
+        if (tr.get("K") == info["K"] and tr.get("n_real") == R and tr.get("n_toa") == info["n_toa"]
+                and kernel.startswith(tr.get("kernel", "?"))):
+            traffic = tr.get("hbm_bytes_per_launch")
+            break
     out_bytes = 8.0 * info["n_toa"] * R
     if path == 4:
         # gridded path: the dominant kernel is the interpolation, an HBM-bound stream:
