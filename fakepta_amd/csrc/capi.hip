@@ -146,8 +146,10 @@ struct fpta_ctx {
   int valu_variant = 1;  // seeded (MT 2, NT 16): fastest on C2 (profiles/r01_sweep_*.txt)
   int fuse_white = 1;    // add white/ECORR in the seeded kernel's epilogue
   int last_path = 0;     // synthesis path of the last batch (1 direct, 2 MFMA, 3 VALU, 4 gridded)
-  int grid_w = 13;       // gridded path: kernel width in grid cells
-  int grid_sigma100 = 200;  // gridded path: oversampling x 100
+  // gridded path defaults (tools/sweep_grid.py --params, profiles/r01_sweep_wsig.txt): w = 14 at sigma = 1.5
+  // matches w = 13 at sigma = 2 to ~1e-12 and shrinks the grid (DFT) by a quarter
+  int grid_w = 14;       // gridded path: kernel width in grid cells
+  int grid_sigma100 = 150;  // gridded path: oversampling x 100
   int grid_mfma = 3;     // gridded path on fp64 MFMA: bit 0 k_grid_dft_mfma, bit 1 k_grid_interp_mfma
   // profiling
   struct Pending {

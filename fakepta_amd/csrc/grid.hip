@@ -13,7 +13,8 @@
 //
 // Kernel: exponential of semicircle phi(z) = exp(beta (sqrt(1 - z^2) - 1)), |z| <= 1, width w grid
 // cells, oversampling nf >= sigma (2N + 1); q_k = (2 pi / nf) / phi_hat(k) deconvolves it.
-// Aliasing error <= ~1e-12 relative at w = 13, sigma = 2 (tests/test_gpu_grid.py).
+// Aliasing error <= ~1e-12 relative at the default w = 14, sigma = 1.5 (and at w = 13, sigma = 2;
+// tests/test_gpu_grid.py, tools/sweep_grid.py).
 // Per sample the interpolation costs sum_s rows_s FMAs (rows ~ w + cells spanned by the chunk)
 // instead of sum_s 2 N_s for the direct contraction.
 #include <hip/hip_runtime.h>

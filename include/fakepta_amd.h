@@ -210,8 +210,8 @@ int fpta_batch_grid_info(fpta_ctx* ctx, double* out);
 #define FPTA_OPT_ANCHOR 4         /* recurrence re-anchor interval in K-steps of 2 modes (0 = once per signal, default) */
 #define FPTA_OPT_VALU_VARIANT 5   /* tile variant of the VALU fused kernel (0..5) */
 #define FPTA_OPT_FUSE_WHITE 6     /* 1 (default): white/ECORR added in the synthesis epilogue; 0: separate pass */
-#define FPTA_OPT_GRID_WIDTH 7     /* gridded path: interpolation kernel width in grid cells (default 13) */
-#define FPTA_OPT_GRID_SIGMA 8     /* gridded path: grid oversampling x 100 (default 200) */
+#define FPTA_OPT_GRID_WIDTH 7     /* gridded path: interpolation kernel width in grid cells (default 14) */
+#define FPTA_OPT_GRID_SIGMA 8     /* gridded path: grid oversampling x 100 (default 150) */
 #define FPTA_OPT_GRID_MFMA 9      /* gridded path kernels on fp64 MFMA: bit 0 the DFT, bit 1 the interpolation
                                      (default 3; 0 = both on the fp64 VALU) */
 int fpta_set_option(fpta_ctx* ctx, int32_t key, int64_t value);
