@@ -1,18 +1,22 @@
-"""Benchmark: BASELINE.json metric on configs[1] (C2), one MI355X per rank.
+"""Benchmark: the BASELINE.json metric, one MI355X per rank.
 
-Workload: 100 pulsars (Fibonacci sky) x 2000 TOAs, per-pulsar power-law
-red noise (30 modes) + DM noise (100 modes, nu^-2) + Hellings-Downs-correlated common GWB
-(30 modes, log10_A = -15, gamma = 13/3); K = 320 basis columns. One step = 1024 new
-realizations per GPU drawn on device (Philox -> ORF mix -> fused MFMA synthesis), written
-to a resident [1024 x 200000] fp64 residual block in HBM. Inputs are resident before the
-timed region; nothing is copied back inside it.
+Default workload = C2 (BASELINE configs[1]): 100 pulsars (Fibonacci sky) x 2000
+TOAs, per-pulsar power-law red noise (30 modes) + DM noise (100 modes, nu^-2) + Hellings-Downs-
+correlated common GWB (30 modes, log10_A = -15, gamma = 13/3); K = 320 basis columns. One step =
+1024 new realizations per GPU drawn on device (Philox -> ORF mix -> synthesis), written to a
+resident [1024 x 200000] fp64 residual block in HBM. Inputs are resident before the timed region;
+nothing is copied back inside it. Weak scaling: rank g of G owns realizations (step G + g) R ...
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+--config c3 (BASELINE configs[2]): the same 100-psr array with the HD GWB only (K = 60), a job of
+100,000 realizations sharded over the ranks (fakepta_amd.batch.simulate_sharded: rank g owns
+[g R/G, (g+1) R/G)), streamed in batches of 4096 per GPU, per-realization checksums gathered to
+rank 0. Strong scaling (the job is fixed); one step = the whole job.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3]
     (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
 
-Realizations shard across ranks with no data-path collective (weak scaling: rank g of G owns
-realizations (step * G + g) * R ...); RCCL is used for the barrier, the max-over-ranks time and
-a gather of per-realization checksums to rank 0.
+RCCL (torch.distributed backend "nccl") carries only the barrier, the max-over-ranks time and the
+checksum gather; the data path has no collective.
 """
 import argparse
 import glob
@@ -31,7 +35,7 @@ FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 matrix (= vector) peak, AMD datasheet (M
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 SYNTH_KERNELS = {3: ("k_synth_valu_seeded<2,16>", "fp64-valu"), 2: ("k_synth_mfma<4,2>", "fp64-mfma"),
                  1: ("k_synth_direct", "fp64-valu")}
-GRID_INTERP = {True: ("k_grid_interp_mfma<8>", "fp64-mfma"), False: ("k_grid_interp<16>", "fp64-valu")}
+GRID_INTERP = {True: ("k_grid_interp_mfma<8>", "fp64-mfma"), False: ("k_grid_interp_sparse<{w}>", "fp64-valu")}
 GRID_DFT = {True: "k_grid_dft_mfma<2,2>", False: "k_grid_dft<8>"}
 
 
@@ -40,110 +44,76 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--real", type=int, default=1024, help="realizations per GPU per step")
+    ap.add_argument("--config", default="c2", choices=("c2", "c3"))
+    ap.add_argument("--real", type=int, default=1024, help="c2: realizations per GPU per step")
+    ap.add_argument("--c3-real", type=int, default=100000, help="c3: realizations of the whole job")
+    ap.add_argument("--c3-batch", type=int, default=4096, help="c3: realizations per batch per GPU")
     ap.add_argument("--npsr", type=int, default=100)
     ap.add_argument("--ntoa", type=int, default=2000)
     ap.add_argument("--seed", type=int, default=1234)
-    ap.add_argument("--cpu-sample", type=int, default=8, help="realizations timed for the CPU baseline (0: skip)")
+    ap.add_argument("--cpu-sample", type=int, default=8,
+                    help="realizations timed for the loop-faithful CPU baseline (0: skip both CPU legs)")
     ap.add_argument("--path", type=int, default=0, help="synthesis path: 0 auto, 1 direct, 2 MFMA, 3 VALU, 4 gridded")
-    ap.add_argument("--anchor", type=int, default=0, help="recurrence re-anchor interval (0: library default)")
     ap.add_argument("--grid-mfma", type=int, default=-1,
                     help="gridded path kernels on MFMA: bit 0 DFT, bit 1 interpolation (-1: library default)")
+    ap.add_argument("--exact-launches", type=int, default=5,
+                    help="launches of the exact fused kernel (path 3) timed after the run for roofline_exact")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL on ROCm) or gloo (CPU rehearsal)")
     ap.add_argument("--traffic", default="",
-                    help="PMC-derived HBM bytes per synth launch (written by profiles/collect_pmc.py); "
-                         "default: the profiles/*traffic.json record matching the kernel and shape")
+                    help="PMC-derived HBM bytes per launch (profiles/*traffic.json, tools/collect_traffic.py); "
+                         "default: the record matching the kernel and shape")
     return ap.parse_args()
 
 
-# --------------------------------------------------------------------------- distributed helpers
-def dist_env():
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    return world, rank, local
+def refuse_debug_environment():
+    """A measurement must run the release library with no debug switch: refuse FPTA_* variables (the
+    release build reads none; a stale one signals a debugging session) and the debug build."""
+    bad = sorted(k for k in os.environ if k.startswith("FPTA_"))
+    if bad:
+        sys.exit(f"bench.py: refusing to measure with debug variables set: {', '.join(bad)}")
+    from fakepta_amd import _capi
+    if _capi.build_flags() & _capi.BUILD_DEBUG:
+        sys.exit(f"bench.py: refusing to measure the debug build ({_capi.LIB_PATH})")
 
 
-def shard_range(n_real, rank, world, step):
-    """Global realization indices of `rank` at `step` (weak scaling; invariant realization ids)."""
-    start = (step * world + rank) * n_real
-    return start, n_real
-
-
-class Comm:
-    """Barrier / max / gather over torch.distributed (RCCL on GPUs, gloo on CPU tests)."""
-
-    def __init__(self, world, rank, local, backend=None, device=None):
-        self.world, self.rank = world, rank
-        self.dist = None
-        if world > 1:
-            import torch
-            import torch.distributed as dist
-            if backend is None:
-                backend = "nccl"
-            if backend == "nccl":
-                torch.cuda.set_device(local)
-                self.device = torch.device("cuda", local)
-            else:
-                self.device = torch.device("cpu")
-            if not dist.is_initialized():
-                dist.init_process_group(backend=backend)
-            self.dist = dist
-            self.torch = torch
-
-    def barrier(self):
-        if self.dist:
-            self.dist.barrier()
-
-    def max(self, x):
-        if not self.dist:
-            return x
-        t = self.torch.tensor([float(x)], dtype=self.torch.float64, device=self.device)
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
-        return float(t.item())
-
-    def gather(self, arr):
-        """All ranks' arrays (same shape) stacked on every rank, in rank order."""
-        if not self.dist:
-            return arr[None]
-        t = self.torch.from_numpy(np.ascontiguousarray(arr)).to(self.device)
-        bufs = [self.torch.empty_like(t) for _ in range(self.world)]
-        self.dist.all_gather(bufs, t)
-        return np.stack([b.cpu().numpy() for b in bufs])
-
-    def close(self):
-        if self.dist and self.dist.is_initialized():
-            self.dist.destroy_process_group()
-
-
-# --------------------------------------------------------------------------- workload
-def build_c2(n_psr, n_toa):
-    """C2 array through the drop-in API (make_fake_array + add_common_correlated_noise, seed 0)."""
-    from fakepta_amd import correlated_noises as cn
-    from fakepta_amd import fake_pta as fp
+# --------------------------------------------------------------------------- workloads
+def build_array(n_psr, n_toa, config):
+    """C2 / C3 array through the drop-in API (make_fake_array + add_common_correlated_noise, seed 0)."""
+    from fakepta import correlated_noises as cn
+    from fakepta import fake_pta as fp
     np.random.seed(0)
+    model = {"RN": 30, "DM": 100, "Sv": None} if config == "c2" else {"RN": None, "DM": None, "Sv": None}
     psrs = fp.make_fake_array(npsrs=n_psr, Tobs=10, ntoas=n_toa, gaps=False, isotropic=True, toaerr=1e-7,
-                              backends="NUPPI.1400", custom_model={"RN": 30, "DM": 100, "Sv": None})
+                              backends="NUPPI.1400", custom_model=model)
     cn.add_common_correlated_noise(psrs, orf="hd", log10_A=-15, gamma=13 / 3, components=30)
     return psrs
 
 
-def cpu_baseline(sim, psrs, n_sample, seed):
-    """Oracle (numpy restatement, loop-faithful to fake_pta.py:385-387 / correlated_noises.py:153-160)
-    timed on this host, 1 thread, for `n_sample` realizations of the same workload."""
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline_loop(sim, psrs, n_sample, seed):
+    """Oracle loop-faithful restatement (the reference's per-mode elementwise structure,
+    fake_pta.py:385-387 / correlated_noises.py:153-160), 1 thread, n_sample realizations."""
     from oracle import fakepta_oracle as O
     P = len(psrs)
-    segs = sim.segments
     t0 = time.perf_counter()
     for r in range(n_sample):
         rng = np.random.default_rng(seed + r)
         res = [np.zeros(len(p.toas)) for p in psrs]
-        for s in segs:
+        for s in sim.segments:
             if s["kind"] == 0:
                 for p in range(P):
                     nm = s["f"].shape[1]
-                    amp = s["amp"][p]
-                    psd = amp ** 2 / O.delta_f(s["f"][p])
+                    psd = s["amp"][p] ** 2 / O.delta_f(s["f"][p])
                     coeffs = O.gp_coeffs_from_z(psd, rng.standard_normal(2 * nm))
                     O.gp_synth_loop(psrs[p].toas, psrs[p].freqs, s["f"][p], coeffs, s["idx"], residuals=res[p])
             else:
@@ -154,129 +124,236 @@ def cpu_baseline(sim, psrs, n_sample, seed):
                                              s["L"], s["idx"])
                 for p in range(P):
                     res[p] += out[p]
-    dt = time.perf_counter() - t0
-    n_samples = sim.n_toa * n_sample
-    return dict(value=n_samples / dt, unit="samples/s", cores=1, kind="port",
-                sample=f"{n_sample} realizations of the C2 array (100 psr x 2000 TOAs, RN30+DM100+HD30), "
-                       f"oracle loop-faithful restatement, numpy {np.__version__}, 1 thread, "
-                       f"{dt:.2f} s on {os.cpu_count()}-CPU host")
+    return time.perf_counter() - t0
 
 
-def main():
-    args = parse()
-    world, rank, local = dist_env()
-    from fakepta_amd import _capi
-    from fakepta_amd.batch import BatchSimulator
-
-    # one process per GPU; local ranks beyond the visible devices wrap (rehearsal of several ranks on
-    # one card with --dist-backend gloo; the driver's N-GPU runs have one rank per device)
-    ndev = max(1, _capi.device_count())
-    device = local % ndev
-    os.environ["FAKEPTA_AMD_DEVICE"] = str(device)  # the drop-in calls of build_c2 use the same card
-    comm = Comm(world, rank, device, backend=args.dist_backend)
-    ctx = _capi.Context(device)
-    psrs = build_c2(args.npsr, args.ntoa)
-    sim = BatchSimulator(psrs, white=False, ctx=ctx)
-    info = ctx.batch_info()
-    if args.path:
-        ctx.set_option(_capi.OPT_SYNTH_PATH, args.path)
-    if args.anchor:
-        ctx.set_option(_capi.OPT_ANCHOR, args.anchor)
-    if args.grid_mfma >= 0:
-        ctx.set_option(_capi.OPT_GRID_MFMA, args.grid_mfma)
-    R = args.real
-
-    for s in range(args.warmup):
-        real0, n = shard_range(R, rank, world, s)
-        ctx.batch_synth(args.seed, real0, n, to_host=False)
-    ctx.synchronize()
-    ctx.set_option(_capi.OPT_PROFILE, 1)
-    ctx.reset_stats()
-
-    comm.barrier()
-    ctx.synchronize()
+def cpu_baseline_vectorised(sim, psrs, n_real, seed):
+    """the vectorised F.A restatement on all the host threads BLAS is given
+    (OMP_NUM_THREADS): per pulsar the basis F [n_p x K_p] (built once per batch, as a CPU user would),
+    the draws, the ORF mix x = L z and one GEMM F @ A [K_p x n_real]."""
+    from oracle import fakepta_oracle as O
+    P = len(psrs)
+    rng = np.random.default_rng(seed)
     t0 = time.perf_counter()
-    for s in range(args.steps):
-        real0, n = shard_range(R, rank, world, args.warmup + s)
-        ctx.batch_synth(args.seed, real0, n, to_host=False)
-    ctx.synchronize()
-    comm.barrier()
-    dt_local = time.perf_counter() - t0
-    dt = comm.max(dt_local)
+    zc = {}
+    for i, s in enumerate(sim.segments):
+        if s["kind"] == 1:
+            nm = len(s["f"])
+            z = rng.standard_normal((P, 2 * nm * n_real))
+            zc[i] = (s["L"] @ z).reshape(P, 2 * nm, n_real)
+    for p in range(P):
+        out = np.zeros((len(psrs[p].toas), n_real))
+        for i, s in enumerate(sim.segments):
+            f = s["f"][p] if s["kind"] == 0 else s["f"]
+            amp = s["amp"][p] if s["kind"] == 0 else s["amp"]
+            F = O.fourier_basis(psrs[p].toas, psrs[p].freqs, f, s["idx"])
+            if s["kind"] == 0:
+                A = rng.standard_normal((2 * len(f), n_real))
+            else:
+                A = zc[i][p]
+            A *= np.repeat(amp, 2)[:, None]
+            out += F @ A
+    return time.perf_counter() - t0
 
-    ctx.set_option(_capi.OPT_PROFILE, 0)
-    kstats = {name: ctx.kernel_stats(k) for name, k in
-              (("gen", _capi.K_GEN), ("mix", _capi.K_MIX), ("grid", _capi.K_GRID), ("synth", _capi.K_SYNTH),
-               ("white", _capi.K_WHITE))}
-    sums = ctx.batch_checksums()  # last step's realizations
-    all_sums = comm.gather(sums)
-    n_samples_total = info["n_toa"] * R * args.steps * world
-    value = n_samples_total / dt
 
-    synth_n, synth_ms = kstats["synth"]
-    synth_avg_s = synth_ms / max(synth_n, 1) / 1e3
-    flops = 2.0 * info["K"] * info["n_toa"] * R
-    gi = ctx.batch_grid_info()
-    path = gi["last_path"]
-    if path == 4:
-        kernel, pipe = GRID_INTERP[bool(gi["grid_mfma"] & 2)]
-    else:
-        kernel, pipe = SYNTH_KERNELS[path]
-    traffic = None
-    candidates = ([args.traffic] if args.traffic else
-                  sorted(glob.glob(os.path.join(ROOT, "profiles", "*traffic.json"))))
+def cpu_baseline(sim, psrs, n_sample, seed):
+    n_toa = sim.n_toa
+    dt_loop = cpu_baseline_loop(sim, psrs, n_sample, seed)
+    threads = os.environ.get("OMP_NUM_THREADS", "")
+    n_vec = 64
+    dt_vec = cpu_baseline_vectorised(sim, psrs, n_vec, seed)
+    while dt_vec < 2.0 and n_vec < 4096:  # grow the sample to a few seconds of CPU work
+        n_vec *= 4
+        dt_vec = cpu_baseline_vectorised(sim, psrs, n_vec, seed)
+    cores = int(threads) if threads.isdigit() else os.cpu_count()
+    vec = dict(value=n_toa * n_vec / dt_vec, unit="samples/s", cores=cores, kind="port",
+               sample=f"{n_vec} realizations, vectorised F.A (numpy {np.__version__} BLAS GEMM per pulsar), "
+                      f"{dt_vec:.2f} s")
+    return dict(value=n_toa * n_sample / dt_loop, unit="samples/s", cores=1, kind="port",
+                sample=f"{n_sample} realizations of the bench array, oracle loop-faithful restatement "
+                       f"(per-mode elementwise numpy as fake_pta.py:385-387), 1 thread, {dt_loop:.2f} s",
+                cpu_model=cpu_model(), nproc=os.cpu_count(), omp_num_threads=threads or None,
+                vectorised_all_cores=vec)
+
+
+def pmc_traffic(kernel, info, R, path_arg):
+    """HBM bytes per launch from the matching profiles/*traffic.json PMC record (same kernel and shape)."""
+    candidates = ([path_arg] if path_arg else sorted(glob.glob(os.path.join(ROOT, "profiles", "*traffic.json"))))
     for cand in candidates:
         try:
             with open(cand) as fh:
                 tr = json.load(fh)
         except (OSError, ValueError):
             continue
-        # a PMC record only counts for the same kernel on the same shape (same launch)
         if (tr.get("K") == info["K"] and tr.get("n_real") == R and tr.get("n_toa") == info["n_toa"]
                 and kernel.startswith(tr.get("kernel", "?"))):
-            traffic = tr.get("hbm_bytes_per_launch")
-            break
-    out_bytes = 8.0 * info["n_toa"] * R
+            return tr.get("hbm_bytes_per_launch"), os.path.relpath(cand, ROOT)
+    return None, None
+
+
+def kernel_avg_s(ctx, which):
+    n, ms = ctx.kernel_stats(which)
+    return ms / max(n, 1) / 1e3
+
+
+def exact_roofline(ctx, capi, sim, seed, R, launches):
+    """The exact fused kernel (path 3, k_synth_valu_seeded) on the same batch, timed with HIP events on the
+    context stream after the main run: its FP64 rate against the MI355X FP64 peak (north-star target >= 50%)."""
+    info = ctx.batch_info()
+    old = ctx.get_option(capi.OPT_SYNTH_PATH)
+    ctx.set_option(capi.OPT_SYNTH_PATH, 3)
+    ctx.set_option(capi.OPT_PROFILE, 1)
+    try:
+        sim.synth(R, seed=seed, real0=0, to_host=False)  # warm (tile table)
+        ctx.synchronize()
+        ctx.reset_stats()
+        for i in range(launches):
+            sim.synth(R, seed=seed, real0=(i + 1) * R, to_host=False)
+        ctx.synchronize()
+        t = kernel_avg_s(ctx, capi.K_SYNTH)
+    finally:
+        ctx.set_option(capi.OPT_SYNTH_PATH, old)
+        ctx.set_option(capi.OPT_PROFILE, 0)
+    kernel = SYNTH_KERNELS[3][0]
+    flops = 2.0 * info["K"] * info["n_toa"] * R
+    achieved = flops / t / 1e12
+    return {"kernel": kernel, "pipe": "fp64-valu", "launches": launches, "avg_launch_ms": t * 1e3,
+            "flops_per_launch": flops, "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": achieved / FP64_PEAK_TFLOPS, "write_GBps": 8.0 * info["n_toa"] * R / t / 1e9}
+
+
+def main():
+    args = parse()
+    refuse_debug_environment()
+    from fakepta_amd import _capi
+    from fakepta_amd.batch import BatchSimulator, RealizationComm, shard_bounds, simulate_sharded
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one process per GPU; local ranks beyond the visible devices wrap (rehearsal of several ranks on one card
+    # with --dist-backend gloo; the driver's N-GPU runs have one rank per device)
+    ndev = max(1, _capi.device_count())
+    device = local % ndev
+    os.environ["FAKEPTA_AMD_DEVICE"] = str(device)  # the drop-in calls of build_array use the same card
+    comm = RealizationComm(backend=args.dist_backend, local_rank=device)
+    rank = comm.rank
+    ctx = _capi.Context(device)
+    psrs = build_array(args.npsr, args.ntoa, args.config)
+    sim = BatchSimulator(psrs, white=False, ctx=ctx)
+    info = ctx.batch_info()
+    if args.path:
+        ctx.set_option(_capi.OPT_SYNTH_PATH, args.path)
+    if args.grid_mfma >= 0:
+        ctx.set_option(_capi.OPT_GRID_MFMA, args.grid_mfma)
+
+    if args.config == "c2":
+        R = args.real
+        for s in range(args.warmup):
+            sim.synth(R, seed=args.seed, real0=(s * world + rank) * R, to_host=False)
+        ctx.synchronize()
+        ctx.set_option(_capi.OPT_PROFILE, 1)
+        ctx.reset_stats()
+        comm.barrier()
+        ctx.synchronize()
+        t0 = time.perf_counter()
+        for s in range(args.steps):
+            sim.synth(R, seed=args.seed, real0=((args.warmup + s) * world + rank) * R, to_host=False)
+        ctx.synchronize()
+        comm.barrier()
+        dt = comm.max(time.perf_counter() - t0)
+        n_samples_total = info["n_toa"] * R * args.steps * world
+        sums = comm.gather_to_root(sim.checksums())  # last step's realizations, rank order = realization order
+    else:
+        R = args.c3_batch
+        n_job = args.c3_real
+        for s in range(args.warmup):  # warm every batch shape of the job (tile tables, grid plan, buffers)
+            lo, hi = shard_bounds(n_job, rank, world)
+            for first in range(lo, hi, R):
+                sim.synth(min(R, hi - first), seed=args.seed, real0=first, to_host=False)
+        ctx.synchronize()
+        ctx.set_option(_capi.OPT_PROFILE, 1)
+        ctx.reset_stats()
+        comm.barrier()
+        ctx.synchronize()
+        t0 = time.perf_counter()
+        for s in range(args.steps):
+            sums = simulate_sharded(sim, n_job, seed=args.seed, real0=(args.warmup + s) * n_job, batch=R,
+                                    comm=comm)
+        ctx.synchronize()
+        comm.barrier()
+        dt = comm.max(time.perf_counter() - t0)
+        n_samples_total = info["n_toa"] * n_job * args.steps
+
+    ctx.set_option(_capi.OPT_PROFILE, 0)
+    kstats = {name: ctx.kernel_stats(k) for name, k in
+              (("gen", _capi.K_GEN), ("mix", _capi.K_MIX), ("grid", _capi.K_GRID), ("synth", _capi.K_SYNTH),
+               ("white", _capi.K_WHITE))}
+    value = n_samples_total / dt
+    synth_avg_s = kernel_avg_s(ctx, _capi.K_SYNTH)
+    gi = ctx.batch_grid_info()
+    path = gi["last_path"]
+    # algorithmic bytes of one synthesis launch (SURVEY.md §8(d)): 8 B per residual sample written; one launch
+    # writes n_toa x R samples (c3: the job's batches averaged, the short last batch included)
+    n_launch_real = R if args.config == "c2" else n_job / max(1, -(-shard_bounds(n_job, 0, world)[1] // R))
+    out_bytes = 8.0 * info["n_toa"] * n_launch_real
     if path == 4:
-        # gridded path: the dominant kernel is the interpolation, an HBM-bound stream:
-        # algorithmic bytes = residual block written once + grid values read once + interpolation weights
-        R_pad = -(-R // 128) * 128
-        alg_bytes = out_bytes + 8.0 * gi["grid_vals"] * R_pad + gi["weight_bytes"]
-        achieved = alg_bytes / synth_avg_s / 1e9
-        grid_n, grid_ms = kstats["grid"]
-        grid_avg_s = grid_ms / max(grid_n, 1) / 1e3
+        kernel, pipe = GRID_INTERP[bool(gi["grid_mfma"] & 2) or gi["width"] > 16]
+        kernel = kernel.format(w=gi["width"])
+        traffic, traffic_src = pmc_traffic(kernel, info, R, args.traffic)
+        achieved = out_bytes / synth_avg_s / 1e9
+        R_pad = -(-int(n_launch_real) // 128) * 128
+        impl_bytes = out_bytes + 8.0 * gi["grid_vals"] * R_pad + gi["weight_bytes"]
+        grid_avg_s = kernel_avg_s(ctx, _capi.K_GRID)
         dft_flops = 2.0 * gi["fma_dft"] * R_pad
         roofline = {"bound": "hbm", "pipe": pipe, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": kernel,
-                    "bytes_per_launch": alg_bytes, "avg_launch_ms": synth_avg_s * 1e3,
-                    "write_GBps": out_bytes / synth_avg_s / 1e9,
+                    "algorithmic_bytes_per_launch": out_bytes, "avg_launch_ms": synth_avg_s * 1e3,
+                    "traffic_over_algorithmic": (traffic / out_bytes) if traffic else None,
+                    "traffic_source": traffic_src,
+                    "implementation_bytes_per_launch": impl_bytes,
                     "interp_fp64_TFLOPs": 2.0 * gi["fma_interp"] * R_pad / synth_avg_s / 1e12,
+                    "grid": {"width": gi["width"], "sigma": gi["sigma"], "err_bound": gi["err_bound"]},
                     "dft": {"kernel": GRID_DFT[bool(gi["grid_mfma"] & 1)], "avg_launch_ms": grid_avg_s * 1e3,
                             "flops_per_launch": dft_flops, "TFLOPs": dft_flops / max(grid_avg_s, 1e-12) / 1e12,
-                            "frac_fp64_peak": dft_flops / max(grid_avg_s, 1e-12) / 1e12 / FP64_PEAK_TFLOPS},
-                    "direct_equivalent_TFLOPs": flops / (synth_avg_s + grid_avg_s) / 1e12}
+                            "frac_fp64_peak": dft_flops / max(grid_avg_s, 1e-12) / 1e12 / FP64_PEAK_TFLOPS}}
     else:
-        # exact paths: compute (FP64) bound, 2K FLOP per 8-byte sample = 80 FLOP/B at K = 320. The peak is
-        # the MI355X FP64 datasheet figure, equal for the vector and matrix pipes (DESIGN.md §5 Calibration)
+        # exact paths: FP64-bound, 2K FLOP per 8-byte sample (80 FLOP/B at K = 320)
+        kernel, pipe = SYNTH_KERNELS[path]
+        traffic, traffic_src = pmc_traffic(kernel, info, R, args.traffic)
+        flops = 2.0 * info["K"] * info["n_toa"] * n_launch_real
         achieved = flops / synth_avg_s / 1e12
         roofline = {"bound": "mfma", "pipe": pipe, "achieved": achieved, "peak": FP64_PEAK_TFLOPS,
                     "unit": "TFLOP/s", "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic, "kernel": kernel,
-                    "flops_per_launch": flops, "avg_launch_ms": synth_avg_s * 1e3,
+                    "traffic_source": traffic_src, "flops_per_launch": flops, "avg_launch_ms": synth_avg_s * 1e3,
                     "write_GBps": out_bytes / synth_avg_s / 1e9}
 
+    roofline_exact = None
+    if args.config == "c2" and args.exact_launches > 0:
+        roofline_exact = exact_roofline(ctx, _capi, sim, args.seed, R, args.exact_launches)
+
     if rank == 0:
+        if args.config == "c2":
+            workload = ("C2 (BASELINE configs[1]): %d psr x %d TOAs, RN30 + DM100(nu^-2) + HD GWB30, "
+                        "%d realizations/GPU/step, Philox seed %d" % (args.npsr, args.ntoa, R, args.seed))
+            scaling, per_key, per_val = "weak", "realizations_per_gpu", R
+        else:
+            workload = ("C3 (BASELINE configs[2]): %d psr x %d TOAs, HD GWB30 only, %d realizations per job "
+                        "sharded over %d GPU(s) in batches of %d, checksums gathered to rank 0, Philox seed %d"
+                        % (args.npsr, args.ntoa, n_job, world, R, args.seed))
+            scaling, per_key, per_val = "strong", "realizations_per_job", n_job
         line = {
             "metric": METRIC, "value": value, "unit": "samples/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
-            "config": {"workload": "C2 (BASELINE configs[1]): %d psr x %d TOAs, RN30 + DM100(nu^-2) + HD GWB30, "
-                                   "%d realizations/GPU/step, Philox seed %d" % (args.npsr, args.ntoa, R, args.seed),
-                       "n_psr": args.npsr, "n_toa_total": info["n_toa"], "K": info["K"], "realizations_per_gpu": R,
-                       "parallelism": "realization-sharded x%d" % world},
+            "scaling": scaling, "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+            "config": {"workload": workload, "n_psr": args.npsr, "n_toa_total": info["n_toa"], "K": info["K"],
+                       per_key: per_val, "parallelism": "realization-sharded x%d" % world},
             "synth_path": {1: "direct", 2: "mfma", 3: "valu-seeded", 4: "gridded"}.get(path, str(path)),
+            "path_reason": gi["path_reason"] or None,
             "roofline": roofline,
+            "roofline_exact": roofline_exact,
             "kernels_ms_per_step": {k: (v[1] / max(v[0], 1)) * (v[0] / max(args.steps, 1)) for k, v in kstats.items()},
-            "checksum": float(np.sum(all_sums[..., 1])),
+            "checksum": float(np.sum(sums[:, 1])),
+            "n_checksums": int(len(sums)),
         }
         if world == 1 and args.cpu_sample > 0:
             line["cpu_baseline"] = cpu_baseline(sim, psrs, args.cpu_sample, args.seed)

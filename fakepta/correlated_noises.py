@@ -11,7 +11,7 @@ import inspect
 
 import numpy as np
 
-from . import _capi
+from fakepta_amd import _capi
 from . import spectrum as _spectrum_module
 from .fake_pta import Pulsar  # noqa: F401  (reference module namespace)
 from .fake_pta import reconstruct_array

@@ -29,7 +29,7 @@ import pickle  # noqa: F401
 import numpy as np
 import scipy.constants as sc
 
-from . import _capi
+from fakepta_amd import _capi
 from . import spectrum as _spectrum_module
 
 # PSD registry (fakepta/fake_pta.py:14-22): name -> function, name -> parameter names (minus f)

@@ -1,8 +1,8 @@
-"""fakepta_amd — MI355X-native Fourier-basis GP residual synthesis for pulsar-timing arrays.
+"""fakepta_amd — the MI355X-native layer under the `fakepta` drop-in package.
 
-Drop-in modules for mfalxa/fakepta: `fake_pta` (Pulsar, make_fake_array, copy_array),
-`correlated_noises` (ORFs, add_common_correlated_noise), `spectrum` (PSD models), plus
-`batch` (BatchSimulator / simulate_batch: many realizations on device).
-The compute path is libfakepta_amd.so (HIP, gfx950) loaded by `_capi`; no CPU fallback.
+`_capi`: ctypes binding of libfakepta_amd.so (HIP kernels for gfx950 + C-ABI,
+include/fakepta_amd.h). `batch`: many realizations of an array's noise model on device
+(BatchSimulator, simulate_batch) and the realization-sharded multi-GPU driver
+(simulate_sharded). The reference-compatible modules live in the `fakepta` package.
 """
 __version__ = "0.1.0"

@@ -59,6 +59,20 @@ _SIGS = [
     ("fpta_reset_stats", _c_int, [_ctx_p]),
     ("fpta_synchronize", _c_int, [_ctx_p]),
     ("fpta_debug_philox", _c_int, [_ctx_p, _i64, _vp, _vp, _vp]),
+    ("fpta_debug_fill_out", _c_int, [_ctx_p, _dbl]),
+    ("fpta_get_option", _c_int, [_ctx_p, _i32, ctypes.POINTER(_i64)]),
+    ("fpta_build_flags", _c_int, []),
+    ("fpta_batch_path_reason", ctypes.c_char_p, [_ctx_p]),
+    ("fpta_multi_create", _c_int, [_i32, _vp, ctypes.POINTER(_vp)]),
+    ("fpta_multi_destroy", _c_int, [_vp]),
+    ("fpta_multi_last_error", ctypes.c_char_p, [_vp]),
+    ("fpta_multi_size", _c_int, [_vp]),
+    ("fpta_multi_context", _ctx_p, [_vp, _i32]),
+    ("fpta_multi_set_toas", _c_int, [_vp, _i32, _vp, _vp, _vp]),
+    ("fpta_multi_add_signal", _c_int, [_vp, _i32, _i32, _vp, _vp, _dbl, _dbl, _vp, _vp]),
+    ("fpta_multi_set_white", _c_int, [_vp, _vp, _i64, _vp, _vp, _vp]),
+    ("fpta_multi_set_option", _c_int, [_vp, _i32, _i64]),
+    ("fpta_multi_synth", _c_int, [_vp, _u64, _i64, _i64, _i32, _vp]),
 ]
 for _name, _res, _args in _SIGS:
     _fn = getattr(_lib, _name)
@@ -69,7 +83,15 @@ EXPORTED = [s[0] for s in _SIGS]
 
 OPT_SYNTH_PATH, OPT_MFMA_MIN_REAL, OPT_PROFILE, OPT_ANCHOR, OPT_VALU_VARIANT, OPT_FUSE_WHITE = 1, 2, 3, 4, 5, 6
 OPT_GRID_WIDTH, OPT_GRID_SIGMA, OPT_GRID_MFMA = 7, 8, 9
+OPTIONS = (OPT_SYNTH_PATH, OPT_MFMA_MIN_REAL, OPT_PROFILE, OPT_ANCHOR, OPT_VALU_VARIANT, OPT_FUSE_WHITE,
+           OPT_GRID_WIDTH, OPT_GRID_SIGMA, OPT_GRID_MFMA)
 K_GEN, K_MIX, K_SYNTH, K_WHITE, K_DENSE, K_GRID = 0, 1, 2, 3, 4, 5
+BUILD_DEBUG = 1
+
+
+def build_flags():
+    """FPTA_BUILD_DEBUG (1) when the loaded library is the debug build (make debug)."""
+    return int(_lib.fpta_build_flags())
 
 
 class FptaError(RuntimeError):
@@ -268,15 +290,18 @@ class Context:
         return dict(n_psr=int(info[0]), n_toa=int(info[1]), n_seg=int(info[2]), K=int(info[3]), max_np=int(info[4]))
 
     def batch_grid_info(self):
-        """Gridded-path plan figures and the path of the last batch (fpta_batch_grid_info)."""
-        g = np.zeros(9, dtype=np.float64)
+        """Gridded-path plan figures, the path of the last batch and why it was not the gridded path
+        (fpta_batch_grid_info, fpta_batch_path_reason)."""
+        g = np.zeros(12, dtype=np.float64)
         self._check(_lib.fpta_batch_grid_info(self._h, _ptr(g)), "fpta_batch_grid_info")
         keys = ("last_path", "ok", "n_chunks", "fma_dft", "fma_interp", "fma_direct", "grid_vals", "weight_bytes",
-                "grid_mfma")
+                "grid_mfma", "err_bound", "width", "sigma")
         d = dict(zip(keys, g.tolist()))
         d["last_path"] = int(d["last_path"])
         d["ok"] = bool(d["ok"])
         d["grid_mfma"] = int(d["grid_mfma"])
+        d["width"] = int(d["width"])
+        d["path_reason"] = _lib.fpta_batch_path_reason(self._h).decode()
         return d
 
     def batch_synth(self, seed, real0, n_real, to_host=True, coeffs=False):
@@ -330,6 +355,19 @@ class Context:
     def set_option(self, key, value):
         self._check(_lib.fpta_set_option(self._h, int(key), int(value)), "fpta_set_option")
 
+    def get_option(self, key):
+        v = _i64()
+        self._check(_lib.fpta_get_option(self._h, int(key), ctypes.byref(v)), "fpta_get_option")
+        return int(v.value)
+
+    def options(self):
+        """Snapshot of every option (restore with set_options)."""
+        return {k: self.get_option(k) for k in OPTIONS}
+
+    def set_options(self, opts):
+        for k, v in opts.items():
+            self.set_option(k, v)
+
     def kernel_stats(self, which):
         n, ms = _i64(), _dbl()
         self._check(_lib.fpta_kernel_stats(self._h, int(which), ctypes.byref(n), ctypes.byref(ms)),
@@ -342,11 +380,97 @@ class Context:
     def synchronize(self):
         self._check(_lib.fpta_synchronize(self._h), "fpta_synchronize")
 
+    def debug_fill_out(self, value):
+        """Fill the last device block with `value` (tests: the next batch must overwrite every sample)."""
+        self._check(_lib.fpta_debug_fill_out(self._h, float(value)), "fpta_debug_fill_out")
+
     def debug_philox(self, ctr, key):
         ctr = np.ascontiguousarray(ctr, dtype=np.uint32).reshape(-1, 4)
         key = np.ascontiguousarray(key, dtype=np.uint32)
         out = np.empty_like(ctr)
         self._check(_lib.fpta_debug_philox(self._h, len(ctr), _ptr(ctr), _ptr(key), _ptr(out)), "fpta_debug_philox")
+        return out
+
+
+class _Borrowed(Context):
+    """A device context owned by a MultiContext (not destroyed by this wrapper)."""
+
+    def __init__(self, handle, device):
+        self._h = handle
+        self.device = device
+
+    def close(self):
+        self._h = None
+
+
+class MultiContext:
+    """Several devices driven from one process (fpta_multi_*): the layout is replicated on each device,
+    realizations are sharded contiguously over them and only per-realization checksums come back."""
+
+    def __init__(self, devices):
+        devs = np.ascontiguousarray(devices, dtype=np.int32)
+        h = _vp()
+        rc = _lib.fpta_multi_create(len(devs), _ptr(devs), ctypes.byref(h))
+        if rc != 0:
+            raise FptaError(f"fpta_multi_create({list(devs)}) failed ({rc}): {_lib.fpta_last_error(None).decode()}")
+        self._h = h
+        self.devices = [int(d) for d in devs]
+
+    def _check(self, rc, what):
+        if rc < 0:
+            raise FptaError(f"{what} failed ({rc}): {_lib.fpta_multi_last_error(self._h).decode()}")
+        return rc
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _lib.fpta_multi_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __len__(self):
+        return int(_lib.fpta_multi_size(self._h))
+
+    def context(self, i):
+        return _Borrowed(_lib.fpta_multi_context(self._h, int(i)), self.devices[i])
+
+    def set_toas(self, offs, toas, nu):
+        offs = np.ascontiguousarray(offs, dtype=np.int64)
+        toas, nu = _f64(toas), _f64(nu)
+        self._check(_lib.fpta_multi_set_toas(self._h, len(offs) - 1, _ptr(offs), _ptr(toas), _ptr(nu)),
+                    "fpta_multi_set_toas")
+
+    def add_signal(self, kind, f, amp, idx=0.0, freqf=1400.0, L=None, mask=None):
+        f, amp = _f64(f), _f64(amp)
+        L = None if L is None else _f64(L)
+        m = None if mask is None else np.ascontiguousarray(mask, dtype=np.uint8)
+        return self._check(_lib.fpta_multi_add_signal(self._h, int(kind), f.shape[-1], _ptr(f), _ptr(amp),
+                                                      float(idx), float(freqf), _ptr(L), _ptr(m)),
+                           "fpta_multi_add_signal")
+
+    def set_white(self, sigma=None, blocks=None, ecorr_sigma=None):
+        s = None if sigma is None else _f64(sigma)
+        nb, bo, bi, es = 0, None, None, None
+        if blocks:
+            nb = len(blocks)
+            bo = np.concatenate([[0], np.cumsum([len(b) for b in blocks])]).astype(np.int64)
+            bi = np.concatenate([np.asarray(b, dtype=np.int64) for b in blocks]).astype(np.int64)
+            es = _f64(ecorr_sigma)
+        self._check(_lib.fpta_multi_set_white(self._h, _ptr(s), nb, _ptr(bo), _ptr(bi), _ptr(es)),
+                    "fpta_multi_set_white")
+
+    def set_option(self, key, value):
+        self._check(_lib.fpta_multi_set_option(self._h, int(key), int(value)), "fpta_multi_set_option")
+
+    def synth_checksums(self, seed, real0, n_real, batch=4096):
+        """Per-realization (sum, sum of squares) of realizations real0 .. real0 + n_real - 1: [n_real, 2]."""
+        out = np.empty((int(n_real), 2))
+        self._check(_lib.fpta_multi_synth(self._h, int(seed) & 0xFFFFFFFFFFFFFFFF, int(real0), int(n_real),
+                                          int(batch), _ptr(out)), "fpta_multi_synth")
         return out
 
 

@@ -15,7 +15,7 @@ the oracle (oracle/fakepta_oracle.py: batch_synth) restates the exact semantics.
 import numpy as np
 
 from . import _capi
-from .correlated_noises import bin_curve, orf_factor, orf_matrix
+from fakepta.correlated_noises import orf_factor, orf_matrix
 
 GP_NAMES = ("red_noise", "dm_gp", "chrom_gp")
 
@@ -143,11 +143,13 @@ class BatchSimulator:
         _, _, R = self.ctx.batch_device_out()
         return self.ctx.batch_correlations(2 if normalized else 1) / R
 
-    def hd_curve(self, bins=10, estimator="ratio"):
+    def hd_curve(self, bins=10, estimator="ratio", return_counts=False):
         """(mean, std, bin centres) of the pairwise correlations against angular separation
         (correlated_noises.py:21-47) for the last block. estimator "ratio": mean cross-power over
         sqrt(mean auto-powers) (consistent); "per_realization": mean of per-realization normalized
-        correlations (biased toward 0 by O(1/n_eff) for red processes)."""
+        correlations (biased toward 0 by O(1/n_eff) for red processes). A bin with no pulsar pair is NaN,
+        as the reference's bin_curve gives, but without NumPy's empty-slice warnings; return_counts=True
+        appends the number of pairs per bin so callers can mask the empty ones."""
         if estimator == "ratio":
             C = self.correlations(normalized=False)
             d = np.sqrt(np.diag(C))
@@ -157,7 +159,16 @@ class BatchSimulator:
         pos = np.array([p.pos for p in self.psrs])
         iu = np.triu_indices(len(self.psrs), 1)
         angles = np.arccos(np.clip(pos @ pos.T, -1.0, 1.0))[iu]
-        return bin_curve(C[iu], angles, bins)
+        corrs = C[iu]
+        edges = np.linspace(0., np.pi, bins + 1)
+        centres = edges[:-1] + 0.5 * (edges[1] - edges[0])
+        mean, std, counts = np.full(bins, np.nan), np.full(bins, np.nan), np.zeros(bins, dtype=np.int64)
+        for b, (lo, hi) in enumerate(zip(edges[:-1], edges[1:])):
+            sel = corrs[(angles > lo) & (angles < hi)]  # open bins, as correlated_noises.py:36-47
+            counts[b] = len(sel)
+            if len(sel):
+                mean[b], std[b] = np.mean(sel), np.std(sel)
+        return (mean, std, centres, counts) if return_counts else (mean, std, centres)
 
     def checksums(self):
         """Per-realization (sum, sum of squares) of the last block, computed on device."""
@@ -172,3 +183,101 @@ def simulate_batch(psrs, n_real, seed=0, real0=0, signals=None, white=True, ecor
     """One-call convenience: [n_real, n_toa_total] residual realizations of the array's noise model."""
     return BatchSimulator(psrs, signals=signals, white=white, ecorr=ecorr, device=device).synth(
         n_real, seed=seed, real0=real0)
+
+
+# ----------------------------------------------------------------------------- multi-GPU (one process per GPU)
+def shard_bounds(n_real, rank, world):
+    """Realizations [start, end) of rank `rank` of `world` for a job of n_real (rank g owns
+    [g R / G, (g + 1) R / G)); contiguous, disjoint, covering, sizes differing by at most one."""
+    return rank * n_real // world, (rank + 1) * n_real // world
+
+
+class RealizationComm:
+    """torch.distributed plumbing of a realization-sharded job: one process per GPU launched by torchrun
+    (WORLD_SIZE / RANK / LOCAL_RANK from the environment), backend "nccl" (= RCCL over xGMI on ROCm) for
+    GPU ranks or "gloo" on CPU. The data path has no collective: only the timing barrier, a max-reduce of the
+    elapsed time and the gather of per-realization checksums to rank 0 go through it."""
+
+    def __init__(self, backend="nccl", world=None, rank=None, local_rank=None):
+        import os
+        self.world = int(os.environ.get("WORLD_SIZE", "1")) if world is None else int(world)
+        self.rank = int(os.environ.get("RANK", "0")) if rank is None else int(rank)
+        self.local_rank = int(os.environ.get("LOCAL_RANK", "0")) if local_rank is None else int(local_rank)
+        self.backend = backend
+        self.dist = None
+        if self.world > 1:
+            import torch
+            import torch.distributed as dist
+            self.torch = torch
+            if backend == "nccl":
+                ndev = torch.cuda.device_count()
+                torch.cuda.set_device(self.local_rank % max(ndev, 1))
+                self.device = torch.device("cuda", torch.cuda.current_device())
+            else:
+                self.device = torch.device("cpu")
+            if not dist.is_initialized():
+                dist.init_process_group(backend=backend)
+            self.dist = dist
+
+    def barrier(self):
+        if self.dist:
+            self.dist.barrier()
+
+    def max(self, x):
+        """max over ranks of a float (the job time is the slowest rank's)."""
+        if not self.dist:
+            return float(x)
+        t = self.torch.tensor([float(x)], dtype=self.torch.float64, device=self.device)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def gather_to_root(self, arr, rows_per_rank=None):
+        """Rank 0 receives every rank's `arr` ([n_g, ...] float64; n_g may differ by rank) concatenated in
+        rank order; other ranks get None. rows_per_rank: list of n_g (known to every rank); arrays are padded
+        to the largest n_g for the collective and trimmed on rank 0."""
+        arr = np.ascontiguousarray(arr, dtype=np.float64)
+        if not self.dist:
+            return arr.copy()
+        if rows_per_rank is None:
+            rows_per_rank = [arr.shape[0]] * self.world
+        n_max = max(rows_per_rank)
+        pad = np.zeros((n_max,) + arr.shape[1:])
+        pad[:arr.shape[0]] = arr
+        t = self.torch.from_numpy(pad).to(self.device)
+        bufs = [self.torch.empty_like(t) for _ in range(self.world)] if self.rank == 0 else None
+        self.dist.gather(t, gather_list=bufs, dst=0)
+        if self.rank != 0:
+            return None
+        return np.concatenate([b.cpu().numpy()[:n] for b, n in zip(bufs, rows_per_rank)])
+
+    def close(self):
+        if self.dist and self.dist.is_initialized():
+            self.dist.destroy_process_group()
+        self.dist = None
+
+
+def simulate_sharded(sim, n_real, seed=0, real0=0, batch=4096, comm=None, on_batch=None):
+    """Realizations real0 .. real0 + n_real - 1 of `sim`'s noise model over every rank of `comm`.
+
+    Rank g of G synthesizes its shard [real0 + g n / G, real0 + (g + 1) n / G) (shard_bounds) in batches of
+    <= `batch` realizations on its own GPU, keeps each batch resident on the device (on_batch(sim, first, n)
+    may consume it there: correlations, downloads) and computes per-realization checksums on the device.
+    Rank 0 receives all checksums, in global realization order: returns [n_real, 2] (sum, sum of squares)
+    on rank 0 and None on the other ranks. TOAs, tables and the ORF factor are replicated (each rank builds
+    its own BatchSimulator); realization r is bit-identical whatever G and `batch` are (Philox counters carry
+    the global index), which tests/test_dist_gloo.py and tests/test_gpu_c3.py check.
+
+    sim: BatchSimulator (or any object with synth(n, seed=, real0=, to_host=False) and checksums()).
+    comm: RealizationComm (default: a single-rank job)."""
+    comm = comm if comm is not None else RealizationComm(world=1, rank=0, local_rank=0)
+    G = comm.world
+    lo, hi = shard_bounds(n_real, comm.rank, G)
+    sums = np.empty((hi - lo, 2))
+    for first in range(lo, hi, batch):
+        n = min(batch, hi - first)
+        sim.synth(n, seed=seed, real0=real0 + first, to_host=False)
+        if on_batch is not None:
+            on_batch(sim, real0 + first, n)
+        sums[first - lo:first - lo + n] = sim.checksums()
+    sizes = [shard_bounds(n_real, g, G)[1] - shard_bounds(n_real, g, G)[0] for g in range(G)]
+    return comm.gather_to_root(sums, sizes)

@@ -62,6 +62,8 @@ struct Seg {
 struct GridSeg {
   int32_t nf = 0, half = 0, lde = 0, rmax = 0, ntab = 0;
   DevBuf ecos, esin, wd, js, g;
+  DevBuf rec, base;  // k_grid_interp_sparse: window-slot weight records [n_toa][kSparseRec], chunk base rows
+  int32_t ws = 0;    // k_grid_interp_sparse window rows (w + largest first-row offset)
 };
 
 // Gridded-synthesis plan of a layout (built once per layout, reused by every batch).
@@ -73,6 +75,8 @@ struct GridPlan {
   double sigma = 0.0;        // oversampling
   int32_t n_chunks = 0;
   DevBuf chunks;             // int4 {pulsar, first TOA (pulsar-local), count, 0}
+  int32_t n_work = 0;
+  DevBuf work;               // k_grid_interp_sparse work items: int4 {first chunk, chunks, pulsar, 0}
   std::vector<GridSeg*> segs;
   double fma_grid = 0.0;     // FMAs per realization: DFT + interpolation
   double fma_dft = 0.0;      // FMAs per realization in k_grid_dft
@@ -80,6 +84,7 @@ struct GridPlan {
   double grid_vals = 0.0;    // grid values per realization (sum over signals of P nf)
   double weight_bytes = 0.0; // interpolation weight tables
   double fma_direct = 0.0;   // FMAs per realization of the direct contraction
+  double err_bound = 1.0;    // a-priori relative aliasing bound of the ES kernel, exp(-pi w sqrt(1 - 1/sigma))
   int64_t g_rpad = 0;        // R_pad the grid buffers are sized for
   ~GridPlan() { clear(); }
   void clear() {
@@ -87,7 +92,12 @@ struct GridPlan {
     segs.clear();
     built = ok = false;
     n_chunks = 0;
+    n_work = 0;
     g_rpad = 0;
+    // the plan figures accumulate over signals in grid_build: a rebuilt plan must start from zero
+    fma_grid = fma_dft = fma_interp = grid_vals = weight_bytes = fma_direct = 0.0;
+    err_bound = 1.0;
+    why.clear();
   }
 };
 
@@ -106,10 +116,11 @@ struct Layout {
   // recurrence seeds [n_seg][n_toa] (double4), valid when every segment is harmonic
   DevBuf seeds;
   bool all_harmonic = false;
-  // MFMA tile table cache
+  // tile table cache of the tiled synthesis kernels: valid for (tiles_toa, tiles_real, tiles_n_real)
   DevBuf tiles;
   int32_t n_tiles = 0;
-  int64_t tiles_R = -1;
+  int32_t tiles_toa = 0, tiles_real = 0;
+  int64_t tiles_n_real = -1;
   GridPlan grid;
   ~Layout() { clear_signals(); }
   void clear_signals() {
@@ -117,7 +128,7 @@ struct Layout {
     segs.clear();
     K = 0;
     dirty = true;
-    tiles_R = -1;
+    tiles_n_real = -1;
     grid.clear();
   }
 };
@@ -146,11 +157,15 @@ struct fpta_ctx {
   int valu_variant = 1;  // seeded (MT 2, NT 16): fastest on C2 (profiles/r01_sweep_*.txt)
   int fuse_white = 1;    // add white/ECORR in the seeded kernel's epilogue
   int last_path = 0;     // synthesis path of the last batch (1 direct, 2 MFMA, 3 VALU, 4 gridded)
-  // gridded path defaults (tools/sweep_grid.py --params, profiles/r01_sweep_wsig.txt): w = 14 at sigma = 1.5
-  // matches w = 13 at sigma = 2 to ~1e-12 and shrinks the grid (DFT) by a quarter
-  int grid_w = 14;       // gridded path: kernel width in grid cells
+  std::string path_reason;  // why the last batch did not take the gridded path (empty if it did)
+  // gridded path defaults: w = 16 at sigma = 1.5. Flat-spectrum worst case at real-MJD epochs 1.4e-12 (100 modes)
+  // and 3.6e-12 (257 modes) relative (the numpy model of oracle.grid_synth and the GPU agree); the earlier
+  // w = 14 reached 3.2e-11 there (profiles/r02_gputest1.log). sigma = 1.5 keeps the grid (DFT) a quarter
+  // smaller than sigma = 2 (tools/sweep_grid.py --params, profiles/r01_sweep_wsig.txt)
+  int grid_w = 16;       // gridded path: kernel width in grid cells
   int grid_sigma100 = 150;  // gridded path: oversampling x 100
-  int grid_mfma = 3;     // gridded path on fp64 MFMA: bit 0 k_grid_dft_mfma, bit 1 k_grid_interp_mfma
+  int grid_mfma = 1;     // gridded path: bit 0 k_grid_dft_mfma (else k_grid_dft), bit 1 k_grid_interp_mfma (else
+                         // k_grid_interp_sparse, widths 12..16)
   // profiling
   struct Pending {
     int which;
@@ -178,15 +193,14 @@ int hip_fail(fpta_ctx* c, hipError_t e, const char* what) {
   return fail(c, e == hipErrorOutOfMemory ? FPTA_ENOMEM : FPTA_EDEVICE, m);
 }
 
-// FPTA_DEBUG_SYNC=1: synchronize after every launch so a device fault is reported by the launch
-// that caused it (debugging aid; off by default).
-bool debug_sync() {
-  static const bool on = [] {
-    const char* e = std::getenv("FPTA_DEBUG_SYNC");
-    return e && e[0] == '1';
-  }();
-  return on;
-}
+// Debug build (make debug, -DFPTA_DEBUG): synchronize after every launch so a device fault is
+// reported by the launch that caused it, and the kernels' FPTA_DCHECK bounds checks are compiled in.
+// Release builds read no environment variable and never add work or synchronisation.
+#ifdef FPTA_DEBUG
+constexpr bool debug_sync() { return true; }
+#else
+constexpr bool debug_sync() { return false; }
+#endif
 
 #define HIPCHK(ctx, expr, what)                                                           \
   do {                                                                                    \
@@ -404,9 +418,13 @@ int run_coefficients(fpta_ctx* c, Layout& L, uint64_t seed, int64_t real0, int32
   return FPTA_OK;
 }
 
+// Tile table of (pulsar, first TOA, first realization) for a kernel whose workgroup covers tile_toa TOAs x
+// tile_real realizations. The cache is keyed on the whole geometry: a table built for one kernel must never
+// drive another (with a key of n_real alone, the tile table of k_synth_mfma drove
+// k_synth_valu<1,32>, whose 128-realization workgroups then read coefficients past the padded block).
 int build_tiles(fpta_ctx* c, Layout& L, int32_t R, int32_t tile_toa, int32_t tile_real) {
-  const int64_t key = ((int64_t)tile_toa << 40) ^ ((int64_t)tile_real << 32) ^ (int64_t)R;
-  if (L.tiles_R == key) return FPTA_OK;
+  if (L.tiles_n_real == R && L.tiles_toa == tile_toa && L.tiles_real == tile_real) return FPTA_OK;
+  L.tiles_n_real = -1;
   std::vector<int4> t;
   for (int32_t p = 0; p < L.P; ++p) {
     const int64_t np_ = L.h_offs[p + 1] - L.h_offs[p];
@@ -426,7 +444,18 @@ int build_tiles(fpta_ctx* c, Layout& L, int32_t R, int32_t tile_toa, int32_t til
   if (rc) return rc;
   HIPCHK(c, hipStreamSynchronize(c->stream), "tiles sync");
   L.n_tiles = (int32_t)o.size();
-  L.tiles_R = key;
+  L.tiles_toa = tile_toa;
+  L.tiles_real = tile_real;
+  L.tiles_n_real = R;
+  return FPTA_OK;
+}
+
+// The tile table in the cache was built for exactly this kernel geometry (checked before every tiled launch).
+int check_tiles(fpta_ctx* c, const Layout& L, int32_t R, int32_t tile_toa, int32_t tile_real, SynthArgs& a) {
+  if (L.tiles_n_real != R || L.tiles_toa != tile_toa || L.tiles_real != tile_real)
+    return fail(c, FPTA_ESTATE, "synth: tile table does not match the kernel's tile geometry");
+  a.tile_toa = tile_toa;
+  a.tile_real = tile_real;
   return FPTA_OK;
 }
 
@@ -461,6 +490,11 @@ void gauss_legendre(int n, std::vector<double>& x, std::vector<double>& wt) {
 // most kGridRowCap cells, and the dense banded weights (device). Not usable -> ok = false + why.
 constexpr int kGridRowCap = 48;
 constexpr double kGridAutoRatio = 0.5;  // auto path: gridded when it needs < half the direct FMAs
+// auto path: gridded only when the a-priori bound exp(-pi w sqrt(1 - 1/sigma)) of the width/oversampling pair is
+// within this. The measured flat-spectrum worst case is ~3-4x the bound (w = 16, sigma = 1.5: bound 2.5e-13,
+// measured <= 3.6e-12; w = 15: 1.5e-12 / 6e-12; w = 14: 9.4e-12 / 3.2e-11, refused). A forced path 4 runs any
+// accepted pair: the caller opted in, and fpta_batch_grid_info reports the bound.
+constexpr double kGridAutoMaxErr = 2e-12;
 int grid_build(fpta_ctx* c, Layout& L) {
   GridPlan& G = L.grid;
   if (G.built && G.w == c->grid_w && G.sigma == c->grid_sigma100 / 100.0) return FPTA_OK;
@@ -468,6 +502,7 @@ int grid_build(fpta_ctx* c, Layout& L) {
   G.built = true;
   G.w = c->grid_w;
   G.sigma = c->grid_sigma100 / 100.0;
+  G.err_bound = std::exp(-M_PI * G.w * std::sqrt(1.0 - 1.0 / G.sigma));
   const int32_t n_seg = (int32_t)L.segs.size();
   if (n_seg == 0 || n_seg > kGridMaxSeg) {
     G.why = "gridded path: needs 1.." + std::to_string(kGridMaxSeg) + " signals";
@@ -520,12 +555,14 @@ int grid_build(fpta_ctx* c, Layout& L) {
       for (int32_t s = 0; s < n_seg; ++s) lo[s] = hi[s] = J[s][t];
       ++t;
       // chunks end on multiples of kGridTT in the global TOA index: every full chunk then writes whole
-      // 128-byte lines of each realization row
+      // 128-byte lines of each realization row. Every signal's first rows span at most kSparseD cells over
+      // the chunk (the register window of k_grid_interp_sparse; the MFMA band is then <= w + kSparseD rows)
       const int64_t t_lim = std::min(t_end, (t0 / kGridTT + 1) * kGridTT);
       while (t < t_lim) {
         bool fits = true;
         for (int32_t s = 0; s < n_seg && fits; ++s)
-          fits = std::max(hi[s], J[s][t]) - std::min(lo[s], J[s][t]) + w + 1 <= kGridRowCap;
+          fits = std::max(hi[s], J[s][t]) - std::min(lo[s], J[s][t]) <= kSparseD &&
+                 std::max(hi[s], J[s][t]) - std::min(lo[s], J[s][t]) + w + 1 <= kGridRowCap;
         if (!fits) break;
         for (int32_t s = 0; s < n_seg; ++s) {
           lo[s] = std::min(lo[s], J[s][t]);
@@ -554,8 +591,19 @@ int grid_build(fpta_ctx* c, Layout& L) {
     return FPTA_OK;
   }
   G.n_chunks = (int32_t)chunks.size();
+  // sparse-kernel work items: <= kSparseChunks consecutive chunks of one pulsar
+  std::vector<int4> work;
+  for (int32_t ci = 0; ci < G.n_chunks;) {
+    const int32_t p = chunks[ci].x;
+    int32_t n = 1;
+    while (n < kSparseChunks && ci + n < G.n_chunks && chunks[ci + n].x == p) ++n;
+    work.push_back(make_int4(ci, n, p, 0));
+    ci += n;
+  }
+  G.n_work = (int32_t)work.size();
   int rc;
   if ((rc = upload(c, G.chunks, chunks.data(), sizeof(int4) * chunks.size(), "grid chunks"))) return rc;
+  if ((rc = upload(c, G.work, work.data(), sizeof(int4) * work.size(), "grid work items"))) return rc;
   DevBuf d_chunk_of, d_tt_of, d_row, d_d;
   if ((rc = upload(c, d_chunk_of, chunk_of.data(), sizeof(int32_t) * N, "grid chunk_of")) ||
       (rc = upload(c, d_tt_of, tt_of.data(), sizeof(int32_t) * N, "grid tt_of")))
@@ -596,6 +644,28 @@ int grid_build(fpta_ctx* c, Layout& L) {
     if ((rc = upload(c, d_row, row.data(), sizeof(int32_t) * N, "grid rows")) ||
         (rc = upload(c, d_d, D[s].data(), sizeof(double) * N, "grid offsets")))
       return rc;
+    // k_grid_interp_sparse tables: per chunk the base row, per TOA the record of window slots; the signal's
+    // window size w + (largest first-row offset of any TOA in its chunk)
+    {
+      std::vector<int32_t> base(G.n_chunks);
+      int32_t dmax = 0;
+      for (int32_t ci = 0; ci < G.n_chunks; ++ci) base[ci] = js[s][ci].x;
+      for (int64_t t = 0; t < N; ++t) {
+        if (row[t] < 0 || row[t] > kSparseD) return fail(c, FPTA_EINVAL, "grid plan: chunk row offset out of range");
+        dmax = std::max(dmax, row[t]);
+      }
+      gs->ws = w + dmax;
+      if ((rc = upload(c, gs->base, base.data(), sizeof(int32_t) * base.size(), "grid sparse base rows"))) return rc;
+      // one step of padding: k_grid_interp_sparse loads a whole step's records unconditionally
+      const size_t rec_bytes = sizeof(double) * kSparseRec * ((size_t)N + kGridTT);
+      HIPCHK(c, gs->rec.ensure(rec_bytes), "grid records alloc");
+      HIPCHK(c, hipMemsetAsync(gs->rec.p, 0, rec_bytes, c->stream), "grid records memset");
+      HIPCHK(c,
+             launch_grid_records(c->stream, d, N, L.nu.as<double>(), d_d.as<double>(), d_row.as<int32_t>(), w, beta,
+                                 gs->rec.as<double>()),
+             "k_grid_records launch");
+      HIPCHK(c, hipStreamSynchronize(c->stream), "grid records sync");  // base host vector
+    }
     const size_t wbytes = sizeof(double) * ((size_t)G.n_chunks * gs->rmax + 1) * kGridTT;
     HIPCHK(c, gs->wd.ensure(wbytes), "grid weights alloc");
     HIPCHK(c, hipMemsetAsync(gs->wd.p, 0, wbytes, c->stream), "grid weights memset");
@@ -651,10 +721,25 @@ int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad) {
            "k_grid_dft launch");
   }
   KTimer kt(c, FPTA_K_SYNTH);
-  HIPCHK(c,
-         (c->grid_mfma & 2) ? launch_grid_interp_mfma(c->stream, a, G.chunks.as<int4>(), G.n_chunks, gsegs, R_pad)
-                            : launch_grid_interp(c->stream, a, G.chunks.as<int4>(), G.n_chunks, gsegs, R_pad),
-         "k_grid_interp launch");
+  // k_grid_interp_sparse writes the block (batch synthesis); accumulation into an existing block and widths
+  // beyond its window take the MFMA interpolation
+  if ((c->grid_mfma & 2) || !sparse_width_supported(G.w) || a.accumulate) {
+    HIPCHK(c, launch_grid_interp_mfma(c->stream, a, G.chunks.as<int4>(), G.n_chunks, gsegs, R_pad),
+           "k_grid_interp_mfma launch");
+  } else {
+    SparseSegs ss{};
+    ss.n = gsegs.n;
+    for (size_t s = 0; s < G.segs.size(); ++s) {
+      GridSeg* gs = G.segs[s];
+      ss.s[s].g = gs->g.as<double>();
+      ss.s[s].rec = gs->rec.as<double>();
+      ss.s[s].base = gs->base.as<int32_t>();
+      ss.s[s].nf = gs->nf;
+      ss.s[s].ws = gs->ws;
+    }
+    HIPCHK(c, launch_grid_interp_sparse(c->stream, a, G.chunks.as<int4>(), G.work.as<int4>(), G.n_work, ss, R_pad),
+           "k_grid_interp_sparse launch");
+  }
   return FPTA_OK;
 }
 
@@ -691,25 +776,43 @@ int run_synth(fpta_ctx* c, Layout& L, int32_t R, int32_t R_pad, double* out, int
   a.n_real = R;
   a.accumulate = accumulate;
   a.anchor = c->anchor;
+  a.coef_len = (int64_t)L.P * std::max(L.K, 1) * R_pad;
   // path: 1 direct, 2 MFMA, 3 VALU, 4 gridded; auto (0) = gridded when its plan needs fewer than
-  // kGridAutoRatio of the direct FMAs, else VALU, for R >= mfma_min_real; direct below
+  // kGridAutoRatio of the direct FMAs and its a-priori error bound is within kGridAutoMaxErr, else VALU,
+  // for R >= mfma_min_real; direct below. c->path_reason says why auto did not take the gridded path.
   int path = c->synth_path;
-  if (!allow_mfma) path = 1;
-  if (path == 0 || path == 4) {
-    const bool want = path == 4;
-    if ((want || R >= c->mfma_min_real) && L.all_harmonic && c->anchor == 0) {
+  c->path_reason.clear();
+  if (!allow_mfma) {
+    path = 1;
+    c->path_reason = "single-realization drop-in call: direct path (exact phases)";
+  } else if (path == 4) {
+    if (!L.all_harmonic) return fail(c, FPTA_EINVAL, "gridded path: every signal needs a harmonic grid f_k = k f_1");
+    if (c->anchor != 0) return fail(c, FPTA_EINVAL, "gridded path: needs anchor 0");
+    int rc = grid_build(c, L);
+    if (rc) return rc;
+    if (!L.grid.ok) return fail(c, FPTA_EINVAL, L.grid.why);
+  } else if (path == 0) {
+    path = 3;
+    if (R < c->mfma_min_real) {
+      path = 1;
+      c->path_reason = "gridded path: n_real below FPTA_OPT_MFMA_MIN_REAL (direct path)";
+    } else if (!L.all_harmonic) {
+      c->path_reason = "gridded path: every signal needs a harmonic grid f_k = k f_1";
+    } else if (c->anchor != 0) {
+      c->path_reason = "gridded path: needs anchor 0";
+    } else {
       int rc = grid_build(c, L);
       if (rc) return rc;
+      if (!L.grid.ok)
+        c->path_reason = L.grid.why;
+      else if (L.grid.err_bound > kGridAutoMaxErr)
+        c->path_reason = "gridded path: a-priori error bound " + std::to_string(L.grid.err_bound) +
+                         " of the width/oversampling options exceeds " + std::to_string(kGridAutoMaxErr);
+      else if (!(L.grid.fma_grid < kGridAutoRatio * L.grid.fma_direct))
+        c->path_reason = "gridded path: not cheaper than the direct contraction for this layout";
+      else
+        path = 4;
     }
-    const bool ok = L.grid.built && L.grid.ok;
-    if (want && !ok)
-      return fail(c, FPTA_EINVAL,
-                  L.grid.why.empty() ? std::string("gridded path: needs harmonic grids and anchor 0")
-                                     : L.grid.why);
-    if (ok && (want || L.grid.fma_grid < kGridAutoRatio * L.grid.fma_direct))
-      path = 4;
-    else if (path == 0)
-      path = R >= c->mfma_min_real ? 3 : 1;
   }
   // host-side guards of what the tiled kernels assume (every tile's realization block lies inside
   // the coefficient padding; the coefficient buffer holds P*K*R_pad values)
@@ -735,13 +838,13 @@ int run_synth(fpta_ctx* c, Layout& L, int32_t R, int32_t R_pad, double* out, int
     return grid_run(c, L, a, R_pad);
   } else if (path == 2) {
     int rc = build_tiles(c, L, R, kTileToa, kTileReal);
-    if (rc) return rc;
+    if (rc || (rc = check_tiles(c, L, R, kTileToa, kTileReal, a))) return rc;
     KTimer kt(c, FPTA_K_SYNTH);
     HIPCHK(c, launch_synth_mfma(c->stream, a, L.tiles.as<int4>(), L.n_tiles), "k_synth_mfma launch");
   } else if (path == 3 && L.all_harmonic && c->anchor == 0) {
     const ValuVariant v = kSeededVariants[c->valu_variant];
     int rc = build_tiles(c, L, R, 4 * 64 * v.mt, v.nt);
-    if (rc) return rc;
+    if (rc || (rc = check_tiles(c, L, R, 4 * 64 * v.mt, v.nt, a))) return rc;
     if (white && white->on && c->fuse_white) {
       a.w_on = 1;
       a.w_sigma = white->sigma;
@@ -762,7 +865,7 @@ int run_synth(fpta_ctx* c, Layout& L, int32_t R, int32_t R_pad, double* out, int
   } else if (path == 3) {
     const ValuVariant v = kValuVariants[c->valu_variant];
     int rc = build_tiles(c, L, R, 64 * v.mt, 4 * v.nt);
-    if (rc) return rc;
+    if (rc || (rc = check_tiles(c, L, R, 64 * v.mt, 4 * v.nt, a))) return rc;
     KTimer kt(c, FPTA_K_SYNTH);
     HIPCHK(c, launch_synth_valu(c->stream, a, L.tiles.as<int4>(), L.n_tiles, c->valu_variant),
            "k_synth_valu launch");
@@ -983,6 +1086,30 @@ int fpta_set_option(fpta_ctx* c, int32_t key, int64_t value) {
       return FPTA_OK;
   }
   return fail(c, FPTA_EINVAL, "set_option: unknown key");
+}
+
+int fpta_get_option(fpta_ctx* c, int32_t key, int64_t* value) {
+  if (!c || !value) return fail(c, FPTA_EINVAL, "get_option: bad arguments");
+  switch (key) {
+    case FPTA_OPT_SYNTH_PATH: *value = c->synth_path; return FPTA_OK;
+    case FPTA_OPT_MFMA_MIN_REAL: *value = c->mfma_min_real; return FPTA_OK;
+    case FPTA_OPT_PROFILE: *value = c->profile; return FPTA_OK;
+    case FPTA_OPT_ANCHOR: *value = c->anchor; return FPTA_OK;
+    case FPTA_OPT_VALU_VARIANT: *value = c->valu_variant; return FPTA_OK;
+    case FPTA_OPT_FUSE_WHITE: *value = c->fuse_white; return FPTA_OK;
+    case FPTA_OPT_GRID_WIDTH: *value = c->grid_w; return FPTA_OK;
+    case FPTA_OPT_GRID_SIGMA: *value = c->grid_sigma100; return FPTA_OK;
+    case FPTA_OPT_GRID_MFMA: *value = c->grid_mfma; return FPTA_OK;
+  }
+  return fail(c, FPTA_EINVAL, "get_option: unknown key");
+}
+
+int fpta_build_flags(void) {
+#ifdef FPTA_DEBUG
+  return FPTA_BUILD_DEBUG;
+#else
+  return 0;
+#endif
 }
 
 int fpta_synchronize(fpta_ctx* c) {
@@ -1454,6 +1581,26 @@ int fpta_batch_grid_info(fpta_ctx* c, double* out) {
   out[6] = ok ? G.grid_vals : 0.0;
   out[7] = ok ? G.weight_bytes : 0.0;
   out[8] = c->grid_mfma;
+  out[9] = std::exp(-M_PI * c->grid_w * std::sqrt(1.0 - 100.0 / c->grid_sigma100));
+  out[10] = c->grid_w;
+  out[11] = c->grid_sigma100 / 100.0;
+  return FPTA_OK;
+}
+
+const char* fpta_batch_path_reason(const fpta_ctx* c) { return c ? c->path_reason.c_str() : ""; }
+
+int fpta_debug_fill_out(fpta_ctx* c, double value) {
+  if (!c) return fail(nullptr, FPTA_EINVAL, "null ctx");
+  if (!c->out_R) return fail(c, FPTA_ESTATE, "fill_out: nothing synthesized yet");
+  HIPCHK(c, hipSetDevice(c->device), "hipSetDevice");
+  const size_t n = (size_t)c->out_R * c->out_ld;
+  std::vector<double> v(std::min<size_t>(n, (size_t)1 << 20), value);
+  for (size_t i = 0; i < n; i += v.size())
+    HIPCHK(c,
+           hipMemcpyAsync(c->out.as<double>() + i, v.data(), sizeof(double) * std::min(v.size(), n - i),
+                          hipMemcpyHostToDevice, c->stream),
+           "fill_out copy");
+  HIPCHK(c, hipStreamSynchronize(c->stream), "fill_out sync");
   return FPTA_OK;
 }
 
@@ -1469,6 +1616,164 @@ int fpta_debug_philox(fpta_ctx* c, int64_t n, const uint32_t* ctr, const uint32_
          "philox download");
   HIPCHK(c, hipStreamSynchronize(c->stream), "philox sync");
   return FPTA_OK;
+}
+
+
+// ------------------------------------------------------------------------------------ multi-device
+// One process driving several devices (SURVEY.md §8(b) fpta_multi_*, §8(e)): one context per listed
+// device, the layout replicated on each, realizations sharded contiguously (device g of G owns
+// [real0 + g n / G, real0 + (g + 1) n / G)) and streamed in batches. Only per-realization checksums
+// leave the devices (async D2H into pinned host memory); the residual blocks stay resident. The work
+// of all devices is issued round-robin from this thread on their own streams, so the devices run
+// concurrently. Output is invariant to the device count and the batch size (Philox counters carry the
+// global realization index). Processes that own one GPU each use fakepta_amd.batch.simulate_sharded
+// (torch.distributed / RCCL) instead.
+struct fpta_multi {
+  std::vector<fpta_ctx*> ctx;
+  std::string err;
+};
+
+namespace {
+int multi_fail(fpta_multi* m, int i, int rc) {
+  if (m) m->err = "device context " + std::to_string(i) + ": " + fpta_last_error(m->ctx[i]);
+  g_err = m ? m->err : g_err;
+  return rc;
+}
+
+// k_checksums of the context's last block -> host (pinned) dst [n_real][2], asynchronously on the ctx stream.
+int checksums_async(fpta_ctx* c, double* dst) {
+  HIPCHK(c, c->sums.ensure(sizeof(double) * 2 * c->out_R), "sums alloc");
+  HIPCHK(c, launch_checksums(c->stream, c->out.as<double>(), c->out_ld, c->out_ld, c->out_R, c->sums.as<double>()),
+         "k_checksums launch");
+  HIPCHK(c, hipMemcpyAsync(dst, c->sums.p, sizeof(double) * 2 * c->out_R, hipMemcpyDeviceToHost, c->stream),
+         "sums download");
+  return FPTA_OK;
+}
+}  // namespace
+
+int fpta_multi_create(int32_t n_dev, const int32_t* devices, fpta_multi** out) {
+  if (!out || n_dev <= 0 || !devices) return fail(nullptr, FPTA_EINVAL, "multi_create: bad arguments");
+  *out = nullptr;
+  fpta_multi* m = new fpta_multi();
+  for (int32_t i = 0; i < n_dev; ++i) {
+    fpta_ctx* c = nullptr;
+    int rc = fpta_create(devices[i], &c);
+    if (rc) {
+      std::string msg = "multi_create: device " + std::to_string(devices[i]) + ": " + g_err;
+      fpta_multi_destroy(m);
+      return fail(nullptr, rc, msg);
+    }
+    m->ctx.push_back(c);
+  }
+  *out = m;
+  return FPTA_OK;
+}
+
+int fpta_multi_destroy(fpta_multi* m) {
+  if (!m) return FPTA_OK;
+  for (fpta_ctx* c : m->ctx) fpta_destroy(c);
+  delete m;
+  return FPTA_OK;
+}
+
+const char* fpta_multi_last_error(const fpta_multi* m) { return m ? m->err.c_str() : g_err.c_str(); }
+
+int fpta_multi_size(const fpta_multi* m) { return m ? (int)m->ctx.size() : 0; }
+
+fpta_ctx* fpta_multi_context(fpta_multi* m, int32_t i) {
+  return (m && i >= 0 && i < (int32_t)m->ctx.size()) ? m->ctx[i] : nullptr;
+}
+
+int fpta_multi_set_toas(fpta_multi* m, int32_t n_psr, const int64_t* offs, const double* toas, const double* nu) {
+  if (!m) return fail(nullptr, FPTA_EINVAL, "null multi");
+  for (size_t i = 0; i < m->ctx.size(); ++i) {
+    int rc = fpta_batch_set_toas(m->ctx[i], n_psr, offs, toas, nu);
+    if (rc) return multi_fail(m, (int)i, rc);
+  }
+  return FPTA_OK;
+}
+
+int fpta_multi_add_signal(fpta_multi* m, int32_t kind, int32_t n_modes, const double* f, const double* amp,
+                          double idx, double freqf, const double* Lmat, const uint8_t* mask) {
+  if (!m) return fail(nullptr, FPTA_EINVAL, "null multi");
+  int id = -1;
+  for (size_t i = 0; i < m->ctx.size(); ++i) {
+    int rc = fpta_batch_add_signal(m->ctx[i], kind, n_modes, f, amp, idx, freqf, Lmat, mask);
+    if (rc < 0) return multi_fail(m, (int)i, rc);
+    id = rc;
+  }
+  return id;
+}
+
+int fpta_multi_set_white(fpta_multi* m, const double* sigma, int64_t n_blocks, const int64_t* block_offs,
+                         const int64_t* block_idx, const double* ecorr_sigma) {
+  if (!m) return fail(nullptr, FPTA_EINVAL, "null multi");
+  for (size_t i = 0; i < m->ctx.size(); ++i) {
+    int rc = fpta_batch_set_white(m->ctx[i], sigma, n_blocks, block_offs, block_idx, ecorr_sigma);
+    if (rc) return multi_fail(m, (int)i, rc);
+  }
+  return FPTA_OK;
+}
+
+int fpta_multi_set_option(fpta_multi* m, int32_t key, int64_t value) {
+  if (!m) return fail(nullptr, FPTA_EINVAL, "null multi");
+  for (size_t i = 0; i < m->ctx.size(); ++i) {
+    int rc = fpta_set_option(m->ctx[i], key, value);
+    if (rc) return multi_fail(m, (int)i, rc);
+  }
+  return FPTA_OK;
+}
+
+int fpta_multi_synth(fpta_multi* m, uint64_t seed, int64_t real0, int64_t n_real, int32_t batch,
+                     double* checksums_out) {
+  if (!m) return fail(nullptr, FPTA_EINVAL, "null multi");
+  if (n_real <= 0 || real0 < 0 || batch <= 0 || !checksums_out) {
+    m->err = "multi_synth: bad arguments";
+    return fail(nullptr, FPTA_EINVAL, m->err);
+  }
+  if (real0 + n_real > ((int64_t)1 << 32)) {
+    m->err = "multi_synth: realization index exceeds the 32-bit Philox counter word";
+    return fail(nullptr, FPTA_EINVAL, m->err);
+  }
+  const int64_t G = (int64_t)m->ctx.size();
+  std::vector<int64_t> beg(G + 1);
+  for (int64_t g = 0; g <= G; ++g) beg[g] = g * n_real / G;
+  // pinned staging for each device's shard of checksums
+  std::vector<double*> stage(G, nullptr);
+  int rc = FPTA_OK;
+  for (int64_t g = 0; g < G && !rc; ++g) {
+    const int64_t n = beg[g + 1] - beg[g];
+    if (n == 0) continue;
+    fpta_ctx* c = m->ctx[g];
+    hipError_t e = hipSetDevice(c->device);
+    if (e == hipSuccess) e = hipHostMalloc((void**)&stage[g], sizeof(double) * 2 * n, hipHostMallocDefault);
+    if (e != hipSuccess) rc = multi_fail(m, (int)g, hip_fail(c, e, "multi_synth staging"));
+  }
+  // round-robin: batch k of every device, then batch k + 1 (each device's stream orders its own work)
+  for (int64_t k = 0; !rc; ++k) {
+    bool any = false;
+    for (int64_t g = 0; g < G && !rc; ++g) {
+      const int64_t first = beg[g] + k * (int64_t)batch;
+      if (first >= beg[g + 1]) continue;
+      any = true;
+      const int32_t n = (int32_t)std::min<int64_t>(batch, beg[g + 1] - first);
+      fpta_ctx* c = m->ctx[g];
+      if ((rc = batch_common(c, seed, real0 + first, n, nullptr, 0, nullptr, nullptr, true)) ||
+          (rc = checksums_async(c, stage[g] + 2 * (first - beg[g]))))
+        rc = multi_fail(m, (int)g, rc);
+    }
+    if (!any) break;
+  }
+  for (int64_t g = 0; g < G; ++g) {
+    if (!stage[g]) continue;
+    fpta_ctx* c = m->ctx[g];
+    (void)hipSetDevice(c->device);
+    hipError_t e = hipStreamSynchronize(c->stream);
+    if (!rc && e != hipSuccess) rc = multi_fail(m, (int)g, hip_fail(c, e, "multi_synth sync"));
+    if (!rc) std::memcpy(checksums_out + 2 * (beg[g] - 0), stage[g], sizeof(double) * 2 * (beg[g + 1] - beg[g]));
+    (void)hipHostFree(stage[g]);
+  }
+  return rc;
 }
 
 }  // extern "C"

@@ -2,6 +2,25 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+// Device-side bounds checks of the debug build (make debug, -DFPTA_DEBUG): a failed check prints the
+// kernel, the index and the bound, then traps (the launch reports a device fault). Release builds
+// compile them out.
+#ifdef FPTA_DEBUG
+#include <cstdio>
+#define FPTA_DCHECK(cond, what, idx, bound)                                                          \
+  do {                                                                                               \
+    if (!(cond)) {                                                                                   \
+      printf("FPTA_DCHECK %s: index %lld outside [0, %lld) (block %u thread %u)\n", what,           \
+             (long long)(idx), (long long)(bound), blockIdx.x, threadIdx.x);                          \
+      __builtin_trap();                                                                              \
+    }                                                                                                \
+  } while (0)
+#else
+#define FPTA_DCHECK(cond, what, idx, bound) \
+  do {                                      \
+  } while (0)
+#endif
+
 namespace fpta {
 
 typedef double d4 __attribute__((ext_vector_type(4)));

@@ -47,6 +47,10 @@ struct SynthArgs {
   int64_t w_nblocks;
   int64_t real0;               // global index of realization 0 of the batch
   uint32_t k0, k1;             // Philox key (seed)
+  // geometry checked by the debug build (FPTA_DCHECK): coefficient values P*K*R_pad, and the TOA x
+  // realization tile the tile table was built for (0 when the kernel takes no tile table)
+  int64_t coef_len;
+  int32_t tile_toa, tile_real;
 };
 
 // MFMA tile geometry
@@ -88,12 +92,33 @@ struct GridSegs {
   int32_t n;
 };
 
+// VALU interpolation (grid_sparse.hip): a TOA's first band row lies at most kSparseD rows past its chunk's base
+// row, so a register window of w + D_s <= w + kSparseD rows per signal serves the whole chunk; weight records of
+// kSparseRec window slots per (signal, TOA); work items of <= kSparseChunks consecutive chunks of one pulsar.
+constexpr int kSparseD = 4;
+constexpr int kSparseRec = 20;
+constexpr int kSparseChunks = 4;
+struct SparseSegDev {
+  const double* g;        // [P][nf][R_pad] grid values of the batch (shared with GridSegDev)
+  const double* rec;      // [n_toa][kSparseRec] window-slot weight records
+  const int32_t* base;    // [n_chunks] base row of the chunk (mod nf)
+  int32_t nf;
+  int32_t ws;             // window rows of this signal: w + the largest first-row offset in any chunk
+};
+struct SparseSegs {
+  SparseSegDev s[kGridMaxSeg];
+  int32_t n;
+};
+bool sparse_width_supported(int32_t w);
+hipError_t launch_grid_records(hipStream_t st, const SegDesc& sd, int64_t n_toa, const double* nu,
+                               const double* d_of, const int32_t* off_of, int32_t w, double beta, double* rec);
+hipError_t launch_grid_interp_sparse(hipStream_t st, const SynthArgs& a, const int4* chunks, const int4* work,
+                                     int32_t n_work, const SparseSegs& ss, int32_t R_pad);
+
 hipError_t launch_grid_weights(hipStream_t st, const SegDesc& sd, int64_t n_toa, const double* nu,
                                const int32_t* chunk_of, const int32_t* tt_of, const int32_t* row_of,
                                const double* d_of, int32_t w, double beta, int32_t rmax, double* wd);
 hipError_t launch_grid_dft(hipStream_t st, GridSegs gsegs, int32_t P, const double* coef, int32_t K, int32_t R_pad);
-hipError_t launch_grid_interp(hipStream_t st, const SynthArgs& a, const int4* chunks, int32_t n_chunks,
-                              const GridSegs& gsegs, int32_t R_pad);
 // the same two steps on v_mfma_f64_16x16x4_f64 (grid_mfma.hip)
 hipError_t launch_grid_dft_mfma(hipStream_t st, GridSegs gsegs, int32_t P, const double* coef, int32_t K,
                                 int32_t R_pad);

@@ -8,8 +8,9 @@
 //                   x_j = 2 pi j / nf, for every (pulsar, realization) - a real DFT done as a GEMM
 //                   against the shared table E (both halves of the grid from one pass: the cos and
 //                   sin partial sums give g_j and g_{nf-j})
-//   k_grid_interp   per batch: r(t) = sum_i W[t][i] g[J_t + i] for all signals of the chunk, white
-//                   noise / ECORR added in the epilogue, one store per sample
+//   interpolation   per batch: r(t) = sum_i W[t][i] g[J_t + i] for all signals, white noise / ECORR in
+//                   the epilogue, one store per sample: k_grid_interp_sparse (grid_sparse.hip, VALU, w FMAs
+//                   per sample and signal) or k_grid_interp_mfma (grid_mfma.hip, dense 4-row MFMA steps)
 //
 // Kernel: exponential of semicircle phi(z) = exp(beta (sqrt(1 - z^2) - 1)), |z| <= 1, width w grid
 // cells, oversampling nf >= sigma (2N + 1); q_k = (2 pi / nf) / phi_hat(k) deconvolves it.
@@ -121,178 +122,6 @@ __global__ __launch_bounds__(256) void k_grid_dft(GridSegs gsegs, const double* 
   }
 }
 
-__device__ __forceinline__ void grid_white_pair(int64_t t, int64_t g, uint32_t k0, uint32_t k1, double& z0,
-                                                double& z1) {
-  const u32x4 c = {(uint32_t)t, kWhitePsrWord, kWhiteStream, (uint32_t)(g >> 1)};
-  box_muller(philox4x32_10(c, k0, k1), z0, z1);
-}
-
-// ----------------------------------------------------------------------------- k_grid_interp
-// 1-D grid of n_chunks * ceil(R_pad / 512) tiles (padded to a multiple of 8), XCD-swizzled so that an
-// XCD walks consecutive chunks of the same pulsar (their grid rows overlap: L2 reuse). Wave = 128
-// realizations (lane: adjacent pair) x the chunk's TT TOAs; per grid row one 16-byte load per lane and
-// TT wave-uniform weights (scalar loads), 2 TT FMAs.
-template <bool WHITE, int DBG, int H = kGridTT / 2, bool NT = false, bool PRIO = false>
-__global__ __launch_bounds__(256) void k_grid_interp(SynthArgs a, const int4* __restrict__ chunks, int32_t n_chunks,
-                                                     int32_t n_rb, GridSegs gsegs, int32_t R_pad, int32_t n_lin_stagger,
-                                                     int32_t stagger, double* __restrict__ out) {
-  // `out` (= a.out) as a noalias argument: the stores of one tile cannot clobber the tables read by the
-  // next, so the weight loads stay scalar (s_load) inside the persistent loop
-  // Workgroups of the first dispatch round (blockIdx.x < stagger_n) start staggered by (b / 8) % 4
-  // quarter-periods. All tiles cost the same, so without it the store bursts of the resident
-  // workgroups stay in phase (compute, then all store together); a new workgroup starts when an old
-  // one exits, so the first round's stagger carries over to the whole grid.
-  // The delay is a scalar-ALU recurrence: s_sleep (builtin or asm) counts as a memory side effect and
-  // would turn every later table load of the kernel into a vector load.
-  if ((int)blockIdx.x < n_lin_stagger) {
-    uint32_t x = blockIdx.x;
-    const int n = ((blockIdx.x >> 3) & 3) * stagger * 256;
-    for (int k = 0; k < n; ++k) x = x * 1664525u + 1013904223u;
-    if (x == 0x7FFFFFFFu && n < 0) return;  // never taken; keeps the loop
-  }
-  const int per = gridDim.x >> 3;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  {
-  const int lin = blockIdx.x;
-  const int tile = (lin & 7) * per + (lin >> 3);
-  if (tile >= n_chunks * n_rb) return;
-  // wave-uniform by construction; readfirstlane keeps the divergence analysis from losing that inside
-  // the persistent loop (the band loop below must stay scalar: scalar weight loads, SGPR operands)
-  const int rb = __builtin_amdgcn_readfirstlane(tile / n_chunks);
-  const int c = __builtin_amdgcn_readfirstlane(tile - rb * n_chunks);
-  const int r0 = (rb * 4 + wave) * 128;
-  if (r0 >= R_pad) return;
-  const int4 ci = chunks[c];
-  const int p = __builtin_amdgcn_readfirstlane(ci.x);
-  const int64_t base = a.offs[p];
-  const int rl = r0 + 2 * lane;
-
-  dbl2 acc[kGridTT];
-#pragma unroll
-  for (int tt = 0; tt < kGridTT; ++tt) acc[tt] = (dbl2){0.0, 0.0};
-
-  // segment tables come from the kernel arguments (constant address space): wave-uniform scalar loads
-  for (int s = 0; s < (DBG == 4 ? 0 : gsegs.n); ++s) {
-    const GridSegDev& gs = gsegs.s[s];
-    const int2 jr0 = gs.js[c];
-    const int2 jr = make_int2(__builtin_amdgcn_readfirstlane(jr0.x), __builtin_amdgcn_readfirstlane(jr0.y));
-    const double* __restrict__ W = gs.wd + (int64_t)c * gs.rmax * kGridTT;
-    const double* __restrict__ G = gs.g + (int64_t)p * gs.nf * R_pad + rl;
-    // rows come in pairs (the host pads every band to an even row count with zero weights); two
-    // register sets alternate so each row's load is issued one row ahead of its FMAs
-    int j = jr.x;
-    dbl2 ga = *(const dbl2*)(G + (int64_t)j * R_pad);
-    if (++j == gs.nf) j = 0;
-    dbl2 gb = *(const dbl2*)(G + (int64_t)j * R_pad);
-    for (int i = 0; i < jr.y; i += 2) {
-      const double* __restrict__ Wi = DBG == 2 ? W : W + i * kGridTT;
-      if (++j == gs.nf) j = 0;
-      const dbl2 gan = DBG == 1 ? (dbl2){1.0 * i, 2.0} : *(const dbl2*)(G + (int64_t)j * R_pad);  // rows past the band are valid grid rows
-#pragma unroll
-      for (int tt = 0; tt < kGridTT; ++tt) {
-        acc[tt].x = fma(Wi[tt], ga.x, acc[tt].x);
-        acc[tt].y = fma(Wi[tt], ga.y, acc[tt].y);
-      }
-      if (++j == gs.nf) j = 0;
-      const dbl2 gbn = DBG == 1 ? (dbl2){2.0 * i, 1.0} : *(const dbl2*)(G + (int64_t)j * R_pad);
-#pragma unroll
-      for (int tt = 0; tt < kGridTT; ++tt) {
-        acc[tt].x = fma(Wi[kGridTT + tt], gb.x, acc[tt].x);
-        acc[tt].y = fma(Wi[kGridTT + tt], gb.y, acc[tt].y);
-      }
-      ga = gan;
-      gb = gbn;
-    }
-  }
-
-  const int cnt = __builtin_amdgcn_readfirstlane(ci.z);
-  if constexpr (WHITE) {
-    const int64_t g0 = a.real0 + rl;  // parity is wave-uniform (r0 and 2 lane are even)
-#pragma unroll
-    for (int tt = 0; tt < kGridTT; ++tt) {
-      if (tt < cnt) {
-        const int64_t tg = base + ci.y + tt;
-        if (a.w_sigma) {
-          const double sg = a.w_sigma[tg];
-          double z0, z1, y0, y1;
-          grid_white_pair(tg, g0, a.k0, a.k1, z0, z1);
-          if (g0 & 1) {  // (g0, g0 + 1) straddle two pairs
-            grid_white_pair(tg, g0 + 1, a.k0, a.k1, y0, y1);
-            acc[tt].x = fma(sg, z1, acc[tt].x);
-            acc[tt].y = fma(sg, y0, acc[tt].y);
-          } else {
-            acc[tt].x = fma(sg, z0, acc[tt].x);
-            acc[tt].y = fma(sg, z1, acc[tt].y);
-          }
-        }
-        const int ep = a.w_block_of ? a.w_block_of[tg] : -1;
-        if (ep >= 0) {
-          const double e = a.w_esig[ep];
-          if (rl < a.n_real) acc[tt].x = fma(e, a.w_zb[(int64_t)rl * a.w_nblocks + ep], acc[tt].x);
-          if (rl + 1 < a.n_real) acc[tt].y = fma(e, a.w_zb[(int64_t)(rl + 1) * a.w_nblocks + ep], acc[tt].y);
-        }
-      }
-    }
-  }
-
-  // Store through LDS in two halves of kGridTT/2 TOAs: lane l then writes TOA (l % 8) of realization
-  // 8 i + l / 8, i.e. 64-byte runs of one realization row instead of 64 scattered 8-byte words
-  // (8x fewer L2 write requests). Each wave uses its own LDS slice; no cross-wave synchronisation.
-  if constexpr (DBG == 10) {  // coalesced scratch layout [chunk][tt][R_pad] (diagnostic)
-    const int64_t lim = (int64_t)a.n_real * a.ldo;
-#pragma unroll
-    for (int tt = 0; tt < kGridTT; ++tt) {
-      const int64_t o = ((int64_t)c * kGridTT + tt) * R_pad + rl;
-      if (o + 1 < lim) *(dbl2*)(out + o) = acc[tt];
-    }
-    return;
-  }
-  if constexpr (DBG == 3) {
-    double sum = 0.0;
-#pragma unroll
-    for (int tt = 0; tt < kGridTT; ++tt) sum += acc[tt].x + acc[tt].y;
-    if (sum == 123.456) out[rl] = sum;
-    return;
-  }
-  // PAR: transpose even and odd realizations in separate passes (half the LDS per wave)
-  if constexpr (PRIO) __builtin_amdgcn_s_setprio(3);
-  constexpr int NP = kGridTT / H;      // TOA passes
-  constexpr int LPR = H;               // lanes per realization row in a store instruction
-  constexpr int RPI = 64 / LPR;        // realization rows per store instruction
-  __shared__ double tbuf[4][64][H + 1];
-  double(*tb)[H + 1] = tbuf[wave];
-  const int q = lane / LPR, th = lane % LPR;
-#pragma unroll
-  for (int h = 0; h < NP; ++h) {
-#pragma unroll
-    for (int par = 0; par < 2; ++par) {
-#pragma unroll
-      for (int u = 0; u < H; ++u) tb[lane][u] = par ? acc[h * H + u].y : acc[h * H + u].x;
-      __builtin_amdgcn_wave_barrier();
-      const int tt = h * H + th;
-      if (tt < cnt) {
-        double* ocol = out + base + ci.y + tt;
-#pragma unroll 4
-        for (int i = 0; i < 64 / RPI; ++i) {
-          const int rr = RPI * i + q;          // lane rr of the wave holds realization 2 rr + par
-          const int r = r0 + 2 * rr + par;
-          if (r < a.n_real) {
-            double* o = ocol + (int64_t)r * a.ldo;
-            const double v = a.accumulate ? *o + tb[rr][th] : tb[rr][th];
-            if constexpr (NT)
-              __builtin_nontemporal_store(v, o);
-            else
-              *o = v;
-          }
-        }
-      }
-      __builtin_amdgcn_wave_barrier();
-    }
-  }
-  }
-}
-
 hipError_t launch_grid_weights(hipStream_t st, const SegDesc& sd, int64_t n_toa, const double* nu,
                                const int32_t* chunk_of, const int32_t* tt_of, const int32_t* row_of,
                                const double* d_of, int32_t w, double beta, int32_t rmax, double* wd) {
@@ -313,47 +142,6 @@ hipError_t launch_grid_dft(hipStream_t st, GridSegs gsegs, int32_t P, const doub
   if (gx > 65535) return hipErrorInvalidValue;
   hipLaunchKernelGGL((k_grid_dft<kGridMI>), dim3((unsigned)((R_pad / 128 + 3) / 4), (unsigned)P, (unsigned)gx), dim3(256),
                      0, st, gsegs, coef, K, R_pad);
-  return hipGetLastError();
-}
-
-hipError_t launch_grid_interp(hipStream_t st, const SynthArgs& a, const int4* chunks, int32_t n_chunks,
-                              const GridSegs& gsegs, int32_t R_pad) {
-  if (R_pad % 128 != 0 || n_chunks <= 0 || gsegs.n < 0 || gsegs.n > kGridMaxSeg) return hipErrorInvalidValue;
-  const int32_t n_rb = (R_pad + 511) / 512;
-  const int64_t tiles = (int64_t)n_chunks * n_rb;
-  const int64_t n_lin = (tiles + 7) / 8 * 8;
-  if (n_lin > 0x7FFFFFFF) return hipErrorInvalidValue;
-  static const int cfg_stagger = [] { const char* e = getenv("FPTA_GRID_STAGGER"); return e ? atoi(e) : 2; }();
-  static const int cfg_wpc = [] { const char* e = getenv("FPTA_GRID_WPC"); return e ? atoi(e) : 4; }();
-  static int n_cu = 0;
-  if (!n_cu) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0)
-      n_cu = 256;
-  }
-  const int64_t grid = n_lin;
-  const int32_t stagger = cfg_stagger;
-  const int32_t nl = (int32_t)std::min<int64_t>(n_lin, (int64_t)n_cu * cfg_wpc);  // first dispatch round
-  static const int dbg = [] { const char* e = getenv("FPTA_GRID_DBG"); return e ? atoi(e) : 0; }();
-#define L_(...) hipLaunchKernelGGL((k_grid_interp<__VA_ARGS__>), dim3((unsigned)grid), dim3(256), 0, st, a, chunks, n_chunks, n_rb, gsegs, R_pad, nl, stagger, a.out)
-  switch (dbg) {
-    case 1: L_(false, 1); break;
-    case 2: L_(false, 2); break;
-    case 3: L_(false, 3); break;
-    case 4: L_(false, 4); break;
-    case 5: L_(false, 0, 8, true); break;
-    case 6: L_(false, 0, 4, false); break;
-    case 7: L_(false, 0, 4, true); break;
-    case 8: L_(false, 4, 4, false); break;
-    case 9: L_(false, 4, 8, true); break;
-    case 10: L_(false, 10); break;
-    case 11: L_(false, 0, 8, false, true); break;
-    case 12: L_(false, 0, 8, false, false); break;
-    case 13: L_(false, 4, 16, false, false); break;
-    default:
-      if (a.w_on) L_(true, 0, 16); else L_(false, 0, 16);
-  }
-#undef L_
   return hipGetLastError();
 }
 

@@ -125,7 +125,7 @@ __device__ __forceinline__ void mfma_white_pair(int64_t t, int64_t g, uint32_t k
 // for the white epilogue), and every store instruction writes 4 full 128-byte runs.
 // Tile = chunk x 64 RW realizations, wave = chunk x 16 RW; per signal the next 4-row step's operands are
 // loaded before the current step's MFMAs (two register sets, unrolled by 2).
-template <bool WHITE, int RW, int EXP = 0>
+template <bool WHITE, int RW>
 __device__ __forceinline__ void interp_tile(const SynthArgs& a, const int4* __restrict__ chunks, int32_t n_chunks,
                                             const GridSegs& gsegs, int32_t R_pad, double* __restrict__ out,
                                             int tile) {
@@ -149,7 +149,7 @@ __device__ __forceinline__ void interp_tile(const SynthArgs& a, const int4* __re
   // per signal: steps of 4 band rows; the next step's operands are loaded (unconditionally: the last
   // prefetch re-reads the final step) before the current step's MFMAs, so the wait ahead of the MFMAs
   // counts only the older loads
-  for (int si = 0; si < (EXP == 2 ? 0 : gsegs.n); ++si) {
+  for (int si = 0; si < gsegs.n; ++si) {
     const GridSegDev& gs = gsegs.s[si];
     const int2 jr = gs.js[c];
     const int nq = __builtin_amdgcn_readfirstlane(jr.y) >> 2;
@@ -228,7 +228,7 @@ __device__ __forceinline__ void interp_tile(const SynthArgs& a, const int4* __re
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const int r = r0 + 32 * (i >> 1) + 2 * (lg + 4 * g) + (i & 1);
-      if (r < a.n_real && (EXP != 1 || acc[i][g] == 123.25)) {
+      if (r < a.n_real) {
         double* o = ocol + (int64_t)r * a.ldo;
         *o = a.accumulate ? *o + acc[i][g] : acc[i][g];
       }
@@ -240,7 +240,7 @@ __device__ __forceinline__ void interp_tile(const SynthArgs& a, const int4* __re
 // b runs on XCD b % 8 and walks that XCD's contiguous range of tiles (consecutive chunks: their grid rows
 // overlap, so they stay in the XCD's L2). One tile per short-lived workgroup instead left the CUs mostly
 // empty (SQ_WAVE_CYCLES ~ 0.7 resident waves per SIMD): workgroup dispatch, not the memory system, paced it.
-template <bool WHITE, int RW, int EXP = 0>
+template <bool WHITE, int RW>
 __global__ __launch_bounds__(256) void k_grid_interp_mfma(SynthArgs a, const int4* __restrict__ chunks,
                                                           int32_t n_chunks, int32_t n_tiles, GridSegs gsegs,
                                                           int32_t R_pad, double* __restrict__ out) {
@@ -249,7 +249,7 @@ __global__ __launch_bounds__(256) void k_grid_interp_mfma(SynthArgs a, const int
   const int step = gridDim.x >> 3;
   const int end = min(n_tiles, (x + 1) * per);
   for (int tile = x * per + (int)(blockIdx.x >> 3); tile < end; tile += step)
-    interp_tile<WHITE, RW, EXP>(a, chunks, n_chunks, gsegs, R_pad, out, tile);
+    interp_tile<WHITE, RW>(a, chunks, n_chunks, gsegs, R_pad, out, tile);
 }
 
 
@@ -287,18 +287,10 @@ hipError_t launch_interp_rw(hipStream_t st, const SynthArgs& a, const int4* chun
         hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0)
       n_cu = 256;
   }
-  // workgroups per CU of the persistent grid (tuning knob; co-residency is set by the register count)
-  static const int wpc = [] { const char* e = getenv("FPTA_INTERP_WPC"); return e ? atoi(e) : 2; }();
-  const int64_t want = (int64_t)n_cu * (wpc > 0 ? wpc : 2);
+  // persistent grid: 2 workgroups per CU (profiles/r01_sweep_interp_wpc.txt: 1 -> 1.06 ms, 2 -> 0.74, 3 -> 0.81)
+  const int64_t want = (int64_t)n_cu * 2;
   const int64_t grid = std::min<int64_t>((tiles + 7) / 8 * 8, (want + 7) / 8 * 8);
-  static const int exp_ = [] { const char* e = getenv("FPTA_INTERP_EXP"); return e ? atoi(e) : 0; }();
-  if (exp_ == 1 && !a.w_on)  // diagnostics: no stores / no band loop
-    hipLaunchKernelGGL((k_grid_interp_mfma<false, RW, 1>), dim3((unsigned)grid), dim3(256), 0, st, a, chunks,
-                       n_chunks, (int32_t)tiles, gsegs, R_pad, a.out);
-  else if (exp_ == 2 && !a.w_on)
-    hipLaunchKernelGGL((k_grid_interp_mfma<false, RW, 2>), dim3((unsigned)grid), dim3(256), 0, st, a, chunks,
-                       n_chunks, (int32_t)tiles, gsegs, R_pad, a.out);
-  else if (a.w_on)
+  if (a.w_on)
     hipLaunchKernelGGL((k_grid_interp_mfma<true, RW>), dim3((unsigned)grid), dim3(256), 0, st, a, chunks, n_chunks,
                        (int32_t)tiles, gsegs, R_pad, a.out);
   else
@@ -312,14 +304,7 @@ hipError_t launch_grid_interp_mfma(hipStream_t st, const SynthArgs& a, const int
   if (n_chunks <= 0 || gsegs.n < 0 || gsegs.n > kGridMaxSeg) return hipErrorInvalidValue;
   for (int s = 0; s < gsegs.n; ++s)
     if (gsegs.s[s].rmax % 4 != 0 || gsegs.s[s].nf < 4) return hipErrorInvalidValue;
-  // realizations per wave / 16 (tuning knob, measured by tools/sweep_grid.py)
-  static const int rw = [] { const char* e = getenv("FPTA_INTERP_RW"); return e ? atoi(e) : kInterpRW; }();
-  switch (rw) {
-    case 2: return launch_interp_rw<2>(st, a, chunks, n_chunks, gsegs, R_pad);
-    case 6: return launch_interp_rw<6>(st, a, chunks, n_chunks, gsegs, R_pad);
-    case 4: return launch_interp_rw<4>(st, a, chunks, n_chunks, gsegs, R_pad);
-    default: return launch_interp_rw<8>(st, a, chunks, n_chunks, gsegs, R_pad);
-  }
+  return launch_interp_rw<kInterpRW>(st, a, chunks, n_chunks, gsegs, R_pad);
 }
 
 }  // namespace fpta

@@ -242,6 +242,9 @@ __global__ __launch_bounds__(256, 2) void k_synth_mfma(SynthArgs a, const int4* 
   const int np_ = (int)(a.offs[p + 1] - base);
   const int tw0 = tl.y + wave * WT * 16;
   const int r0 = tl.z;
+  FPTA_DCHECK(a.tile_toa == kWaves * WT * 16 && a.tile_real == WR * 16, "k_synth_mfma tile geometry", a.tile_real,
+              WR * 16 + 1);
+  FPTA_DCHECK(r0 + WR * 16 <= a.R_pad, "k_synth_mfma realization block", r0 + WR * 16, a.R_pad + 1);
   if (tw0 >= np_) return;  // whole wave past the pulsar's last TOA (no cross-wave sync below)
 
   double t[WT], nuv[WT];
@@ -351,7 +354,10 @@ __global__ __launch_bounds__(256) void k_synth_valu(SynthArgs a, const int4* __r
   const int64_t base = a.offs[p];
   const int np_ = (int)(a.offs[p + 1] - base);
   const int r0 = tl.z + wave * NT;
+  FPTA_DCHECK(a.tile_toa == 64 * MT && a.tile_real == 4 * NT, "k_synth_valu tile geometry", a.tile_real, 4 * NT + 1);
   if (r0 >= a.n_real) return;
+  // every coefficient read below is cb[col * R_pad + n], n < NT: the wave's realizations must lie in the padding
+  FPTA_DCHECK(r0 + NT <= a.R_pad, "k_synth_valu realization block", r0 + NT, a.R_pad + 1);
 
   double t[MT], nuv[MT];
   int tc[MT];
@@ -478,6 +484,10 @@ __global__ __launch_bounds__(256) void k_synth_valu_seeded(SynthArgs a, const in
   const int np_ = (int)(a.offs[p + 1] - base);
   const int tw0 = tl.y + wave * 64 * MT;
   const int r0 = tl.z;
+  FPTA_DCHECK(a.tile_toa == 256 * MT && a.tile_real == NT, "k_synth_valu_seeded tile geometry", a.tile_real, NT + 1);
+  FPTA_DCHECK(r0 + NT <= a.R_pad, "k_synth_valu_seeded realization block", r0 + NT, a.R_pad + 1);
+  FPTA_DCHECK((int64_t)(p + 1) * a.K * a.R_pad <= a.coef_len, "k_synth_valu_seeded coefficient rows",
+              (int64_t)(p + 1) * a.K * a.R_pad, a.coef_len + 1);
   if (tw0 >= np_) return;  // whole wave past the pulsar's last TOA (no cross-wave sync below)
 
   int tc[MT];

@@ -198,23 +198,65 @@ int fpta_batch_info(fpta_ctx* ctx, int64_t* info);
  * out[0] synthesis path of the last batch (1 direct, 2 MFMA, 3 VALU, 4 gridded), out[1] plan usable,
  * out[2] interpolation chunks, out[3] k_grid_dft FMAs per realization, out[4] k_grid_interp FMAs per
  * realization, out[5] direct-contraction FMAs per realization, out[6] grid values per realization,
- * out[7] interpolation-weight bytes, out[8] the FPTA_OPT_GRID_MFMA mask in force. out: host double[9]. */
+ * out[7] interpolation-weight bytes, out[8] the FPTA_OPT_GRID_MFMA mask in force, out[9] the a-priori
+ * relative aliasing bound exp(-pi w sqrt(1 - 1/sigma)) of the width/oversampling options in force (auto
+ * selection takes the gridded path only when it is <= 2e-12), out[10] width w, out[11] oversampling sigma.
+ * out: host double[12]. */
 int fpta_batch_grid_info(fpta_ctx* ctx, double* out);
+/* Why the last batch did not take the gridded path (signal count, non-harmonic grid, error bound, cost,
+ * n_real below the threshold, ...); "" when it did. Owned by the context, valid until the next batch. */
+const char* fpta_batch_path_reason(const fpta_ctx* ctx);
+
+/* ------------------------------------------------------------------ multi-device (one process)
+ * one context per listed device (a device may repeat), the layout replicated on
+ * each, realizations [real0, real0 + n_real) sharded contiguously (device g of G owns
+ * [real0 + g n/G, real0 + (g+1) n/G)) and streamed in batches of <= batch realizations; only the
+ * per-realization checksums (sum, sum of squares; fpta_batch_checksums order) come back, in global
+ * realization order: checksums_out host [n_real][2]. The result is bit-identical for every device
+ * count and batch size. Replaces running the reference's make_fake_array / add_* loop once per
+ * realization (fakepta/fake_pta.py:648-668, fakepta/correlated_noises.py:153-160) over a large
+ * ensemble. One-process-per-GPU jobs (torchrun) use fakepta_amd.batch.simulate_sharded instead. */
+typedef struct fpta_multi fpta_multi;
+int fpta_multi_create(int32_t n_dev, const int32_t* devices, fpta_multi** out);
+int fpta_multi_destroy(fpta_multi* m);
+const char* fpta_multi_last_error(const fpta_multi* m);
+int fpta_multi_size(const fpta_multi* m);
+/* The i-th device context (options, kernel statistics, downloads of its last block). */
+fpta_ctx* fpta_multi_context(fpta_multi* m, int32_t i);
+int fpta_multi_set_toas(fpta_multi* m, int32_t n_psr, const int64_t* offs, const double* toas,
+                        const double* nu);
+int fpta_multi_add_signal(fpta_multi* m, int32_t kind, int32_t n_modes, const double* f,
+                          const double* amp, double idx, double freqf, const double* L,
+                          const uint8_t* mask);
+int fpta_multi_set_white(fpta_multi* m, const double* sigma, int64_t n_blocks,
+                         const int64_t* block_offs, const int64_t* block_idx,
+                         const double* ecorr_sigma);
+int fpta_multi_set_option(fpta_multi* m, int32_t key, int64_t value);
+int fpta_multi_synth(fpta_multi* m, uint64_t seed, int64_t real0, int64_t n_real, int32_t batch,
+                     double* checksums_out);
 
 /* ------------------------------------------------------------------ tuning / profiling */
 #define FPTA_OPT_SYNTH_PATH 1     /* 0 auto, 1 direct (sincos per basis element), 2 fp64 MFMA, 3 fp64 VALU fused,
                                      4 gridded (real DFT to an oversampled phase grid + banded interpolation,
-                                     harmonic grids only; aliasing error ~1e-12 relative at the defaults) */
+                                     harmonic grids only; aliasing error <= ~4e-12 relative at the defaults) */
 #define FPTA_OPT_MFMA_MIN_REAL 2  /* auto: MFMA path when n_real >= this (default 16) */
 #define FPTA_OPT_PROFILE 3        /* 1: time every batch kernel with HIP events on the ctx stream */
 #define FPTA_OPT_ANCHOR 4         /* recurrence re-anchor interval in K-steps of 2 modes (0 = once per signal, default) */
 #define FPTA_OPT_VALU_VARIANT 5   /* tile variant of the VALU fused kernel (0..5) */
 #define FPTA_OPT_FUSE_WHITE 6     /* 1 (default): white/ECORR added in the synthesis epilogue; 0: separate pass */
-#define FPTA_OPT_GRID_WIDTH 7     /* gridded path: interpolation kernel width in grid cells (default 14) */
+#define FPTA_OPT_GRID_WIDTH 7     /* gridded path: interpolation kernel width in grid cells (default 16) */
 #define FPTA_OPT_GRID_SIGMA 8     /* gridded path: grid oversampling x 100 (default 150) */
-#define FPTA_OPT_GRID_MFMA 9      /* gridded path kernels on fp64 MFMA: bit 0 the DFT, bit 1 the interpolation
-                                     (default 3; 0 = both on the fp64 VALU) */
+#define FPTA_OPT_GRID_MFMA 9      /* gridded path kernels on fp64 MFMA: bit 0 the DFT (else fp64 VALU), bit 1 the
+                                     interpolation as dense 4-row MFMA band steps (else the sparse fp64 VALU
+                                     kernel, w FMAs per sample and signal, widths 12..16; wider kernels always
+                                     take the MFMA interpolation). Default 1. */
 int fpta_set_option(fpta_ctx* ctx, int32_t key, int64_t value);
+/* Current value of option `key` (same keys as fpta_set_option). */
+int fpta_get_option(fpta_ctx* ctx, int32_t key, int64_t* value);
+/* Build flags of the loaded library: FPTA_BUILD_DEBUG when built with -DFPTA_DEBUG (make debug: per-launch
+ * synchronisation and device-side bounds checks; never used for measurements). */
+#define FPTA_BUILD_DEBUG 1
+int fpta_build_flags(void);
 /* Kernel ids for fpta_kernel_stats */
 #define FPTA_K_GEN 0
 #define FPTA_K_MIX 1
@@ -232,6 +274,8 @@ int fpta_synchronize(fpta_ctx* ctx);
 /* Philox4x32-10 on device: ctr [n][4], key [2] -> out [n][4]. */
 int fpta_debug_philox(fpta_ctx* ctx, int64_t n, const uint32_t* ctr, const uint32_t* key,
                       uint32_t* out);
+/* Fill the last synthesized device block with `value` (tests: a later batch must overwrite every sample). */
+int fpta_debug_fill_out(fpta_ctx* ctx, double value);
 
 #ifdef __cplusplus
 }

@@ -3,7 +3,7 @@
 This module is a plain numpy restatement of the reference algorithm
 (mfalxa/fakepta @ 2025-08-08, /root/reference), used as the CHECKER for the HIP
 product path. Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline
-leg may import it. The product package (fakepta_amd) never imports it and has
+leg may import it. The product packages (fakepta, fakepta_amd) never import it and has
 no CPU fallback.
 
 Parity pinning: every reference-semantics function below is checked against the

@@ -20,7 +20,7 @@ def built():
 
 def declared():
     text = open(HEADER).read()
-    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(fpta_\w+)\s*\(", text, flags=re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|const char\*|fpta_ctx\*)\s+(fpta_\w+)\s*\(", text, flags=re.M)))
 
 
 def test_header_declares_api():
@@ -46,6 +46,19 @@ def test_version_and_errors_without_gpu():
     if _capi.device_count() == 0:
         with pytest.raises(_capi.FptaError):
             _capi.Context(0)
+        with pytest.raises(_capi.FptaError):
+            _capi.MultiContext([0, 0])
+
+
+def test_release_build_reads_no_environment():
+    """The shipped library is the release build and its code reads no FPTA_* environment variable
+    (debug switches live in the separate -DFPTA_DEBUG build, which bench.py refuses)."""
+    from fakepta_amd import _capi
+    assert _capi.build_flags() == 0
+    csrc = os.path.join(ROOT, "fakepta_amd", "csrc")
+    for name in os.listdir(csrc):
+        if name.endswith((".hip", ".h")):
+            assert "getenv" not in open(os.path.join(csrc, name)).read(), name
 
 
 def test_built_for_gfx950():

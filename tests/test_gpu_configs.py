@@ -4,7 +4,8 @@ own coefficient dump, and from the oracle's own Philox stream) on a subset of pu
 
 C4: 1000 pulsars x 10k TOAs, HD GWB 100 modes, 1000x1000 ORF factor, R = 256.
 C5: 100 pulsars, 2 backends x 2 sub-epoch TOAs, RN30 + DM100 (nu^-2) + Sv100 (nu^-4) + HD30 +
-    monopole30 + dipole30 + EFAC/EQUAD + ECORR (ENTERPRISE convention), R = 128.
+    monopole30 + dipole30 + EFAC/EQUAD + ECORR (ENTERPRISE convention), R = 1024 (the configured size).
+C3 lives in tests/test_gpu_c3.py.
 """
 import numpy as np
 import pytest
@@ -68,10 +69,10 @@ def test_c4_ska_scale(ctx):
 
 
 def test_c5_mixed(ctx):
-    from fakepta_amd import correlated_noises as cn
-    from fakepta_amd import fake_pta as fp
+    from fakepta import correlated_noises as cn
+    from fakepta import fake_pta as fp
     from fakepta_amd.batch import BatchSimulator
-    P, R, seed = 100, 128, 99
+    P, R, seed = 100, 1024, 99
     np.random.seed(7)
     pos = fibonacci(P)
     epochs = np.arange(1, 501) * 7.3 * 86400.0
@@ -101,7 +102,7 @@ def test_c5_mixed(ctx):
     for b, q in enumerate(sim.blocks):
         block_of[q] = b
     segs = oracle_segments(sim)
-    for r0, n in ((0, 2), (127, 1)):
+    for r0, n in ((0, 2), (511, 1), (1023, 1)):
         got = ctx.batch_download(r0, n)
         want = O.batch_synth(sim.offs, sim.toas, sim.freqs, segs, seed, r0, n, sigma=sim.sigma, block_of=block_of,
                              ecorr_sigma=sim.ecorr_sigma)

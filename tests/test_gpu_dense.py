@@ -50,8 +50,8 @@ def test_noise_covariance_and_wiener_vs_reference(ctx, golden):
 
 
 def test_dropin_pulsar_covariance_replay(golden):
-    """The reference's call sequence of tools/gen_golden.py gen_g6 through fakepta_amd.Pulsar."""
-    from fakepta_amd import fake_pta as fp
+    """The reference's call sequence of tools/gen_golden.py gen_g6 through fakepta.fake_pta.Pulsar."""
+    from fakepta import fake_pta as fp
     g = golden("g6_dense_cov.npz")
     rng = np.random.default_rng(17)
     yr = 365.25 * 24 * 3600

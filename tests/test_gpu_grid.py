@@ -2,10 +2,12 @@
 
 The gridded path evaluates the same Fourier sums as the direct kernels through an oversampled
 phase grid (real DFT) and a banded exponential-of-semicircle interpolation.
-It is an approximation with a bounded aliasing error: at the defaults (width 13, oversampling 2)
-the error is ~1e-12 relative for a FLAT spectrum (every mode weighs equally, the worst case)
-and smaller for red spectra. Tolerance: the suite's 1e-10; the accuracy tests
-below also check the tighter bound GRID_TOL the defaults are designed for.
+It is an approximation with a bounded aliasing error: at the shipped defaults (width 16,
+oversampling 1.5; a-priori bound exp(-pi w sqrt(1 - 1/sigma)) = 2.5e-13) the error is <= ~4e-12
+relative for a FLAT spectrum (every mode weighs equally, the worst case) and smaller for red
+spectra (width 14 reached 3.2e-11 on these cases: profiles/r02_gputest1.log). Tolerance: the suite's 1e-10; the accuracy tests below also check the
+tighter bound GRID_TOL the defaults are designed for, AT the shipped defaults (the fixture restores
+the context's own options after every test instead of writing fixed values).
 """
 import numpy as np
 import pytest
@@ -33,17 +35,26 @@ def ctx(capi):
     c.close()
 
 
+SHIPPED_WIDTH, SHIPPED_SIGMA100 = 16, 150  # capi.hip fpta_ctx defaults
+
+
+@pytest.fixture(scope="module")
+def shipped(ctx, capi):
+    """The options of a fresh context: the shipped defaults every test must run at unless it says otherwise."""
+    opts = ctx.options()
+    assert opts[capi.OPT_GRID_WIDTH] == SHIPPED_WIDTH and opts[capi.OPT_GRID_SIGMA] == SHIPPED_SIGMA100
+    return opts
+
+
 @pytest.fixture(params=[3, 0, 1, 2], ids=["mfma", "valu", "dft_mfma", "interp_mfma"])
-def gridded(ctx, capi, request):
-    """Gridded path with the DFT / interpolation on fp64 MFMA (mask bits 0 / 1) or the fp64 VALU."""
+def gridded(ctx, capi, shipped, request):
+    """Gridded path with the DFT on fp64 MFMA or VALU (mask bit 0) and the interpolation as the dense-band
+    MFMA kernel or the sparse VALU kernel (bit 1); the context's options are restored to the shipped
+    snapshot afterwards."""
     ctx.set_option(capi.OPT_SYNTH_PATH, 4)
     ctx.set_option(capi.OPT_GRID_MFMA, request.param)
     yield ctx
-    ctx.set_option(capi.OPT_GRID_MFMA, 3)
-    ctx.set_option(capi.OPT_SYNTH_PATH, 0)
-    ctx.set_option(capi.OPT_GRID_WIDTH, 13)
-    ctx.set_option(capi.OPT_GRID_SIGMA, 200)
-    ctx.set_option(capi.OPT_FUSE_WHITE, 1)
+    ctx.set_options(shipped)
 
 
 def _flat_layout(ctx, rng, P=4, n_range=(100, 300), n_modes=100, idx=2.0, t0=4.5e9):
@@ -57,8 +68,11 @@ def _flat_layout(ctx, rng, P=4, n_range=(100, 300), n_modes=100, idx=2.0, t0=4.5
 
 
 @pytest.mark.parametrize("n_modes", [1, 30, 100, 257])
-def test_flat_spectrum_real_epochs(gridded, n_modes):
-    """Worst case for the aliasing error: flat spectrum, real-MJD-like epochs (t ~ 5e9 s)."""
+def test_flat_spectrum_real_epochs(gridded, capi, n_modes):
+    """Worst case for the aliasing error: flat spectrum, real-MJD-like epochs (t ~ 5e9 s), at the shipped
+    width / oversampling."""
+    assert gridded.get_option(capi.OPT_GRID_WIDTH) == SHIPPED_WIDTH
+    assert gridded.get_option(capi.OPT_GRID_SIGMA) == SHIPPED_SIGMA100
     rng = np.random.default_rng(n_modes)
     offs, toas, nu, segs = _flat_layout(gridded, rng, n_modes=n_modes)
     got = gridded.batch_synth(5, 0, 64)
@@ -80,6 +94,35 @@ def test_width_and_oversampling_options(gridded, capi):
     fine = rel_err(gridded.batch_synth(8, 0, 32), want)
     assert 1e-9 < coarse < 1e-3
     assert fine <= GRID_TOL
+
+
+def test_auto_path_respects_error_bound(ctx, capi, shipped):
+    """Auto selection (path 0) takes the gridded path at the shipped defaults, refuses it (and says why) when
+    the width / oversampling pair's a-priori bound exceeds 2e-11, and reports the bound in grid_info."""
+    rng = np.random.default_rng(4)
+    # 2000-TOA pulsars: the gridded plan needs well under half the direct FMAs (auto's cost rule)
+    offs, toas, nu = random_layout(rng, 4, (2000, 2000), ragged=False)
+    ctx.batch_set_toas(offs, toas, nu)
+    f, a = per_psr_signal(rng, offs, toas, 30)
+    ctx.batch_add_signal(0, f, a, idx=2.0)
+    segs = [O.Segment(0, 2 * np.pi * f, a, 2.0)]
+    try:
+        ctx.batch_synth(3, 0, 64, to_host=False)
+        gi = ctx.batch_grid_info()
+        assert gi["last_path"] == 4 and gi["path_reason"] == "", gi
+        assert gi["width"] == SHIPPED_WIDTH
+        assert abs(gi["err_bound"] - np.exp(-np.pi * SHIPPED_WIDTH * np.sqrt(1 / 3))) < 1e-15
+        ctx.set_option(capi.OPT_GRID_WIDTH, 8)
+        got = ctx.batch_synth(3, 0, 64)
+        gi = ctx.batch_grid_info()
+        assert gi["last_path"] == 3 and "error bound" in gi["path_reason"]
+        assert_parity(got, O.batch_synth(offs, toas, nu, segs, 3, 0, 64), TOL)
+        ctx.set_options(shipped)
+        ctx.batch_synth(3, 0, 8, to_host=False)  # below FPTA_OPT_MFMA_MIN_REAL: direct
+        gi = ctx.batch_grid_info()
+        assert gi["last_path"] == 1 and "n_real" in gi["path_reason"]
+    finally:
+        ctx.set_options(shipped)
 
 
 def test_unsorted_and_clustered_toas(gridded):
@@ -161,8 +204,8 @@ def test_c2_full_size_gridded_vs_seeded(ctx, capi):
     """BASELINE configs[1] (100 psr x 2000 TOAs, RN30 + DM100 + HD30, R = 1024): the gridded path and
     the exact seeded VALU path agree over the whole block (size-independent cross-check of two
     different algorithms on the same device coefficients)."""
-    from fakepta_amd import correlated_noises as cn
-    from fakepta_amd import fake_pta as fp
+    from fakepta import correlated_noises as cn
+    from fakepta import fake_pta as fp
     from fakepta_amd.batch import BatchSimulator
     np.random.seed(0)
     psrs = fp.make_fake_array(npsrs=100, Tobs=10, ntoas=2000, gaps=False, isotropic=True, toaerr=1e-7,

@@ -63,8 +63,8 @@ def test_gp_accumulate_vs_reference(ctx, golden, lab):
 
 
 def test_dropin_single_pulsar_replay(golden):
-    """The reference's own call sequence (tools/gen_golden.py gen_g2) through fakepta_amd."""
-    from fakepta_amd import fake_pta as fp
+    """The reference's own call sequence (tools/gen_golden.py gen_g2) through the fakepta drop-in."""
+    from fakepta import fake_pta as fp
     g = golden("g2_single_psr.npz")
     rng = np.random.default_rng(7)
     yr = 365.25 * 24 * 3600
@@ -100,8 +100,8 @@ def test_dropin_single_pulsar_replay(golden):
 
 @pytest.mark.parametrize("orf", ["hd", "monopole", "dipole", "curn"])
 def test_dropin_common_vs_reference(golden, orf):
-    from fakepta_amd import correlated_noises as cn
-    from fakepta_amd import fake_pta as fp
+    from fakepta import correlated_noises as cn
+    from fakepta import fake_pta as fp
     g = golden("g3_common.npz")
     np.random.seed(5)
     psrs = fp.make_fake_array(npsrs=25, Tobs=None, ntoas=120, gaps=True, toaerr=1e-7, isotropic=True,
@@ -122,13 +122,77 @@ def test_dropin_common_vs_reference(golden, orf):
     assert_parity(np.concatenate([p.residuals for p in psrs]), g[f"{orf}_residuals"], TOL)
     assert_parity(np.concatenate([p.reconstruct_signal(["gw_common"]) for p in psrs]), g[f"{orf}_reconstruct"],
                   TOL)
+    # the one-launch array reconstruct against the reference's own per-pulsar reconstruct_signal
+    assert_parity(np.concatenate(fp.reconstruct_array(psrs, ["gw_common"])), g[f"{orf}_reconstruct"], TOL)
+
+
+def test_user_orf_matrix_dropin(golden):
+    """orf= an ORF matrix (this package accepts any PSD matrix; the reference's string ORFs are the
+    named cases): passing the reference's own Hellings-Downs matrix reproduces its orf='hd' injection
+    (same draws, same SVD factor), and BatchSimulator on that array equals the named-ORF array bit for bit."""
+    from fakepta import correlated_noises as cn
+    from fakepta import fake_pta as fp
+    from fakepta_amd.batch import BatchSimulator
+    g = golden("g3_common.npz")
+    np.random.seed(5)
+    psrs = fp.make_fake_array(npsrs=25, Tobs=None, ntoas=120, gaps=True, toaerr=1e-7, isotropic=True,
+                              backends=["A.1400", "B.800"], custom_model={"RN": None, "DM": None, "Sv": None})
+    for p in psrs:
+        p.make_ideal()
+    cn.add_common_correlated_noise(psrs, orf=np.array(g["hd_orf"]), spectrum="powerlaw", name="gw", idx=0,
+                                   components=30, log10_A=-14.2, gamma=13 / 3)
+    assert_parity(np.concatenate([p.residuals for p in psrs]), g["hd_residuals"], TOL)
+    fourier = np.array([p.signal_model["gw_common"]["fourier"] for p in psrs])
+    np.testing.assert_allclose(fourier, g["hd_fourier"], rtol=1e-10, atol=1e-10 * np.abs(fourier).max())
+    user = BatchSimulator(psrs, white=False).synth(40, seed=3)
+    for p in psrs:
+        p.signal_model["gw_common"]["orf"] = "hd"
+    named = BatchSimulator(psrs, white=False).synth(40, seed=3)
+    np.testing.assert_array_equal(user, named)
+    seg = oracle_segments(BatchSimulator(psrs, white=False))
+    offs = np.concatenate([[0], np.cumsum([len(p.toas) for p in psrs])])
+    want = O.batch_synth(offs, np.concatenate([p.toas for p in psrs]), np.concatenate([p.freqs for p in psrs]),
+                         seg, 3, 0, 40)
+    assert_parity(user, want, TOL)
+
+
+def test_reference_pickle_session_continues(golden):
+    """Pulsars pickled by the reference (fixture g7, class path fakepta.fake_pta.Pulsar) load into the drop-in
+    and the session continues as in the reference: reconstruct_signal() of every signal, then a seeded
+    replace-on-reinject of the red noise and a second common-signal injection."""
+    import os
+    import pickle
+    from fakepta import correlated_noises as cn
+    from tests.conftest import GOLDEN
+    g = golden("g7_ref_pulsars.npz")
+    with open(os.path.join(GOLDEN, "g7_ref_pulsars.pkl"), "rb") as fh:
+        psrs = pickle.load(fh)
+    for i, p in enumerate(psrs):
+        assert_parity(p.reconstruct_signal(), g[f"reconstruct_all_{i}"], 1e-12)
+    np.random.seed(32)
+    for p in psrs:
+        p.add_red_noise(spectrum="powerlaw", log10_A=-13.5, gamma=3.5)
+    cn.add_common_correlated_noise(psrs, orf="hd", components=15, log10_A=-14.0, gamma=4.0)
+    for i, p in enumerate(psrs):
+        np.testing.assert_allclose(p.signal_model["red_noise"]["fourier"], g[f"rn_fourier_after_{i}"], rtol=1e-15)
+        assert_parity(p.residuals, g[f"residuals_after_{i}"], 1e-11)
+
+
+def test_reference_script_imports_reproduce_g4(golden):
+    """examples/make_fake_array.py's own import line and call, BASELINE configs[0] (G4)."""
+    from fakepta.fake_pta import make_fake_array
+    g = golden("g4_make_fake_array.npz")
+    np.random.seed(0)
+    psrs = make_fake_array(npsrs=25, Tobs=10, ntoas=1000, isotropic=True, gaps=True, toaerr=1e-7,
+                           backends="NUPPI.1400", custom_model={"RN": 30, "DM": None, "Sv": None})
+    assert_parity(np.concatenate([p.residuals for p in psrs]), g["residuals"], TOL)
 
 
 def test_reconstruct_array_and_common_reinject():
     """One-launch array reconstruct == per-pulsar reconstruct_signal; re-injecting a common signal
     replaces it (correlated_noises.py:133-134)."""
-    from fakepta_amd import correlated_noises as cn
-    from fakepta_amd import fake_pta as fp
+    from fakepta import correlated_noises as cn
+    from fakepta import fake_pta as fp
     np.random.seed(12)
     psrs = fp.make_fake_array(npsrs=9, Tobs=None, ntoas=80, gaps=True, toaerr=1e-7, isotropic=False,
                               backends=["A.1400", "B.800"], custom_model={"RN": 20, "DM": 35, "Sv": None})
@@ -159,7 +223,7 @@ def test_reconstruct_array_and_common_reinject():
 ])
 def test_make_fake_array_end_to_end(golden, fixture, kwargs):
     """BASELINE configs[0]: seeded make_fake_array reproduces the reference's residuals."""
-    from fakepta_amd import fake_pta as fp
+    from fakepta import fake_pta as fp
     g = golden(fixture)
     kwargs = dict(kwargs)
     np.random.seed(kwargs.pop("seed"))
@@ -190,7 +254,7 @@ def test_white_ecorr_dropin(ctx):
 
 def test_masked_system_noise(ctx):
     """Backend mask (fake_pta.py:361-368, D9 fixed) and add_system_noise (D3 fixed)."""
-    from fakepta_amd import fake_pta as fp
+    from fakepta import fake_pta as fp
     np.random.seed(4)
     psr = fp.Pulsar(np.linspace(0, 3e8, 200), 1e-7, 0.3, 0.4, backends=["A.1400", "B.800"],
                     custom_model={"RN": None, "DM": None, "Sv": None})
@@ -253,6 +317,7 @@ def test_batch_vs_oracle(ctx, capi, path, variant, case):
               ecorr_only=dict(ecorr=True, per_psr=((12, 0.0),), common=()), common_only=dict(per_psr=(), common=((30, 0.0), (13, 2.0))),
               tiny_pulsars=dict(P=5, n_range=(1, 18)))[case]
     offs, toas, nu, segs, sigma, block_of, es = _build(ctx, rng, **kw)
+    shipped = ctx.options()
     ctx.set_option(capi.OPT_SYNTH_PATH, path)
     ctx.set_option(capi.OPT_VALU_VARIANT, variant)
     try:
@@ -262,8 +327,32 @@ def test_batch_vs_oracle(ctx, capi, path, variant, case):
                                  ecorr_sigma=es)
             assert_parity(got, want, TOL)
     finally:
-        ctx.set_option(capi.OPT_SYNTH_PATH, 0)
-        ctx.set_option(capi.OPT_VALU_VARIANT, 0)
+        ctx.set_options(shipped)
+
+
+def test_variant_switches_write_every_sample(ctx, capi):
+    """Regression for DESIGN.md §10 (the tile table of one kernel must never drive another): replay the
+    synthesis sweep's order (MFMA, then every VALU and seeded-VALU variant, then the gridded path, at one
+    fixed n_real) with the device block poisoned with NaN before every launch, so a kernel that skips part
+    of the block, or reuses a stale tile table, fails here instead of being masked by the previous output."""
+    rng = np.random.default_rng(44)
+    offs, toas, nu, segs, *_ = _build(ctx, rng, P=6, n_range=(150, 700))
+    want = O.batch_synth(offs, toas, nu, segs, 1234, 0, 256)
+    shipped = ctx.options()
+    order = [(2, 0)] + [(3, v) for v in range(6)] + [(2, 0), (4, 0), (1, 0), (3, 4)]
+    try:
+        ctx.batch_synth(1234, 0, 256, to_host=False)
+        for path, variant in order:
+            for anchor in ((0, 1) if path == 3 else (0,)):  # anchor 1: the sincos VALU kernel's own tiles
+                ctx.set_option(capi.OPT_SYNTH_PATH, path)
+                ctx.set_option(capi.OPT_VALU_VARIANT, variant)
+                ctx.set_option(capi.OPT_ANCHOR, anchor)
+                ctx.debug_fill_out(np.nan)
+                got = ctx.batch_synth(1234, 0, 256)
+                assert np.all(np.isfinite(got)), (path, variant, anchor)
+                assert_parity(got, want, TOL)
+    finally:
+        ctx.set_options(shipped)
 
 
 def test_batch_from_z_vs_oracle(ctx):
@@ -374,8 +463,8 @@ def test_c2_full_size(ctx):
     """BASELINE configs[1] shape: 100 psr x 2000 TOAs, RN30 + DM100 + HD30, R = 1024 on device.
     Size-independent checks: 4 realizations re-synthesized by the oracle from the device's own
     coefficients; determinism; per-realization checksums."""
-    from fakepta_amd import correlated_noises as cn
-    from fakepta_amd import fake_pta as fp
+    from fakepta import correlated_noises as cn
+    from fakepta import fake_pta as fp
     from fakepta_amd.batch import BatchSimulator
     np.random.seed(0)
     psrs = fp.make_fake_array(npsrs=100, Tobs=10, ntoas=2000, gaps=False, isotropic=True, toaerr=1e-7,

@@ -106,8 +106,8 @@ def test_device_correlations_match_numpy(ctx):
 
 def test_hd_curve_on_device():
     """BatchSimulator.hd_curve recovers Hellings-Downs from on-device statistics."""
-    from fakepta_amd import correlated_noises as cn
-    from fakepta_amd import fake_pta as fp
+    from fakepta import correlated_noises as cn
+    from fakepta import fake_pta as fp
     from fakepta_amd.batch import BatchSimulator
     np.random.seed(2)
     psrs = fp.make_fake_array(npsrs=50, Tobs=10, ntoas=300, gaps=False, isotropic=True, toaerr=1e-7,
@@ -115,6 +115,11 @@ def test_hd_curve_on_device():
     cn.add_common_correlated_noise(psrs, orf="hd", log10_A=-14, gamma=13 / 3, components=30)
     sim = BatchSimulator(psrs, white=False)
     sim.synth(2048, seed=11, to_host=False)
+    import warnings
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")  # empty bins must not warn
+        mean, std, centres, counts = sim.hd_curve(bins=40, return_counts=True)
+    assert np.array_equal(np.isnan(mean), counts == 0) and counts.sum() == 50 * 49 // 2
     mean, std, centres = sim.hd_curve(bins=8)
     pos = np.array([p.pos for p in psrs])
     gam = O.orf_hd(pos)

@@ -3,9 +3,9 @@ nothing here launches a kernel)."""
 import numpy as np
 import pytest
 
-from fakepta_amd import correlated_noises as cn
-from fakepta_amd import fake_pta as fp
-from fakepta_amd import spectrum as sp
+from fakepta import correlated_noises as cn
+from fakepta import fake_pta as fp
+from fakepta import spectrum as sp
 from tests.conftest import assert_parity
 
 
@@ -116,3 +116,37 @@ def test_noisedict_conventions():
     p.init_noisedict({"efac": 1.5, "log10_tnequad": -6.5})
     assert p.noisedict == {"J0000+0000_A_efac": 1.5, "J0000+0000_A_log10_tnequad": -6.5,
                            "J0000+0000_B_efac": 1.5, "J0000+0000_B_log10_tnequad": -6.5}
+
+
+def test_reference_pickles_load_into_the_dropin():
+    """Pulsar objects pickled by the reference itself (class path fakepta.fake_pta.Pulsar, as
+    examples/make_fake_array.py:65 saves an array; fixture g7 written by tools/gen_golden.py) unpickle
+    into this package's Pulsar with the reference's state, and this package's pickles record the same
+    class path. The pickle is our own fixture file (written by the generator), not a reference artefact."""
+    import os
+    import pickle
+    from tests.conftest import GOLDEN
+    g = np.load(os.path.join(GOLDEN, "g7_ref_pulsars.npz"))
+    with open(os.path.join(GOLDEN, "g7_ref_pulsars.pkl"), "rb") as fh:
+        psrs = pickle.load(fh)
+    assert len(psrs) == 4 and all(type(p) is fp.Pulsar for p in psrs)
+    for i, p in enumerate(psrs):
+        np.testing.assert_array_equal(p.residuals, g[f"residuals_{i}"])
+        assert set(p.signal_model) == {"red_noise", "dm_gp", "gw_common"}
+        assert p.signal_model["gw_common"]["orf"] == "hd"
+    assert pickle.loads(pickle.dumps(psrs[0])).name == psrs[0].name
+    assert b"fakepta.fake_pta" in pickle.dumps(psrs[0]) and b"fakepta_amd" not in pickle.dumps(psrs[0])
+
+
+def test_reference_import_paths():
+    """The reference's own import lines resolve (examples/make_fake_array.py:1,6, README.md:15)."""
+    import importlib
+    for mod, names in (("fakepta.fake_pta", ("Pulsar", "make_fake_array", "copy_array", "spec", "spec_params")),
+                       ("fakepta.correlated_noises", ("add_common_correlated_noise", "hd", "monopole", "dipole",
+                                                      "curn", "anisotropic", "get_correlations", "bin_curve")),
+                       ("fakepta.spectrum", ("powerlaw", "turnover", "t_process", "t_process_adapt",
+                                             "turnover_knee", "broken_powerlaw")),
+                       ("fakepta.constants", ("fyr", "yr"))):
+        m = importlib.import_module(mod)
+        for n in names:
+            assert hasattr(m, n), (mod, n)

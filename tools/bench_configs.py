@@ -44,7 +44,7 @@ def timed(ctx, capi, fn, steps, warmup=2):
 
 
 def c1():
-    from fakepta_amd import fake_pta as fp
+    from fakepta import fake_pta as fp
     kw = dict(npsrs=25, Tobs=10, ntoas=1000, isotropic=True, gaps=True, toaerr=1e-7, backends="NUPPI.1400",
               custom_model={"RN": 30, "DM": None, "Sv": None})
     np.random.seed(0)
@@ -71,7 +71,7 @@ def fib(P):
 def c3(total):
     import bench
     from fakepta_amd import _capi
-    from fakepta_amd import correlated_noises as cn
+    from fakepta import correlated_noises as cn
     from fakepta_amd.batch import BatchSimulator
     ctx = _capi.Context(0)
     psrs = bench.build_c2(100, 2000)
@@ -103,11 +103,11 @@ def c4():
     offs = (np.arange(P + 1) * n_p).astype(np.int64)
     toas = (np.linspace(0, T, n_p)[None, :] + rng.uniform(0, 86400, (P, 1))).ravel()
     nu = np.abs(1400.0 + rng.normal(0, 10, P * n_p))
-    from fakepta_amd.correlated_noises import orf_factor
+    from fakepta.correlated_noises import orf_factor
     class _P:  # noqa: E306
         def __init__(self, p):
             self.pos = p
-    from fakepta_amd.correlated_noises import hd
+    from fakepta.correlated_noises import hd
     L = orf_factor(hd([_P(x) for x in fib(P)]))
     f = np.arange(1, N + 1) / np.ptp(toas)
     amp = np.sqrt(O.powerlaw(f, -15.0, 13 / 3) * O.delta_f(f))
@@ -123,8 +123,8 @@ def c4():
 
 def c5():
     from fakepta_amd import _capi
-    from fakepta_amd import correlated_noises as cn
-    from fakepta_amd import fake_pta as fp
+    from fakepta import correlated_noises as cn
+    from fakepta import fake_pta as fp
     from fakepta_amd.batch import BatchSimulator
     ctx = _capi.Context(0)
     P = 100

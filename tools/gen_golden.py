@@ -21,6 +21,9 @@ Fixture map:
   g5_tutorial.json    known answers printed in examples/tutorial.ipynb
   g6_dense_cov.npz    one 2-backend pulsar: make_time_correlated_noise_cov per GP,
                       make_noise_covariance_matrix, draw_noise_model(residuals) (Wiener)
+  g7_ref_pulsars.pkl  4 Pulsar objects pickled by the reference (class fakepta.fake_pta.Pulsar)
+  g7_ref_pulsars.npz  the reference's reconstruct_signal() on them, then its residuals after
+                      np.random.seed(32) + add_red_noise (replace) + add_common_correlated_noise
 """
 import json
 import os
@@ -274,6 +277,32 @@ def gen_g6(fp):
     np.savez_compressed(os.path.join(OUT, "g6_dense_cov.npz"), **d)
 
 
+def gen_g7(fp, cn):
+    """Pulsar objects pickled by the reference itself (class path fakepta.fake_pta.Pulsar, the way
+    examples/make_fake_array.py:65 saves an array) and what the reference computes on them afterwards:
+    the drop-in must unpickle them and continue the session with the same results."""
+    import pickle
+    np.random.seed(31)
+    psrs = fp.make_fake_array(npsrs=4, Tobs=5, ntoas=150, gaps=True, toaerr=1e-7, isotropic=True,
+                              backends=["A.1400", "B.800"], custom_model={"RN": 20, "DM": 25, "Sv": None})
+    cn.add_common_correlated_noise(psrs, orf="hd", components=15, log10_A=-14.3, gamma=13 / 3)
+    assert type(psrs[0]).__module__ == "fakepta.fake_pta"
+    with open(os.path.join(OUT, "g7_ref_pulsars.pkl"), "wb") as fh:
+        pickle.dump(psrs, fh, protocol=4)
+    d = {}
+    for i, p in enumerate(psrs):
+        d[f"residuals_{i}"] = p.residuals.copy()
+        d[f"reconstruct_all_{i}"] = p.reconstruct_signal()
+    np.random.seed(32)
+    for p in psrs:
+        p.add_red_noise(spectrum="powerlaw", log10_A=-13.5, gamma=3.5)  # replace-on-reinject
+    cn.add_common_correlated_noise(psrs, orf="hd", components=15, log10_A=-14.0, gamma=4.0)
+    for i, p in enumerate(psrs):
+        d[f"residuals_after_{i}"] = p.residuals.copy()
+        d[f"rn_fourier_after_{i}"] = p.signal_model["red_noise"]["fourier"].copy()
+    np.savez_compressed(os.path.join(OUT, "g7_ref_pulsars.npz"), **d)
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
     fp, cn, sp = ref_shim.load_reference()
@@ -283,6 +312,7 @@ def main():
     gen_g4(fp)
     gen_g5()
     gen_g6(fp)
+    gen_g7(fp, cn)
     for fn in sorted(os.listdir(OUT)):
         print(fn, os.path.getsize(os.path.join(OUT, fn)))
 
