@@ -182,7 +182,7 @@ __device__ __forceinline__ void interp_tile(const SynthArgs& a, const int4* __re
       load(min(q + 1, nq - 1), a1, b1);
       mfma(a0, b0);
       load(min(q + 2, nq - 1), a0, b0);
-      mfma(a1, q + 1 < nq ? b1 : 0.0);  // odd step count: the re-read last step weighs 0 (no branch)
+      if (q + 1 < nq) mfma(a1, b1);  // odd step count: skip the re-read last step (wave-uniform branch)
     }
   }
 
