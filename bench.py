@@ -35,7 +35,7 @@ FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 matrix (= vector) peak, AMD datasheet (M
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 SYNTH_KERNELS = {3: ("k_synth_valu_seeded<2,16>", "fp64-valu"), 2: ("k_synth_mfma<4,2>", "fp64-mfma"),
                  1: ("k_synth_direct", "fp64-valu")}
-GRID_INTERP = {True: ("k_grid_interp_mfma<8>", "fp64-mfma"), False: ("k_grid_interp_sparse<{w}>", "fp64-valu")}
+GRID_INTERP = ("k_grid_interp_mfma<8>", "fp64-mfma")
 GRID_DFT = {True: "k_grid_dft_mfma<2,2>", False: "k_grid_dft<8>"}
 
 
@@ -297,7 +297,7 @@ def main():
     n_launch_real = R if args.config == "c2" else n_job / max(1, -(-shard_bounds(n_job, 0, world)[1] // R))
     out_bytes = 8.0 * info["n_toa"] * n_launch_real
     if path == 4:
-        kernel, pipe = GRID_INTERP[bool(gi["grid_mfma"] & 2) or gi["width"] > 16]
+        kernel, pipe = GRID_INTERP
         kernel = kernel.format(w=gi["width"])
         traffic, traffic_src = pmc_traffic(kernel, info, R, args.traffic)
         achieved = out_bytes / synth_avg_s / 1e9

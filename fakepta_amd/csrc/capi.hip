@@ -62,8 +62,6 @@ struct Seg {
 struct GridSeg {
   int32_t nf = 0, half = 0, lde = 0, rmax = 0, ntab = 0;
   DevBuf ecos, esin, wd, js, g;
-  DevBuf rec, base;  // k_grid_interp_sparse: window-slot weight records [n_toa][kSparseRec], chunk base rows
-  int32_t ws = 0;    // k_grid_interp_sparse window rows (w + largest first-row offset)
 };
 
 // Gridded-synthesis plan of a layout (built once per layout, reused by every batch).
@@ -75,8 +73,6 @@ struct GridPlan {
   double sigma = 0.0;        // oversampling
   int32_t n_chunks = 0;
   DevBuf chunks;             // int4 {pulsar, first TOA (pulsar-local), count, 0}
-  int32_t n_work = 0;
-  DevBuf work;               // k_grid_interp_sparse work items: int4 {first chunk, chunks, pulsar, 0}
   std::vector<GridSeg*> segs;
   double fma_grid = 0.0;     // FMAs per realization: DFT + interpolation
   double fma_dft = 0.0;      // FMAs per realization in k_grid_dft
@@ -92,7 +88,6 @@ struct GridPlan {
     segs.clear();
     built = ok = false;
     n_chunks = 0;
-    n_work = 0;
     g_rpad = 0;
     // the plan figures accumulate over signals in grid_build: a rebuilt plan must start from zero
     fma_grid = fma_dft = fma_interp = grid_vals = weight_bytes = fma_direct = 0.0;
@@ -162,10 +157,10 @@ struct fpta_ctx {
   // and 3.6e-12 (257 modes) relative (the numpy model of oracle.grid_synth and the GPU agree); the earlier
   // w = 14 reached 3.2e-11 there (profiles/r02_gputest1.log). sigma = 1.5 keeps the grid (DFT) a quarter
   // smaller than sigma = 2 (tools/sweep_grid.py --params, profiles/r01_sweep_wsig.txt)
-  int grid_w = 16;       // gridded path: kernel width in grid cells
+  int grid_w = 15;       // gridded path: kernel width in grid cells
   int grid_sigma100 = 150;  // gridded path: oversampling x 100
-  int grid_mfma = 1;     // gridded path: bit 0 k_grid_dft_mfma (else k_grid_dft), bit 1 k_grid_interp_mfma (else
-                         // k_grid_interp_sparse, widths 12..16)
+  int grid_mfma = 1;     // gridded path: bit 0 k_grid_dft_mfma (else k_grid_dft); the interpolation is always
+                         // k_grid_interp_mfma
   // profiling
   struct Pending {
     int which;
@@ -555,14 +550,12 @@ int grid_build(fpta_ctx* c, Layout& L) {
       for (int32_t s = 0; s < n_seg; ++s) lo[s] = hi[s] = J[s][t];
       ++t;
       // chunks end on multiples of kGridTT in the global TOA index: every full chunk then writes whole
-      // 128-byte lines of each realization row. Every signal's first rows span at most kSparseD cells over
-      // the chunk (the register window of k_grid_interp_sparse; the MFMA band is then <= w + kSparseD rows)
+      // 256-byte runs of each realization row
       const int64_t t_lim = std::min(t_end, (t0 / kGridTT + 1) * kGridTT);
       while (t < t_lim) {
         bool fits = true;
         for (int32_t s = 0; s < n_seg && fits; ++s)
-          fits = std::max(hi[s], J[s][t]) - std::min(lo[s], J[s][t]) <= kSparseD &&
-                 std::max(hi[s], J[s][t]) - std::min(lo[s], J[s][t]) + w + 1 <= kGridRowCap;
+          fits = std::max(hi[s], J[s][t]) - std::min(lo[s], J[s][t]) + w + 1 <= kGridRowCap;
         if (!fits) break;
         for (int32_t s = 0; s < n_seg; ++s) {
           lo[s] = std::min(lo[s], J[s][t]);
@@ -578,7 +571,7 @@ int grid_build(fpta_ctx* c, Layout& L) {
       }
       for (int32_t s = 0; s < n_seg; ++s) {
         int32_t rows = (int32_t)(hi[s] - lo[s]) + w;
-        rows = (rows + 3) & ~3;  // k_grid_interp_mfma: 4 rows per MFMA; k_grid_interp: pairs (pad rows weigh 0)
+        rows = (rows + 3) & ~3;  // k_grid_interp_mfma: 4 rows per MFMA step (pad rows weigh 0)
         const int64_t m = ((lo[s] % nf[s]) + nf[s]) % nf[s];
         js[s].push_back(make_int2((int)m, rows));
         rmax[s] = std::max(rmax[s], rows);
@@ -591,19 +584,8 @@ int grid_build(fpta_ctx* c, Layout& L) {
     return FPTA_OK;
   }
   G.n_chunks = (int32_t)chunks.size();
-  // sparse-kernel work items: <= kSparseChunks consecutive chunks of one pulsar
-  std::vector<int4> work;
-  for (int32_t ci = 0; ci < G.n_chunks;) {
-    const int32_t p = chunks[ci].x;
-    int32_t n = 1;
-    while (n < kSparseChunks && ci + n < G.n_chunks && chunks[ci + n].x == p) ++n;
-    work.push_back(make_int4(ci, n, p, 0));
-    ci += n;
-  }
-  G.n_work = (int32_t)work.size();
   int rc;
   if ((rc = upload(c, G.chunks, chunks.data(), sizeof(int4) * chunks.size(), "grid chunks"))) return rc;
-  if ((rc = upload(c, G.work, work.data(), sizeof(int4) * work.size(), "grid work items"))) return rc;
   DevBuf d_chunk_of, d_tt_of, d_row, d_d;
   if ((rc = upload(c, d_chunk_of, chunk_of.data(), sizeof(int32_t) * N, "grid chunk_of")) ||
       (rc = upload(c, d_tt_of, tt_of.data(), sizeof(int32_t) * N, "grid tt_of")))
@@ -644,28 +626,6 @@ int grid_build(fpta_ctx* c, Layout& L) {
     if ((rc = upload(c, d_row, row.data(), sizeof(int32_t) * N, "grid rows")) ||
         (rc = upload(c, d_d, D[s].data(), sizeof(double) * N, "grid offsets")))
       return rc;
-    // k_grid_interp_sparse tables: per chunk the base row, per TOA the record of window slots; the signal's
-    // window size w + (largest first-row offset of any TOA in its chunk)
-    {
-      std::vector<int32_t> base(G.n_chunks);
-      int32_t dmax = 0;
-      for (int32_t ci = 0; ci < G.n_chunks; ++ci) base[ci] = js[s][ci].x;
-      for (int64_t t = 0; t < N; ++t) {
-        if (row[t] < 0 || row[t] > kSparseD) return fail(c, FPTA_EINVAL, "grid plan: chunk row offset out of range");
-        dmax = std::max(dmax, row[t]);
-      }
-      gs->ws = w + dmax;
-      if ((rc = upload(c, gs->base, base.data(), sizeof(int32_t) * base.size(), "grid sparse base rows"))) return rc;
-      // one step of padding: k_grid_interp_sparse loads a whole step's records unconditionally
-      const size_t rec_bytes = sizeof(double) * kSparseRec * ((size_t)N + kGridTT);
-      HIPCHK(c, gs->rec.ensure(rec_bytes), "grid records alloc");
-      HIPCHK(c, hipMemsetAsync(gs->rec.p, 0, rec_bytes, c->stream), "grid records memset");
-      HIPCHK(c,
-             launch_grid_records(c->stream, d, N, L.nu.as<double>(), d_d.as<double>(), d_row.as<int32_t>(), w, beta,
-                                 gs->rec.as<double>()),
-             "k_grid_records launch");
-      HIPCHK(c, hipStreamSynchronize(c->stream), "grid records sync");  // base host vector
-    }
     const size_t wbytes = sizeof(double) * ((size_t)G.n_chunks * gs->rmax + 1) * kGridTT;
     HIPCHK(c, gs->wd.ensure(wbytes), "grid weights alloc");
     HIPCHK(c, hipMemsetAsync(gs->wd.p, 0, wbytes, c->stream), "grid weights memset");
@@ -721,25 +681,8 @@ int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad) {
            "k_grid_dft launch");
   }
   KTimer kt(c, FPTA_K_SYNTH);
-  // k_grid_interp_sparse writes the block (batch synthesis); accumulation into an existing block and widths
-  // beyond its window take the MFMA interpolation
-  if ((c->grid_mfma & 2) || !sparse_width_supported(G.w) || a.accumulate) {
-    HIPCHK(c, launch_grid_interp_mfma(c->stream, a, G.chunks.as<int4>(), G.n_chunks, gsegs, R_pad),
-           "k_grid_interp_mfma launch");
-  } else {
-    SparseSegs ss{};
-    ss.n = gsegs.n;
-    for (size_t s = 0; s < G.segs.size(); ++s) {
-      GridSeg* gs = G.segs[s];
-      ss.s[s].g = gs->g.as<double>();
-      ss.s[s].rec = gs->rec.as<double>();
-      ss.s[s].base = gs->base.as<int32_t>();
-      ss.s[s].nf = gs->nf;
-      ss.s[s].ws = gs->ws;
-    }
-    HIPCHK(c, launch_grid_interp_sparse(c->stream, a, G.chunks.as<int4>(), G.work.as<int4>(), G.n_work, ss, R_pad),
-           "k_grid_interp_sparse launch");
-  }
+  HIPCHK(c, launch_grid_interp_mfma(c->stream, a, G.chunks.as<int4>(), G.n_chunks, gsegs, R_pad),
+         "k_grid_interp_mfma launch");
   return FPTA_OK;
 }
 

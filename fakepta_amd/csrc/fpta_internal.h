@@ -74,7 +74,7 @@ constexpr ValuVariant kSeededVariants[] = {{1, 16}, {2, 16}, {1, 8}, {2, 8}, {1,
 static_assert(sizeof(kSeededVariants) == sizeof(kValuVariants), "one variant index selects both tables");
 
 // Gridded synthesis (grid.hip): one signal's tables as the kernels see them.
-constexpr int kGridTT = 16;  // TOAs per interpolation chunk
+constexpr int kGridTT = 32;  // TOAs per interpolation chunk (k_grid_interp_mfma: even / odd TOAs = two MFMA B-tiles)
 constexpr int kGridMI = 8;   // grid rows per wave in k_grid_dft
 struct GridSegDev {
   const double* ecos;  // [nm][lde] q_k cos(2 pi k j / nf), k = m + 1 (zero-padded columns)
@@ -91,29 +91,6 @@ struct GridSegs {
   GridSegDev s[kGridMaxSeg];
   int32_t n;
 };
-
-// VALU interpolation (grid_sparse.hip): a TOA's first band row lies at most kSparseD rows past its chunk's base
-// row, so a register window of w + D_s <= w + kSparseD rows per signal serves the whole chunk; weight records of
-// kSparseRec window slots per (signal, TOA); work items of <= kSparseChunks consecutive chunks of one pulsar.
-constexpr int kSparseD = 4;
-constexpr int kSparseRec = 20;
-constexpr int kSparseChunks = 4;
-struct SparseSegDev {
-  const double* g;        // [P][nf][R_pad] grid values of the batch (shared with GridSegDev)
-  const double* rec;      // [n_toa][kSparseRec] window-slot weight records
-  const int32_t* base;    // [n_chunks] base row of the chunk (mod nf)
-  int32_t nf;
-  int32_t ws;             // window rows of this signal: w + the largest first-row offset in any chunk
-};
-struct SparseSegs {
-  SparseSegDev s[kGridMaxSeg];
-  int32_t n;
-};
-bool sparse_width_supported(int32_t w);
-hipError_t launch_grid_records(hipStream_t st, const SegDesc& sd, int64_t n_toa, const double* nu,
-                               const double* d_of, const int32_t* off_of, int32_t w, double beta, double* rec);
-hipError_t launch_grid_interp_sparse(hipStream_t st, const SynthArgs& a, const int4* chunks, const int4* work,
-                                     int32_t n_work, const SparseSegs& ss, int32_t R_pad);
 
 hipError_t launch_grid_weights(hipStream_t st, const SegDesc& sd, int64_t n_toa, const double* nu,
                                const int32_t* chunk_of, const int32_t* tt_of, const int32_t* row_of,

@@ -3,19 +3,19 @@
 // evaluated as a type-2 non-uniform FFT factorisation F ~= W E:
 //
 //   k_grid_weights  once per layout: dense banded interpolation weights W (chromatic factor and
-//                   mask folded in) for every chunk of <= 16 consecutive TOAs of one pulsar
+//                   mask folded in) for every chunk of <= kGridTT (32) consecutive TOAs of one pulsar
 //   k_grid_dft      per batch: grid values g_j = sum_k q_k (c_k cos(k x_j) + s_k sin(k x_j)),
 //                   x_j = 2 pi j / nf, for every (pulsar, realization) - a real DFT done as a GEMM
 //                   against the shared table E (both halves of the grid from one pass: the cos and
 //                   sin partial sums give g_j and g_{nf-j})
 //   interpolation   per batch: r(t) = sum_i W[t][i] g[J_t + i] for all signals, white noise / ECORR in
-//                   the epilogue, one store per sample: k_grid_interp_sparse (grid_sparse.hip, VALU, w FMAs
-//                   per sample and signal) or k_grid_interp_mfma (grid_mfma.hip, dense 4-row MFMA steps)
+//                   the epilogue, one store per sample: k_grid_interp_mfma (grid_mfma.hip, dense 4-row band
+//                   steps on the fp64 matrix cores)
 //
 // Kernel: exponential of semicircle phi(z) = exp(beta (sqrt(1 - z^2) - 1)), |z| <= 1, width w grid
 // cells, oversampling nf >= sigma (2N + 1); q_k = (2 pi / nf) / phi_hat(k) deconvolves it.
-// Aliasing error <= ~1e-12 relative at the default w = 14, sigma = 1.5 (and at w = 13, sigma = 2;
-// tests/test_gpu_grid.py, tools/sweep_grid.py).
+// A-priori relative aliasing bound exp(-pi w sqrt(1 - 1/sigma)): 1.5e-12 at the default w = 15, sigma = 1.5
+// (measured flat-spectrum worst case ~4x the bound; tests/test_gpu_grid.py, tools/sweep_grid.py).
 // Per sample the interpolation costs sum_s rows_s FMAs (rows ~ w + cells spanned by the chunk)
 // instead of sum_s 2 N_s for the direct contraction.
 #include <hip/hip_runtime.h>

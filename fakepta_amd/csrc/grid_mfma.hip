@@ -114,22 +114,27 @@ __device__ __forceinline__ void mfma_white_pair(int64_t t, int64_t g, uint32_t k
 }
 
 // ----------------------------------------------------------------------------- k_grid_interp_mfma
-// out[r][t] = sum_s sum_i W_s[chunk][i][tt] G_s[(J_s + i) mod nf][r] for a chunk of <= 16 TOAs: per 4
-// band rows one MFMA per 16 realizations, A = grid values (realization, row), B = weights (row, TOA).
-// Realization tiles come in pairs: lane (lr, lg) loads the adjacent realizations 2 lr, 2 lr + 1 of a
-// 32-realization pair block with one 16-byte load, the .x half feeding tile 2m and the .y half tile
-// 2m + 1 (the address unit costs ~28 cycles per wave-instruction whatever its width: TA-bound, so bytes
-// per instruction are what count). D row rho of tile 2m + h is realization 32 m + 2 rho + h, so D's
-// register g of lane l holds realization 32 m + 2 (lg + 4 g) + h of TOA l & 15: the two tiles of a pair
-// hold an adjacent (even, odd) realization pair in the same lane and register (one Philox call per pair
-// for the white epilogue), and every store instruction writes 4 full 128-byte runs.
-// Tile = chunk x 64 RW realizations, wave = chunk x 16 RW; per signal the next 4-row step's operands are
-// loaded before the current step's MFMAs (two register sets, unrolled by 2).
+// out[r][t] = sum_s sum_i W_s[chunk][i][tt] G_s[(J_s + i) mod nf][r] for a chunk of <= 32 TOAs: per 4 band
+// rows, A = grid values (realization, row), B = weights (row, TOA).
+//  * The chunk's even and odd TOAs are two B-tiles (column j = TOA 2j, 2j + 1) over the same band rows, so one
+//    set of grid loads feeds both: the address unit, the busiest block of the 16-TOA version (one dbl2 grid
+//    load per 2 MFMAs), now sees one per 4. Lane (lr, lg) loads W[row lg][2 lr .. 2 lr + 1] with one 16-byte
+//    load (.x even tile, .y odd tile).
+//  * Realization tiles come in pairs: lane (lr, lg) loads the adjacent realizations 2 lr, 2 lr + 1 of a
+//    32-realization block with one 16-byte load (.x tile 2m, .y tile 2m + 1). D row rho of tile 2m + h is then
+//    realization 32 m + 2 rho + h.
+//  * D's register g of lane l holds TOA 2 (l & 15) + e of realization 32 m + 2 (lg + 4 g) + h in acc[e][2m + h]:
+//    the two TOA parities of a lane are adjacent samples of one realization row (one 16-byte store, 256-byte
+//    runs per row), and the two tiles of a realization pair sit in the same lane and register (one Philox call
+//    per pair for the white epilogue).
+// Wave tile = chunk x 16 RW realizations; per signal the next 4-row step's operands are loaded before the
+// current step's MFMAs (two register sets, unrolled by 2, the odd last step skipped by a uniform branch).
 template <bool WHITE, int RW>
 __device__ __forceinline__ void interp_tile(const SynthArgs& a, const int4* __restrict__ chunks, int32_t n_chunks,
                                             const GridSegs& gsegs, int32_t R_pad, double* __restrict__ out,
                                             int tile) {
   static_assert(RW % 2 == 0, "realization tiles come in pairs");
+  static_assert(kGridTT == 32, "two 16-TOA B-tiles per chunk");
   constexpr int NP = RW / 2;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
@@ -138,17 +143,17 @@ __device__ __forceinline__ void interp_tile(const SynthArgs& a, const int4* __re
   const int c = __builtin_amdgcn_readfirstlane(tile - rb * n_chunks);
   const int r0 = (rb * 4 + wave) * 16 * RW;
   if (r0 >= R_pad) return;
+  FPTA_DCHECK(r0 + 16 * RW <= R_pad, "k_grid_interp_mfma realization block", r0 + 16 * RW, R_pad + 1);
   const int4 ci = chunks[c];
   const int p = __builtin_amdgcn_readfirstlane(ci.x);
   const int64_t base = a.offs[p];
 
-  d4 acc[RW];
+  d4 acc[2][RW];  // [TOA parity][realization tile]
 #pragma unroll
-  for (int i = 0; i < RW; ++i) acc[i] = d4{0.0, 0.0, 0.0, 0.0};
+  for (int e = 0; e < 2; ++e)
+#pragma unroll
+    for (int i = 0; i < RW; ++i) acc[e][i] = d4{0.0, 0.0, 0.0, 0.0};
 
-  // per signal: steps of 4 band rows; the next step's operands are loaded (unconditionally: the last
-  // prefetch re-reads the final step) before the current step's MFMAs, so the wait ahead of the MFMAs
-  // counts only the older loads
   for (int si = 0; si < gsegs.n; ++si) {
     const GridSegDev& gs = gsegs.s[si];
     const int2 jr = gs.js[c];
@@ -156,25 +161,25 @@ __device__ __forceinline__ void interp_tile(const SynthArgs& a, const int4* __re
     if (nq == 0) continue;
     const int nf = gs.nf;
     const double* __restrict__ Gp = gs.g + (int64_t)p * nf * R_pad + r0 + 2 * lr;
-    const double* __restrict__ Wp = gs.wd + (int64_t)c * gs.rmax * kGridTT + lg * kGridTT + lr;
+    const double* __restrict__ Wp = gs.wd + (int64_t)c * gs.rmax * kGridTT + lg * kGridTT + 2 * lr;
     int j = __builtin_amdgcn_readfirstlane(jr.x) + lg;  // grid row of this lane's k index
     if (j >= nf) j -= nf;
-    // two operand sets alternate (unrolled by 2, no register copies that would wait on the prefetch)
-    dbl2 a0[NP], a1[NP];
-    double b0, b1;
-    auto load = [&](int qq, dbl2(&av)[NP], double& bv) {
+    dbl2 a0[NP], a1[NP], b0, b1;
+    auto load = [&](int qq, dbl2(&av)[NP], dbl2& bv) {
       int jj = j + 4 * qq;
       while (jj >= nf) jj -= nf;
       const double* __restrict__ gr = Gp + (int64_t)jj * R_pad;
 #pragma unroll
       for (int m = 0; m < NP; ++m) av[m] = *(const dbl2*)(gr + 32 * m);
-      bv = Wp[4 * kGridTT * qq];
+      bv = *(const dbl2*)(Wp + 4 * kGridTT * qq);
     };
-    auto mfma = [&](const dbl2(&av)[NP], double bv) {
+    auto mfma = [&](const dbl2(&av)[NP], const dbl2& bv) {
 #pragma unroll
       for (int m = 0; m < NP; ++m) {
-        acc[2 * m] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m].x, bv, acc[2 * m], 0, 0, 0);
-        acc[2 * m + 1] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m].y, bv, acc[2 * m + 1], 0, 0, 0);
+        acc[0][2 * m] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m].x, bv.x, acc[0][2 * m], 0, 0, 0);
+        acc[0][2 * m + 1] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m].y, bv.x, acc[0][2 * m + 1], 0, 0, 0);
+        acc[1][2 * m] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m].x, bv.y, acc[1][2 * m], 0, 0, 0);
+        acc[1][2 * m + 1] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m].y, bv.y, acc[1][2 * m + 1], 0, 0, 0);
       }
     };
     load(0, a0, b0);
@@ -187,42 +192,52 @@ __device__ __forceinline__ void interp_tile(const SynthArgs& a, const int4* __re
   }
 
   const int cnt = __builtin_amdgcn_readfirstlane(ci.z);
-  if (lr >= cnt) return;
-  const int64_t tg = base + ci.y + lr;
+  const int tt = 2 * lr;  // this lane's even TOA in the chunk; tt + 1 the odd one
+  if (tt >= cnt) return;
+  const int64_t tg = base + ci.y + tt;
   if constexpr (WHITE) {
-    const double sg = a.w_sigma ? a.w_sigma[tg] : 0.0;
-    const int ep = a.w_block_of ? a.w_block_of[tg] : -1;
-    const double e = ep >= 0 ? a.w_esig[ep] : 0.0;
 #pragma unroll
-    for (int m = 0; m < NP; ++m) {
+    for (int e = 0; e < 2; ++e) {
+      if (tt + e >= cnt) break;
+      const int64_t te = tg + e;
+      const double sg = a.w_sigma ? a.w_sigma[te] : 0.0;
+      const int ep = a.w_block_of ? a.w_block_of[te] : -1;
+      const double es = ep >= 0 ? a.w_esig[ep] : 0.0;
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int rl = r0 + 32 * m + 2 * (lg + 4 * g);  // batch index of acc[2m][g]; acc[2m + 1][g] is rl + 1
-        double x0 = acc[2 * m][g], x1 = acc[2 * m + 1][g];
-        if (a.w_sigma) {
-          const int64_t g0 = a.real0 + rl;  // parity uniform over the launch (rl even)
-          double z0, z1;
-          mfma_white_pair(tg, g0, a.k0, a.k1, z0, z1);
-          if (g0 & 1) {  // (g0, g0 + 1) straddle two pairs
-            double y0, y1;
-            mfma_white_pair(tg, g0 + 1, a.k0, a.k1, y0, y1);
-            x0 = fma(sg, z1, x0);
-            x1 = fma(sg, y0, x1);
-          } else {
-            x0 = fma(sg, z0, x0);
-            x1 = fma(sg, z1, x1);
+      for (int m = 0; m < NP; ++m) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int rl = r0 + 32 * m + 2 * (lg + 4 * g);  // batch index of acc[e][2m][g]; acc[e][2m + 1][g]: rl + 1
+          double x0 = acc[e][2 * m][g], x1 = acc[e][2 * m + 1][g];
+          if (a.w_sigma) {
+            const int64_t g0 = a.real0 + rl;  // parity uniform over the launch (rl even)
+            double z0, z1;
+            mfma_white_pair(te, g0, a.k0, a.k1, z0, z1);
+            if (g0 & 1) {  // (g0, g0 + 1) straddle two pairs
+              double y0, y1;
+              mfma_white_pair(te, g0 + 1, a.k0, a.k1, y0, y1);
+              x0 = fma(sg, z1, x0);
+              x1 = fma(sg, y0, x1);
+            } else {
+              x0 = fma(sg, z0, x0);
+              x1 = fma(sg, z1, x1);
+            }
           }
+          if (ep >= 0) {
+            if (rl < a.n_real) x0 = fma(es, a.w_zb[(int64_t)rl * a.w_nblocks + ep], x0);
+            if (rl + 1 < a.n_real) x1 = fma(es, a.w_zb[(int64_t)(rl + 1) * a.w_nblocks + ep], x1);
+          }
+          acc[e][2 * m][g] = x0;
+          acc[e][2 * m + 1][g] = x1;
         }
-        if (ep >= 0) {
-          if (rl < a.n_real) x0 = fma(e, a.w_zb[(int64_t)rl * a.w_nblocks + ep], x0);
-          if (rl + 1 < a.n_real) x1 = fma(e, a.w_zb[(int64_t)(rl + 1) * a.w_nblocks + ep], x1);
-        }
-        acc[2 * m][g] = x0;
-        acc[2 * m + 1][g] = x1;
       }
     }
   }
+  // one 16-byte store per (lane, realization) when both TOAs exist: the row offset r * ldo + tg is even
+  // whenever ldo and tg are, else the pair is stored as two 8-byte stores
   double* __restrict__ ocol = out + tg;
+  const bool pair = tt + 1 < cnt;
+  const bool vec = pair && ((((uintptr_t)ocol) | ((uintptr_t)a.ldo << 3)) & 15) == 0;
 #pragma unroll
   for (int i = 0; i < RW; ++i) {
 #pragma unroll
@@ -230,7 +245,17 @@ __device__ __forceinline__ void interp_tile(const SynthArgs& a, const int4* __re
       const int r = r0 + 32 * (i >> 1) + 2 * (lg + 4 * g) + (i & 1);
       if (r < a.n_real) {
         double* o = ocol + (int64_t)r * a.ldo;
-        *o = a.accumulate ? *o + acc[i][g] : acc[i][g];
+        double v0 = acc[0][i][g], v1 = acc[1][i][g];
+        if (a.accumulate) {
+          v0 += o[0];
+          if (pair) v1 += o[1];
+        }
+        if (vec) {
+          *(dbl2*)o = dbl2{v0, v1};
+        } else {
+          o[0] = v0;
+          if (pair) o[1] = v1;
+        }
       }
     }
   }
@@ -241,7 +266,7 @@ __device__ __forceinline__ void interp_tile(const SynthArgs& a, const int4* __re
 // overlap, so they stay in the XCD's L2). One tile per short-lived workgroup instead left the CUs mostly
 // empty (SQ_WAVE_CYCLES ~ 0.7 resident waves per SIMD): workgroup dispatch, not the memory system, paced it.
 template <bool WHITE, int RW>
-__global__ __launch_bounds__(256) void k_grid_interp_mfma(SynthArgs a, const int4* __restrict__ chunks,
+__global__ __launch_bounds__(256, 2) void k_grid_interp_mfma(SynthArgs a, const int4* __restrict__ chunks,
                                                           int32_t n_chunks, int32_t n_tiles, GridSegs gsegs,
                                                           int32_t R_pad, double* __restrict__ out) {
   const int per = (n_tiles + 7) >> 3;
@@ -254,7 +279,7 @@ __global__ __launch_bounds__(256) void k_grid_interp_mfma(SynthArgs a, const int
 
 
 constexpr int kDftMJ = 2, kDftMR = 2;  // k_grid_dft_mfma wave tile: 32 grid rows x 32 realizations
-constexpr int kInterpRW = 8;           // k_grid_interp_mfma: 128 realizations per wave
+constexpr int kInterpRW = 8;           // k_grid_interp_mfma: 32 TOAs x 128 realizations per wave
 
 hipError_t launch_grid_dft_mfma(hipStream_t st, GridSegs gsegs, int32_t P, const double* coef, int32_t K,
                                 int32_t R_pad) {

@@ -238,18 +238,16 @@ int fpta_multi_synth(fpta_multi* m, uint64_t seed, int64_t real0, int64_t n_real
 /* ------------------------------------------------------------------ tuning / profiling */
 #define FPTA_OPT_SYNTH_PATH 1     /* 0 auto, 1 direct (sincos per basis element), 2 fp64 MFMA, 3 fp64 VALU fused,
                                      4 gridded (real DFT to an oversampled phase grid + banded interpolation,
-                                     harmonic grids only; aliasing error <= ~4e-12 relative at the defaults) */
+                                     harmonic grids only; aliasing error <= ~6e-12 relative at the defaults) */
 #define FPTA_OPT_MFMA_MIN_REAL 2  /* auto: MFMA path when n_real >= this (default 16) */
 #define FPTA_OPT_PROFILE 3        /* 1: time every batch kernel with HIP events on the ctx stream */
 #define FPTA_OPT_ANCHOR 4         /* recurrence re-anchor interval in K-steps of 2 modes (0 = once per signal, default) */
 #define FPTA_OPT_VALU_VARIANT 5   /* tile variant of the VALU fused kernel (0..5) */
 #define FPTA_OPT_FUSE_WHITE 6     /* 1 (default): white/ECORR added in the synthesis epilogue; 0: separate pass */
-#define FPTA_OPT_GRID_WIDTH 7     /* gridded path: interpolation kernel width in grid cells (default 16) */
+#define FPTA_OPT_GRID_WIDTH 7     /* gridded path: interpolation kernel width in grid cells (default 15) */
 #define FPTA_OPT_GRID_SIGMA 8     /* gridded path: grid oversampling x 100 (default 150) */
-#define FPTA_OPT_GRID_MFMA 9      /* gridded path kernels on fp64 MFMA: bit 0 the DFT (else fp64 VALU), bit 1 the
-                                     interpolation as dense 4-row MFMA band steps (else the sparse fp64 VALU
-                                     kernel, w FMAs per sample and signal, widths 12..16; wider kernels always
-                                     take the MFMA interpolation). Default 1. */
+#define FPTA_OPT_GRID_MFMA 9      /* gridded path: bit 0 runs the DFT on fp64 MFMA (else fp64 VALU); the
+                                     interpolation always runs on fp64 MFMA. Default 1. */
 int fpta_set_option(fpta_ctx* ctx, int32_t key, int64_t value);
 /* Current value of option `key` (same keys as fpta_set_option). */
 int fpta_get_option(fpta_ctx* ctx, int32_t key, int64_t* value);

@@ -2,12 +2,13 @@
 
 The gridded path evaluates the same Fourier sums as the direct kernels through an oversampled
 phase grid (real DFT) and a banded exponential-of-semicircle interpolation.
-It is an approximation with a bounded aliasing error: at the shipped defaults (width 16,
-oversampling 1.5; a-priori bound exp(-pi w sqrt(1 - 1/sigma)) = 2.5e-13) the error is <= ~4e-12
+It is an approximation with a bounded aliasing error: at the shipped defaults (width 15,
+oversampling 1.5; a-priori bound exp(-pi w sqrt(1 - 1/sigma)) = 1.5e-12) the error is <= ~6e-12
 relative for a FLAT spectrum (every mode weighs equally, the worst case) and smaller for red
-spectra (width 14 reached 3.2e-11 on these cases: profiles/r02_gputest1.log). Tolerance: the suite's 1e-10; the accuracy tests below also check the
-tighter bound GRID_TOL the defaults are designed for, AT the shipped defaults (the fixture restores
-the context's own options after every test instead of writing fixed values).
+spectra (width 14 reached 3.2e-11 on these cases: profiles/r02_gputest1.log). Tolerance: the suite's
+1e-10; the accuracy tests below also check the tighter bound GRID_TOL the defaults are
+designed for, AT the shipped defaults (the fixture restores the context's own options after every test
+instead of writing fixed values).
 """
 import numpy as np
 import pytest
@@ -35,7 +36,7 @@ def ctx(capi):
     c.close()
 
 
-SHIPPED_WIDTH, SHIPPED_SIGMA100 = 16, 150  # capi.hip fpta_ctx defaults
+SHIPPED_WIDTH, SHIPPED_SIGMA100 = 15, 150  # capi.hip fpta_ctx defaults
 
 
 @pytest.fixture(scope="module")
@@ -46,11 +47,10 @@ def shipped(ctx, capi):
     return opts
 
 
-@pytest.fixture(params=[3, 0, 1, 2], ids=["mfma", "valu", "dft_mfma", "interp_mfma"])
+@pytest.fixture(params=[1, 0], ids=["dft_mfma", "dft_valu"])
 def gridded(ctx, capi, shipped, request):
-    """Gridded path with the DFT on fp64 MFMA or VALU (mask bit 0) and the interpolation as the dense-band
-    MFMA kernel or the sparse VALU kernel (bit 1); the context's options are restored to the shipped
-    snapshot afterwards."""
+    """Gridded path with the DFT on fp64 MFMA or VALU (FPTA_OPT_GRID_MFMA bit 0; the interpolation is always
+    k_grid_interp_mfma); the context's options are restored to the shipped snapshot afterwards."""
     ctx.set_option(capi.OPT_SYNTH_PATH, 4)
     ctx.set_option(capi.OPT_GRID_MFMA, request.param)
     yield ctx

@@ -2,9 +2,9 @@
 
     FAKEPTA_AMD_LIB=<lib.so> python tools/interp_diag.py [--grid-mfma M]
 
-Prints the average k_grid_interp* launch time (HIP events on the context stream) over 10 batches of 1024
-realizations. Used with the diagnostic builds of tools/interp_diag.sh (FMAs, stores or grid loads removed
-in a throwaway copy of grid_sparse.hip) to see which part paces the kernel."""
+Prints the average k_grid_interp_mfma and k_grid_dft launch times (HIP events on the context stream) over 10
+batches of 1024 realizations, and the plan figures. FAKEPTA_AMD_LIB selects a diagnostic build of the library
+(never the bench)."""
 import argparse
 import json
 import os
