@@ -58,10 +58,12 @@ struct Seg {
   DevBuf w, amp, L, mask;
 };
 
-// Gridded-synthesis tables of one signal (grid.hip): real-DFT table E, interpolation weights.
+// Gridded-synthesis tables of one signal (grid.hip): real-DFT table E; its grid block starts at row rowoff of
+// the plan's grid buffer.
 struct GridSeg {
-  int32_t nf = 0, half = 0, lde = 0, rmax = 0, ntab = 0;
-  DevBuf ecos, esin, wd, js, g;
+  int32_t nf = 0, half = 0, lde = 0, ntab = 0;
+  int64_t rowoff = 0;
+  DevBuf ecos, esin;
 };
 
 // Gridded-synthesis plan of a layout (built once per layout, reused by every batch).
@@ -72,7 +74,12 @@ struct GridPlan {
   int32_t w = 0;             // kernel width (grid cells)
   double sigma = 0.0;        // oversampling
   int32_t n_chunks = 0;
-  DevBuf chunks;             // int4 {pulsar, first TOA (pulsar-local), count, 0}
+  DevBuf chunks;             // int4 {pulsar, first TOA (pulsar-local), count, band rows V (multiple of 4)}
+  int32_t vmax = 0;          // largest V: row pitch of the row-index and weight tables
+  int64_t grid_rows = 0;     // rows of the grid buffer: sum over signals of P nf
+  DevBuf rows;               // [n_chunks][vmax] int32 grid-buffer row of each band row (all signals back to back)
+  DevBuf wd;                 // [n_chunks][vmax][kGridTT] interpolation weights (chromatic factor, mask folded in)
+  DevBuf g;                  // [grid_rows][R_pad] grid values of the batch
   std::vector<GridSeg*> segs;
   double fma_grid = 0.0;     // FMAs per realization: DFT + interpolation
   double fma_dft = 0.0;      // FMAs per realization in k_grid_dft
@@ -88,6 +95,8 @@ struct GridPlan {
     segs.clear();
     built = ok = false;
     n_chunks = 0;
+    vmax = 0;
+    grid_rows = 0;
     g_rpad = 0;
     // the plan figures accumulate over signals in grid_build: a rebuilt plan must start from zero
     fma_grid = fma_dft = fma_interp = grid_vals = weight_bytes = fma_direct = 0.0;
@@ -539,8 +548,8 @@ int grid_build(fpta_ctx* c, Layout& L) {
   // chunks: <= kGridTT consecutive TOAs of one pulsar, every signal's band <= kGridRowCap rows
   std::vector<int4> chunks;
   std::vector<int32_t> chunk_of(N), tt_of(N);
-  std::vector<std::vector<int2>> js(n_seg);
-  std::vector<int32_t> rmax(n_seg, 0);
+  std::vector<std::vector<int64_t>> band_lo(n_seg);  // per chunk: first grid row (unwrapped) of each signal
+  std::vector<std::vector<int32_t>> band_n(n_seg);   // per chunk: band rows of each signal (span + w)
   std::vector<int64_t> lo(n_seg), hi(n_seg);
   for (int32_t p = 0; p < L.P; ++p) {
     int64_t t = L.h_offs[p];
@@ -570,12 +579,9 @@ int grid_build(fpta_ctx* c, Layout& L) {
         tt_of[u] = (int32_t)(u - t0);
       }
       for (int32_t s = 0; s < n_seg; ++s) {
-        int32_t rows = (int32_t)(hi[s] - lo[s]) + w;
-        rows = (rows + 3) & ~3;  // k_grid_interp_mfma: 4 rows per MFMA step (pad rows weigh 0)
-        const int64_t m = ((lo[s] % nf[s]) + nf[s]) % nf[s];
-        js[s].push_back(make_int2((int)m, rows));
-        rmax[s] = std::max(rmax[s], rows);
-        for (int64_t u = t0; u < t; ++u) J[s][u] -= lo[s];  // row of the TOA's first weight in the chunk
+        band_lo[s].push_back(lo[s]);
+        band_n[s].push_back((int32_t)(hi[s] - lo[s]) + w);
+        for (int64_t u = t0; u < t; ++u) J[s][u] -= lo[s];  // row of the TOA's first weight in its band
       }
     }
   }
@@ -584,16 +590,66 @@ int grid_build(fpta_ctx* c, Layout& L) {
     return FPTA_OK;
   }
   G.n_chunks = (int32_t)chunks.size();
+  const int32_t n_chunks = G.n_chunks;
+  // band rows of a chunk: every signal's band back to back (virtual rows voff_s ..), padded to a multiple of
+  // 4 once per chunk (k_grid_interp_mfma: 4 rows per MFMA step; pad rows re-read a valid row at weight 0)
+  std::vector<int32_t> voff((size_t)n_seg * n_chunks);
+  int32_t vmax = 4;
+  for (int32_t ci = 0; ci < n_chunks; ++ci) {
+    int32_t v = 0;
+    for (int32_t s = 0; s < n_seg; ++s) {
+      voff[(size_t)s * n_chunks + ci] = v;
+      v += band_n[s][ci];
+    }
+    chunks[ci].w = (v + 3) & ~3;
+    vmax = std::max(vmax, chunks[ci].w);
+  }
+  if (vmax > kGridVMax) {
+    G.why = "gridded path: a chunk's band rows over all signals exceed " + std::to_string(kGridVMax);
+    return FPTA_OK;
+  }
+  G.vmax = vmax;
+  std::vector<int64_t> rowoff(n_seg);
+  int64_t grid_rows = 0;
+  for (int32_t s = 0; s < n_seg; ++s) {
+    rowoff[s] = grid_rows;
+    grid_rows += (int64_t)L.P * nf[s];
+  }
+  if (grid_rows > 0x7FFFFFFF) {
+    G.why = "gridded path: grid too large";
+    return FPTA_OK;
+  }
+  G.grid_rows = grid_rows;
+  std::vector<int32_t> rt((size_t)n_chunks * vmax);
+  for (int32_t ci = 0; ci < n_chunks; ++ci) {
+    int32_t* r = rt.data() + (size_t)ci * vmax;
+    const int32_t p = chunks[ci].x;
+    int32_t v = 0;
+    for (int32_t s = 0; s < n_seg; ++s)
+      for (int32_t i = 0; i < band_n[s][ci]; ++i) {
+        const int64_t j = ((band_lo[s][ci] + i) % nf[s] + nf[s]) % nf[s];
+        r[v++] = (int32_t)(rowoff[s] + (int64_t)p * nf[s] + j);
+      }
+    for (; v < vmax; ++v) r[v] = r[0];
+  }
   int rc;
-  if ((rc = upload(c, G.chunks, chunks.data(), sizeof(int4) * chunks.size(), "grid chunks"))) return rc;
+  if ((rc = upload(c, G.chunks, chunks.data(), sizeof(int4) * chunks.size(), "grid chunks")) ||
+      (rc = upload(c, G.rows, rt.data(), sizeof(int32_t) * rt.size(), "grid band rows")))
+    return rc;
   DevBuf d_chunk_of, d_tt_of, d_row, d_d;
   if ((rc = upload(c, d_chunk_of, chunk_of.data(), sizeof(int32_t) * N, "grid chunk_of")) ||
       (rc = upload(c, d_tt_of, tt_of.data(), sizeof(int32_t) * N, "grid tt_of")))
     return rc;
+  const size_t wbytes = sizeof(double) * (size_t)n_chunks * vmax * kGridTT;
+  HIPCHK(c, G.wd.ensure(wbytes), "grid weights alloc");
+  HIPCHK(c, hipMemsetAsync(G.wd.p, 0, wbytes, c->stream), "grid weights memset");
   std::vector<double> gx, gw;
   gauss_legendre(256, gx, gw);
   G.fma_direct = 0.0;
   G.fma_grid = 0.0;
+  G.fma_interp = 0.0;
+  for (int32_t ci = 0; ci < n_chunks; ++ci) G.fma_interp += (double)chunks[ci].w * kGridTT;
+  G.weight_bytes = (double)wbytes;
   for (int32_t s = 0; s < n_seg; ++s) {
     const SegDesc& d = L.segs[s]->d;
     GridSeg* gs = new GridSeg();
@@ -602,7 +658,7 @@ int grid_build(fpta_ctx* c, Layout& L) {
     gs->half = nf[s] / 2;
     gs->lde = (gs->half + 32) / 32 * 32;  // row tiles of k_grid_dft_mfma (32) and k_grid_dft (kGridMI)
     gs->ntab = (d.nm + 7) / 8 * 8;         // whole pairs of 4-mode MFMA k-steps (zero rows)
-    gs->rmax = rmax[s];
+    gs->rowoff = rowoff[s];
     // q_k = (2 pi / nf) / phi_hat(k), phi_hat(k) = alpha int_{-1}^{1} phi(z) cos(k alpha z) dz, alpha = pi w / nf
     const double alpha = M_PI * w / nf[s];
     std::vector<double> ec((size_t)gs->ntab * gs->lde, 0.0), es((size_t)gs->ntab * gs->lde, 0.0);
@@ -619,28 +675,22 @@ int grid_build(fpta_ctx* c, Layout& L) {
       }
     }
     if ((rc = upload(c, gs->ecos, ec.data(), sizeof(double) * ec.size(), "grid ecos")) ||
-        (rc = upload(c, gs->esin, es.data(), sizeof(double) * es.size(), "grid esin")) ||
-        (rc = upload(c, gs->js, js[s].data(), sizeof(int2) * js[s].size(), "grid js")))
+        (rc = upload(c, gs->esin, es.data(), sizeof(double) * es.size(), "grid esin")))
       return rc;
-    std::vector<int32_t> row(J[s].begin(), J[s].end());
+    // weight rows of signal s: its band's virtual offset in the chunk + the TOA's first row in the band
+    std::vector<int32_t> row(N);
+    for (int64_t t = 0; t < N; ++t) row[t] = (int32_t)J[s][t] + voff[(size_t)s * n_chunks + chunk_of[t]];
     if ((rc = upload(c, d_row, row.data(), sizeof(int32_t) * N, "grid rows")) ||
         (rc = upload(c, d_d, D[s].data(), sizeof(double) * N, "grid offsets")))
       return rc;
-    const size_t wbytes = sizeof(double) * ((size_t)G.n_chunks * gs->rmax + 1) * kGridTT;
-    HIPCHK(c, gs->wd.ensure(wbytes), "grid weights alloc");
-    HIPCHK(c, hipMemsetAsync(gs->wd.p, 0, wbytes, c->stream), "grid weights memset");
     HIPCHK(c,
            launch_grid_weights(c->stream, d, N, L.nu.as<double>(), d_chunk_of.as<int32_t>(), d_tt_of.as<int32_t>(),
-                               d_row.as<int32_t>(), d_d.as<double>(), w, beta, gs->rmax, gs->wd.as<double>()),
+                               d_row.as<int32_t>(), d_d.as<double>(), w, beta, vmax, G.wd.as<double>()),
            "k_grid_weights launch");
     HIPCHK(c, hipStreamSynchronize(c->stream), "grid weights sync");  // d_row / d_d are reused
-    double rows_sum = 0.0;
-    for (const int2& q : js[s]) rows_sum += q.y;
     G.fma_direct += 2.0 * d.nm * (double)N;
     G.fma_dft += (double)L.P * (gs->half + 1) * 2.0 * d.nm;
-    G.fma_interp += rows_sum * kGridTT;
     G.grid_vals += (double)L.P * gs->nf;
-    G.weight_bytes += (double)wbytes;
     G.fma_grid = G.fma_dft + G.fma_interp;
   }
   G.ok = true;
@@ -653,7 +703,7 @@ int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad) {
   GridSegs gsegs{};
   gsegs.n = (int32_t)G.segs.size();
   if (G.g_rpad != R_pad) {
-    for (GridSeg* gs : G.segs) HIPCHK(c, gs->g.ensure(sizeof(double) * (size_t)L.P * gs->nf * R_pad), "grid alloc");
+    HIPCHK(c, G.g.ensure(sizeof(double) * (size_t)G.grid_rows * R_pad), "grid alloc");
     G.g_rpad = R_pad;
   }
   {
@@ -664,13 +714,10 @@ int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad) {
       GridSegDev& g = gsegs.s[s];
       g.ecos = gs->ecos.as<double>();
       g.esin = gs->esin.as<double>();
-      g.wd = gs->wd.as<double>();
-      g.js = gs->js.as<int2>();
-      g.g = gs->g.as<double>();
+      g.g = G.g.as<double>() + gs->rowoff * R_pad;
       g.nf = gs->nf;
       g.half = gs->half;
       g.lde = gs->lde;
-      g.rmax = gs->rmax;
       g.nm = d.nm;
       g.col0 = d.col0;
       g.ntab = gs->ntab;
@@ -681,8 +728,9 @@ int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad) {
            "k_grid_dft launch");
   }
   KTimer kt(c, FPTA_K_SYNTH);
-  HIPCHK(c, launch_grid_interp_mfma(c->stream, a, G.chunks.as<int4>(), G.n_chunks, gsegs, R_pad),
-         "k_grid_interp_mfma launch");
+  GridBand band{G.chunks.as<int4>(), G.rows.as<int32_t>(), G.wd.as<double>(), G.g.as<double>(), G.n_chunks, G.vmax,
+                G.grid_rows};
+  HIPCHK(c, launch_grid_interp_mfma(c->stream, a, band, R_pad), "k_grid_interp_mfma launch");
   return FPTA_OK;
 }
 

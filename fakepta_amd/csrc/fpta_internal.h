@@ -74,15 +74,14 @@ constexpr ValuVariant kSeededVariants[] = {{1, 16}, {2, 16}, {1, 8}, {2, 8}, {1,
 static_assert(sizeof(kSeededVariants) == sizeof(kValuVariants), "one variant index selects both tables");
 
 // Gridded synthesis (grid.hip): one signal's tables as the kernels see them.
+constexpr int kGridVMax = 256;  // band rows per chunk, all signals (k_grid_interp_mfma keeps them in 4 VGPRs)
 constexpr int kGridTT = 32;  // TOAs per interpolation chunk (k_grid_interp_mfma: even / odd TOAs = two MFMA B-tiles)
 constexpr int kGridMI = 8;   // grid rows per wave in k_grid_dft
 struct GridSegDev {
   const double* ecos;  // [nm][lde] q_k cos(2 pi k j / nf), k = m + 1 (zero-padded columns)
   const double* esin;  // [nm][lde] q_k sin(2 pi k j / nf)
-  const double* wd;    // [n_chunks][rmax][kGridTT] interpolation weights (chromatic factor, mask folded in)
-  const int2* js;      // [n_chunks] {first grid row mod nf, rows}
-  double* g;           // [P][nf][R_pad] grid values of the batch
-  int32_t nf, half, lde, rmax, nm, col0;
+  double* g;           // [P][nf][R_pad] grid values of the batch (this signal's block of the grid buffer)
+  int32_t nf, half, lde, nm, col0;
   int32_t ntab;        // mode rows of ecos/esin (nm zero-padded to a multiple of 8)
   int32_t nblk;        // k_grid_dft row blocks of this signal (set by launch_grid_dft*)
 };
@@ -94,13 +93,22 @@ struct GridSegs {
 
 hipError_t launch_grid_weights(hipStream_t st, const SegDesc& sd, int64_t n_toa, const double* nu,
                                const int32_t* chunk_of, const int32_t* tt_of, const int32_t* row_of,
-                               const double* d_of, int32_t w, double beta, int32_t rmax, double* wd);
+                               const double* d_of, int32_t w, double beta, int32_t vmax, double* wd);
 hipError_t launch_grid_dft(hipStream_t st, GridSegs gsegs, int32_t P, const double* coef, int32_t K, int32_t R_pad);
 // the same two steps on v_mfma_f64_16x16x4_f64 (grid_mfma.hip)
 hipError_t launch_grid_dft_mfma(hipStream_t st, GridSegs gsegs, int32_t P, const double* coef, int32_t K,
                                 int32_t R_pad);
-hipError_t launch_grid_interp_mfma(hipStream_t st, const SynthArgs& a, const int4* chunks, int32_t n_chunks,
-                                   const GridSegs& gsegs, int32_t R_pad);
+// Interpolation band of the whole layout: per chunk of <= kGridTT TOAs the band rows of every signal back to back
+// (V rows, a multiple of 4), the grid-buffer row of each and the weights of each (row, TOA).
+struct GridBand {
+  const int4* chunks;   // [n_chunks] {pulsar, first TOA (pulsar-local), count, V}
+  const int32_t* rows;  // [n_chunks][vmax] grid-buffer row of band row v
+  const double* wd;     // [n_chunks][vmax][kGridTT] weights
+  const double* g;      // [grid_rows][R_pad] grid values (all signals)
+  int32_t n_chunks, vmax;
+  int64_t grid_rows;
+};
+hipError_t launch_grid_interp_mfma(hipStream_t st, const SynthArgs& a, const GridBand& band, int32_t R_pad);
 
 hipError_t launch_seeds(hipStream_t st, const SegDesc* segs, int32_t n_seg, const int32_t* psr_of,
                         const double* toas, const double* nu, int64_t n_toa, double4* seeds);

@@ -31,20 +31,21 @@ namespace fpta {
 typedef double dbl2 __attribute__((ext_vector_type(2)));
 
 // ----------------------------------------------------------------------------- k_grid_weights
-// One thread per TOA of the segment: W[chunk][row + i][tt] = ch(t) phi((d - i) / (w / 2)), i < w.
+// One thread per TOA of the segment: W[chunk][row + i][tt] = ch(t) phi((d - i) / (w / 2)), i < w; row = the
+// signal's band offset in the chunk + the TOA's first row in that band (host plan), pitch vmax rows per chunk.
 __global__ __launch_bounds__(256) void k_grid_weights(SegDesc sd, int64_t n_toa, const double* __restrict__ nu,
                                                       const int32_t* __restrict__ chunk_of,
                                                       const int32_t* __restrict__ tt_of,
                                                       const int32_t* __restrict__ row_of,
                                                       const double* __restrict__ d_of, int32_t w, double beta,
-                                                      int32_t rmax, double* __restrict__ wd) {
+                                                      int32_t vmax, double* __restrict__ wd) {
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (t >= n_toa) return;
   double ch = chrom_factor(sd.freqf, nu[t], sd.idx);
   if (sd.mask && !sd.mask[t]) ch = 0.0;
   const double d = d_of[t];
   const double hw = 0.5 * (double)w;
-  double* dst = wd + ((int64_t)chunk_of[t] * rmax + row_of[t]) * kGridTT + tt_of[t];
+  double* dst = wd + ((int64_t)chunk_of[t] * vmax + row_of[t]) * kGridTT + tt_of[t];
   for (int i = 0; i < w; ++i) {
     const double z = (d - (double)i) / hw;
     const double s = 1.0 - z * z;
@@ -124,9 +125,9 @@ __global__ __launch_bounds__(256) void k_grid_dft(GridSegs gsegs, const double* 
 
 hipError_t launch_grid_weights(hipStream_t st, const SegDesc& sd, int64_t n_toa, const double* nu,
                                const int32_t* chunk_of, const int32_t* tt_of, const int32_t* row_of,
-                               const double* d_of, int32_t w, double beta, int32_t rmax, double* wd) {
+                               const double* d_of, int32_t w, double beta, int32_t vmax, double* wd) {
   hipLaunchKernelGGL(k_grid_weights, dim3((unsigned)((n_toa + 255) / 256)), dim3(256), 0, st, sd, n_toa, nu,
-                     chunk_of, tt_of, row_of, d_of, w, beta, rmax, wd);
+                     chunk_of, tt_of, row_of, d_of, w, beta, vmax, wd);
   return hipGetLastError();
 }
 

@@ -18,17 +18,38 @@ namespace fpta {
 
 typedef double dbl2 __attribute__((ext_vector_type(2)));
 
+// k_grid_interp_mfma: 32 TOAs x 16 kInterpRW realizations per wave, kInterpWPC persistent workgroups per CU
+// (compile-time; tools/interp_variants.sh builds the alternatives it measures into build/diag)
+#ifndef FPTA_INTERP_RW
+#define FPTA_INTERP_RW 8
+#endif
+#ifndef FPTA_INTERP_WPC
+#define FPTA_INTERP_WPC 2
+#endif
+#ifndef FPTA_INTERP_DIAG
+#define FPTA_INTERP_DIAG 0  // 0 in every product build
+#endif
+constexpr int kInterpRW = FPTA_INTERP_RW;
+constexpr int kInterpWPC = FPTA_INTERP_WPC;
+
 // ----------------------------------------------------------------------------- k_grid_dft_mfma
 // Per pulsar two GEMMs sharing the output tile (4 modes per MFMA):
 //   Cj[j][r] = sum_k ecos[k][j] c_k[r],  Sj[j][r] = sum_k esin[k][j] s_k[r],
 //   g_j = Cj + Sj, g_{nf - j} = Cj - Sj (cos even, sin odd in j).
-// A = table (row j, mode), B = coefficients (mode, realization), D: lane holds rows j = (l >> 4) + 4 g of
-// realization l & 15, so every store instruction writes 4 runs of 128 bytes. Wave tile 16 MJ rows x 16 MR
-// realizations. The table is zero-padded to ntab (multiple of 8) modes and lde (multiple of 16 MJ) rows;
-// padded coefficient modes re-read the signal's last mode (finite) against zero table rows.
+// A = table (grid row, mode), B = coefficients (mode, realization). Both operands come in tile pairs from one
+// 16-byte load per lane: lane (lr, lg) loads table rows 2 lr, 2 lr + 1 (.x row tile 2u, .y row tile 2u + 1) and
+// realizations 2 lr, 2 lr + 1 (.x realization tile 2m, .y tile 2m + 1), so a 4-mode step issues MJ + MR loads
+// for 2 MJ MR MFMAs (the one-double-per-lane version issued one load per MFMA and was address-unit bound).
+// D of (row tile 2u + h, realization tile 2m + e): lane (lr, lg) register g holds grid row
+// j0 + 32 u + 2 (lg + 4 g) + h, realization r0 + 32 m + 2 lr + e, so the two realization tiles of a pair store
+// one 16-byte value per lane (256-byte runs per grid row). Wave tile 16 MJ rows x 16 MR realizations. The table
+// is zero-padded to ntab (multiple of 8) modes and lde (multiple of 16 MJ) rows; padded coefficient modes
+// re-read the signal's last mode (finite) against zero table rows.
 template <int MJ, int MR>
-__global__ __launch_bounds__(256) void k_grid_dft_mfma(GridSegs gsegs, const double* __restrict__ coef, int32_t K,
-                                                       int32_t R_pad) {
+__global__ __launch_bounds__(256, 2) void k_grid_dft_mfma(GridSegs gsegs, const double* __restrict__ coef,
+                                                          int32_t K, int32_t R_pad) {
+  static_assert(MJ % 2 == 0 && MR % 2 == 0, "operands come in tile pairs");
+  constexpr int PJ = MJ / 2, PR = MR / 2;
   int bz = blockIdx.z, s = 0;
   while (s + 1 < gsegs.n && bz >= gsegs.s[s].nblk) bz -= gsegs.s[s++].nblk;
   const GridSegDev& gs = gsegs.s[s];
@@ -39,9 +60,9 @@ __global__ __launch_bounds__(256) void k_grid_dft_mfma(GridSegs gsegs, const dou
   if (r0 >= R_pad) return;
   const int p = blockIdx.y;
   const int j0 = bz * 16 * MJ;
-  const double* __restrict__ cp = coef + ((int64_t)p * K + gs.col0 + 2 * lg) * R_pad + r0 + lr;
-  const double* __restrict__ ec = gs.ecos + (int64_t)lg * gs.lde + j0 + lr;
-  const double* __restrict__ es = gs.esin + (int64_t)lg * gs.lde + j0 + lr;
+  const double* __restrict__ cp = coef + ((int64_t)p * K + gs.col0 + 2 * lg) * R_pad + r0 + 2 * lr;
+  const double* __restrict__ ec = gs.ecos + (int64_t)lg * gs.lde + j0 + 2 * lr;
+  const double* __restrict__ es = gs.esin + (int64_t)lg * gs.lde + j0 + 2 * lr;
   d4 C[MJ][MR], S[MJ][MR];
 #pragma unroll
   for (int u = 0; u < MJ; ++u)
@@ -56,15 +77,23 @@ __global__ __launch_bounds__(256) void k_grid_dft_mfma(GridSegs gsegs, const dou
   // flight across the current step's MFMAs. Two operand sets alternate (unrolled by 2: no register
   // copies, which would wait on the prefetch).
   struct Ops {
-    double bc[MR], bs[MR], ac[MJ], as[MJ];
+    dbl2 bc[PR], bs[PR], ac[PJ], as[PJ];
   };
   auto mfma = [&](const Ops& o) {
 #pragma unroll
-    for (int u = 0; u < MJ; ++u)
+    for (int u = 0; u < PJ; ++u)
 #pragma unroll
-      for (int i = 0; i < MR; ++i) {
-        C[u][i] = __builtin_amdgcn_mfma_f64_16x16x4f64(o.ac[u], o.bc[i], C[u][i], 0, 0, 0);
-        S[u][i] = __builtin_amdgcn_mfma_f64_16x16x4f64(o.as[u], o.bs[i], S[u][i], 0, 0, 0);
+      for (int i = 0; i < PR; ++i) {
+        C[2 * u][2 * i] = __builtin_amdgcn_mfma_f64_16x16x4f64(o.ac[u].x, o.bc[i].x, C[2 * u][2 * i], 0, 0, 0);
+        C[2 * u][2 * i + 1] = __builtin_amdgcn_mfma_f64_16x16x4f64(o.ac[u].x, o.bc[i].y, C[2 * u][2 * i + 1], 0, 0, 0);
+        C[2 * u + 1][2 * i] = __builtin_amdgcn_mfma_f64_16x16x4f64(o.ac[u].y, o.bc[i].x, C[2 * u + 1][2 * i], 0, 0, 0);
+        C[2 * u + 1][2 * i + 1] =
+            __builtin_amdgcn_mfma_f64_16x16x4f64(o.ac[u].y, o.bc[i].y, C[2 * u + 1][2 * i + 1], 0, 0, 0);
+        S[2 * u][2 * i] = __builtin_amdgcn_mfma_f64_16x16x4f64(o.as[u].x, o.bs[i].x, S[2 * u][2 * i], 0, 0, 0);
+        S[2 * u][2 * i + 1] = __builtin_amdgcn_mfma_f64_16x16x4f64(o.as[u].x, o.bs[i].y, S[2 * u][2 * i + 1], 0, 0, 0);
+        S[2 * u + 1][2 * i] = __builtin_amdgcn_mfma_f64_16x16x4f64(o.as[u].y, o.bs[i].x, S[2 * u + 1][2 * i], 0, 0, 0);
+        S[2 * u + 1][2 * i + 1] =
+            __builtin_amdgcn_mfma_f64_16x16x4f64(o.as[u].y, o.bs[i].y, S[2 * u + 1][2 * i + 1], 0, 0, 0);
       }
   };
   auto load = [&](int qq, Ops& o) {
@@ -72,14 +101,14 @@ __global__ __launch_bounds__(256) void k_grid_dft_mfma(GridSegs gsegs, const dou
     const double* __restrict__ cq = cp + (int64_t)(2 * m) * R_pad;
     const int64_t eo = (int64_t)(4 * qq) * gs.lde;
 #pragma unroll
-    for (int i = 0; i < MR; ++i) {
-      o.bc[i] = cq[16 * i];
-      o.bs[i] = cq[R_pad + 16 * i];
+    for (int i = 0; i < PR; ++i) {
+      o.bc[i] = *(const dbl2*)(cq + 32 * i);
+      o.bs[i] = *(const dbl2*)(cq + R_pad + 32 * i);
     }
 #pragma unroll
-    for (int u = 0; u < MJ; ++u) {
-      o.ac[u] = ec[eo + 16 * u];
-      o.as[u] = es[eo + 16 * u];
+    for (int u = 0; u < PJ; ++u) {
+      o.ac[u] = *(const dbl2*)(ec + eo + 32 * u);
+      o.as[u] = *(const dbl2*)(es + eo + 32 * u);
     }
   };
   Ops o0, o1;
@@ -90,19 +119,22 @@ __global__ __launch_bounds__(256) void k_grid_dft_mfma(GridSegs gsegs, const dou
     load(min(q + 2, nq - 1), o0);
     mfma(o1);
   }
-  double* __restrict__ gp = gs.g + (int64_t)p * gs.nf * R_pad + r0 + lr;
+  double* __restrict__ gp = gs.g + (int64_t)p * gs.nf * R_pad + r0 + 2 * lr;
 #pragma unroll
-  for (int u = 0; u < MJ; ++u)
+  for (int u = 0; u < PJ; ++u)
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int j = j0 + 16 * u + lg + 4 * g;
+    for (int h = 0; h < 2; ++h)
 #pragma unroll
-      for (int i = 0; i < MR; ++i) {
-        const double cv = C[u][i][g], sv = S[u][i][g];
-        if (j <= gs.half) gp[(int64_t)j * R_pad + 16 * i] = cv + sv;
-        if (j > 0 && 2 * j < gs.nf) gp[(int64_t)(gs.nf - j) * R_pad + 16 * i] = cv - sv;
+      for (int g = 0; g < 4; ++g) {
+        const int j = j0 + 32 * u + 2 * (lg + 4 * g) + h;
+#pragma unroll
+        for (int i = 0; i < PR; ++i) {
+          const double c0 = C[2 * u + h][2 * i][g], s0 = S[2 * u + h][2 * i][g];
+          const double c1 = C[2 * u + h][2 * i + 1][g], s1 = S[2 * u + h][2 * i + 1][g];
+          if (j <= gs.half) *(dbl2*)(gp + (int64_t)j * R_pad + 32 * i) = dbl2{c0 + s0, c1 + s1};
+          if (j > 0 && 2 * j < gs.nf) *(dbl2*)(gp + (int64_t)(gs.nf - j) * R_pad + 32 * i) = dbl2{c0 - s0, c1 - s1};
+        }
       }
-    }
 }
 
 // White-noise normals of (TOA t, global realizations g, g + 1 of the pair containing g): the
@@ -114,38 +146,43 @@ __device__ __forceinline__ void mfma_white_pair(int64_t t, int64_t g, uint32_t k
 }
 
 // ----------------------------------------------------------------------------- k_grid_interp_mfma
-// out[r][t] = sum_s sum_i W_s[chunk][i][tt] G_s[(J_s + i) mod nf][r] for a chunk of <= 32 TOAs: per 4 band
-// rows, A = grid values (realization, row), B = weights (row, TOA).
-//  * The chunk's even and odd TOAs are two B-tiles (column j = TOA 2j, 2j + 1) over the same band rows, so one
-//    set of grid loads feeds both: the address unit, the busiest block of the 16-TOA version (one dbl2 grid
-//    load per 2 MFMAs), now sees one per 4. Lane (lr, lg) loads W[row lg][2 lr .. 2 lr + 1] with one 16-byte
-//    load (.x even tile, .y odd tile).
-//  * Realization tiles come in pairs: lane (lr, lg) loads the adjacent realizations 2 lr, 2 lr + 1 of a
+// out[r][t] = sum_v W[chunk][v][tt] G[row(chunk, v)][r] over the chunk's band rows v < V: every signal's band
+// back to back (host plan), so one flat loop of V / 4 MFMA steps covers all signals. Per step A = grid values
+// (realization, row), B = weights (row, TOA):
+//  * the grid rows of a step come from the chunk's row table with one scalar 16-byte load (4 rows, any
+//    signal: each lane group loads its own row), so signals need no separate pipeline fill and the band is
+//    padded to 4 rows once per chunk, not per signal;
+//  * the chunk's even and odd TOAs are two B-tiles (column j = TOA 2j, 2j + 1) over the same rows, so one set
+//    of grid loads feeds both. Lane (lr, lg) loads W[v = 4q + lg][2 lr .. 2 lr + 1] with one 16-byte load
+//    (.x even tile, .y odd tile);
+//  * realization tiles come in pairs: lane (lr, lg) loads the adjacent realizations 2 lr, 2 lr + 1 of a
 //    32-realization block with one 16-byte load (.x tile 2m, .y tile 2m + 1). D row rho of tile 2m + h is then
-//    realization 32 m + 2 rho + h.
+//    realization 32 m + 2 rho + h;
 //  * D's register g of lane l holds TOA 2 (l & 15) + e of realization 32 m + 2 (lg + 4 g) + h in acc[e][2m + h]:
 //    the two TOA parities of a lane are adjacent samples of one realization row (one 16-byte store, 256-byte
 //    runs per row), and the two tiles of a realization pair sit in the same lane and register (one Philox call
 //    per pair for the white epilogue).
-// Wave tile = chunk x 16 RW realizations; per signal the next 4-row step's operands are loaded before the
-// current step's MFMAs (two register sets, unrolled by 2, the odd last step skipped by a uniform branch).
+// Wave tile = chunk x 16 RW realizations; the next step's operands are loaded before the current step's MFMAs
+// (two register sets, unrolled by 2; the last prefetch re-reads the final step, the odd last step is skipped by
+// a uniform branch).
 template <bool WHITE, int RW>
-__device__ __forceinline__ void interp_tile(const SynthArgs& a, const int4* __restrict__ chunks, int32_t n_chunks,
-                                            const GridSegs& gsegs, int32_t R_pad, double* __restrict__ out,
-                                            int tile) {
+__device__ __forceinline__ void interp_tile(const SynthArgs& a, const GridBand& band, int32_t R_pad,
+                                            double* __restrict__ out, int tile) {
   static_assert(RW % 2 == 0, "realization tiles come in pairs");
   static_assert(kGridTT == 32, "two 16-TOA B-tiles per chunk");
   constexpr int NP = RW / 2;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const int lr = lane & 15, lg = lane >> 4;
-  const int rb = __builtin_amdgcn_readfirstlane(tile / n_chunks);  // realization block of 64 RW
-  const int c = __builtin_amdgcn_readfirstlane(tile - rb * n_chunks);
+  const int rb = __builtin_amdgcn_readfirstlane(tile / band.n_chunks);  // realization block of 64 RW
+  const int c = __builtin_amdgcn_readfirstlane(tile - rb * band.n_chunks);
   const int r0 = (rb * 4 + wave) * 16 * RW;
   if (r0 >= R_pad) return;
   FPTA_DCHECK(r0 + 16 * RW <= R_pad, "k_grid_interp_mfma realization block", r0 + 16 * RW, R_pad + 1);
-  const int4 ci = chunks[c];
+  const int4 ci = band.chunks[c];
   const int p = __builtin_amdgcn_readfirstlane(ci.x);
+  const int nq = __builtin_amdgcn_readfirstlane(ci.w) >> 2;
+  FPTA_DCHECK(4 * nq <= band.vmax, "k_grid_interp_mfma band rows", 4 * nq, band.vmax + 1);
   const int64_t base = a.offs[p];
 
   d4 acc[2][RW];  // [TOA parity][realization tile]
@@ -154,41 +191,59 @@ __device__ __forceinline__ void interp_tile(const SynthArgs& a, const int4* __re
 #pragma unroll
     for (int i = 0; i < RW; ++i) acc[e][i] = d4{0.0, 0.0, 0.0, 0.0};
 
-  for (int si = 0; si < gsegs.n; ++si) {
-    const GridSegDev& gs = gsegs.s[si];
-    const int2 jr = gs.js[c];
-    const int nq = __builtin_amdgcn_readfirstlane(jr.y) >> 2;
-    if (nq == 0) continue;
-    const int nf = gs.nf;
-    const double* __restrict__ Gp = gs.g + (int64_t)p * nf * R_pad + r0 + 2 * lr;
-    const double* __restrict__ Wp = gs.wd + (int64_t)c * gs.rmax * kGridTT + lg * kGridTT + 2 * lr;
-    int j = __builtin_amdgcn_readfirstlane(jr.x) + lg;  // grid row of this lane's k index
-    if (j >= nf) j -= nf;
-    dbl2 a0[NP], a1[NP], b0, b1;
-    auto load = [&](int qq, dbl2(&av)[NP], dbl2& bv) {
-      int jj = j + 4 * qq;
-      while (jj >= nf) jj -= nf;
-      const double* __restrict__ gr = Gp + (int64_t)jj * R_pad;
+  // the chunk's row table in registers: lane l holds band row l + 64 i in rr[i] (V <= kGridVMax = 256, host
+  // plan); a step's rows then come from one ds_bpermute (no address-unit work, no vmcnt wait on the grid
+  // prefetch). A per-step scalar load of the table compiled to a vector load + vmcnt(0) behind the epilogue's
+  // stores.
+  const int32_t* __restrict__ rt = band.rows + (int64_t)c * band.vmax;
+  const int V = 4 * nq;
+  int rr[kGridVMax / 64];
 #pragma unroll
-      for (int m = 0; m < NP; ++m) av[m] = *(const dbl2*)(gr + 32 * m);
-      bv = *(const dbl2*)(Wp + 4 * kGridTT * qq);
-    };
-    auto mfma = [&](const dbl2(&av)[NP], const dbl2& bv) {
+  for (int i = 0; i < kGridVMax / 64; ++i) rr[i] = rt[min(64 * i + lane, V - 1)];
+  const double* __restrict__ G0 = band.g + r0 + 2 * lr;
+  const double* __restrict__ Wp = band.wd + ((int64_t)c * band.vmax + lg) * kGridTT + 2 * lr;
+  dbl2 a0[NP], a1[NP], b0, b1;
+  auto row_of = [&](int qq) {  // grid row of this lane's k index in step qq
+    const int blk = qq >> 4;     // 64-row block of the step's rows (uniform)
+    const int src = blk == 0 ? rr[0] : (blk == 1 ? rr[1] : (blk == 2 ? rr[2] : rr[3]));
+    return __builtin_amdgcn_ds_bpermute(((4 * qq + lg) & 63) << 2, src);
+  };
+  auto load = [&](int qq, int row, dbl2(&av)[NP], dbl2& bv) {
+    FPTA_DCHECK(row >= 0 && row < band.grid_rows, "k_grid_interp_mfma grid row", row, band.grid_rows);
+#if FPTA_INTERP_DIAG == 1  // diagnostic build only (tools/interp_variants.sh): every step reads one L1-resident row
+    const double* __restrict__ gr = G0 + (int64_t)(row & 3) * R_pad;
+#else
+    const double* __restrict__ gr = G0 + (int64_t)row * R_pad;
+#endif
 #pragma unroll
-      for (int m = 0; m < NP; ++m) {
-        acc[0][2 * m] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m].x, bv.x, acc[0][2 * m], 0, 0, 0);
-        acc[0][2 * m + 1] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m].y, bv.x, acc[0][2 * m + 1], 0, 0, 0);
-        acc[1][2 * m] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m].x, bv.y, acc[1][2 * m], 0, 0, 0);
-        acc[1][2 * m + 1] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m].y, bv.y, acc[1][2 * m + 1], 0, 0, 0);
-      }
-    };
-    load(0, a0, b0);
-    for (int q = 0; q < nq; q += 2) {
-      load(min(q + 1, nq - 1), a1, b1);
-      mfma(a0, b0);
-      load(min(q + 2, nq - 1), a0, b0);
-      if (q + 1 < nq) mfma(a1, b1);  // odd step count: skip the re-read last step (wave-uniform branch)
+    for (int m = 0; m < NP; ++m) av[m] = *(const dbl2*)(gr + 32 * m);
+    bv = *(const dbl2*)(Wp + 4 * kGridTT * qq);
+  };
+  auto mfma = [&](const dbl2(&av)[NP], const dbl2& bv) {
+#pragma unroll
+    for (int m = 0; m < NP; ++m) {
+      acc[0][2 * m] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m].x, bv.x, acc[0][2 * m], 0, 0, 0);
+      acc[0][2 * m + 1] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m].y, bv.x, acc[0][2 * m + 1], 0, 0, 0);
+      acc[1][2 * m] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m].x, bv.y, acc[1][2 * m], 0, 0, 0);
+      acc[1][2 * m + 1] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m].y, bv.y, acc[1][2 * m + 1], 0, 0, 0);
     }
+  };
+  // rows are looked up one step ahead of their loads, loads one step ahead of their MFMAs; the scheduling
+  // barriers keep each step's loads issued before the MFMAs of the step before (else the first MFMA, hoisted
+  // above them, waits for every outstanding load)
+  int row1 = row_of(min(1, nq - 1));
+  load(0, row_of(0), a0, b0);
+  for (int q = 0; q < nq; q += 2) {
+    const int row2 = row_of(min(q + 2, nq - 1));
+    load(min(q + 1, nq - 1), row1, a1, b1);
+    __builtin_amdgcn_sched_barrier(0);
+    mfma(a0, b0);
+    __builtin_amdgcn_sched_barrier(0);
+    row1 = row_of(min(q + 3, nq - 1));
+    load(min(q + 2, nq - 1), row2, a0, b0);
+    __builtin_amdgcn_sched_barrier(0);
+    if (q + 1 < nq) mfma(a1, b1);  // odd step count: skip the re-read last step (wave-uniform branch)
+    __builtin_amdgcn_sched_barrier(0);
   }
 
   const int cnt = __builtin_amdgcn_readfirstlane(ci.z);
@@ -233,8 +288,12 @@ __device__ __forceinline__ void interp_tile(const SynthArgs& a, const int4* __re
       }
     }
   }
-  // one 16-byte store per (lane, realization) when both TOAs exist: the row offset r * ldo + tg is even
-  // whenever ldo and tg are, else the pair is stored as two 8-byte stores
+  // one 16-byte store per (lane, realization) when both TOAs exist and the row offset r * ldo + tg keeps 16-byte
+  // alignment (ldo and tg even), else the pair is stored as two 8-byte stores
+#if FPTA_INTERP_DIAG == 2  // diagnostic build only: no stores (one conditional store keeps the sums live)
+  if (acc[0][0][0] == 12345.678) out[tg] = acc[0][RW - 1][3] + acc[1][RW - 1][3];
+  return;
+#endif
   double* __restrict__ ocol = out + tg;
   const bool pair = tt + 1 < cnt;
   const bool vec = pair && ((((uintptr_t)ocol) | ((uintptr_t)a.ldo << 3)) & 15) == 0;
@@ -266,20 +325,17 @@ __device__ __forceinline__ void interp_tile(const SynthArgs& a, const int4* __re
 // overlap, so they stay in the XCD's L2). One tile per short-lived workgroup instead left the CUs mostly
 // empty (SQ_WAVE_CYCLES ~ 0.7 resident waves per SIMD): workgroup dispatch, not the memory system, paced it.
 template <bool WHITE, int RW>
-__global__ __launch_bounds__(256, 2) void k_grid_interp_mfma(SynthArgs a, const int4* __restrict__ chunks,
-                                                          int32_t n_chunks, int32_t n_tiles, GridSegs gsegs,
-                                                          int32_t R_pad, double* __restrict__ out) {
+__global__ __launch_bounds__(256, FPTA_INTERP_WPC) void k_grid_interp_mfma(SynthArgs a, GridBand band, int32_t n_tiles,
+                                                                         int32_t R_pad, double* __restrict__ out) {
   const int per = (n_tiles + 7) >> 3;
   const int x = blockIdx.x & 7;
   const int step = gridDim.x >> 3;
   const int end = min(n_tiles, (x + 1) * per);
   for (int tile = x * per + (int)(blockIdx.x >> 3); tile < end; tile += step)
-    interp_tile<WHITE, RW>(a, chunks, n_chunks, gsegs, R_pad, out, tile);
+    interp_tile<WHITE, RW>(a, band, R_pad, out, tile);
 }
 
-
-constexpr int kDftMJ = 2, kDftMR = 2;  // k_grid_dft_mfma wave tile: 32 grid rows x 32 realizations
-constexpr int kInterpRW = 8;           // k_grid_interp_mfma: 32 TOAs x 128 realizations per wave
+constexpr int kDftMJ = 2, kDftMR = 4;  // k_grid_dft_mfma wave tile: 32 grid rows x 64 realizations
 
 hipError_t launch_grid_dft_mfma(hipStream_t st, GridSegs gsegs, int32_t P, const double* coef, int32_t K,
                                 int32_t R_pad) {
@@ -298,12 +354,12 @@ hipError_t launch_grid_dft_mfma(hipStream_t st, GridSegs gsegs, int32_t P, const
   return hipGetLastError();
 }
 
-template <int RW>
-hipError_t launch_interp_rw(hipStream_t st, const SynthArgs& a, const int4* chunks, int32_t n_chunks,
-                            const GridSegs& gsegs, int32_t R_pad) {
-  if (R_pad % (16 * RW) != 0) return hipErrorInvalidValue;
+hipError_t launch_grid_interp_mfma(hipStream_t st, const SynthArgs& a, const GridBand& band, int32_t R_pad) {
+  constexpr int RW = kInterpRW;
+  if (band.n_chunks <= 0 || band.vmax < 4 || band.vmax % 4 != 0 || R_pad % (16 * RW) != 0)
+    return hipErrorInvalidValue;
   const int32_t n_rb = (R_pad + 64 * RW - 1) / (64 * RW);
-  const int64_t tiles = (int64_t)n_chunks * n_rb;
+  const int64_t tiles = (int64_t)band.n_chunks * n_rb;
   if (tiles > 0x7FFFFFFF) return hipErrorInvalidValue;
   static int n_cu = 0;
   if (!n_cu) {
@@ -312,24 +368,17 @@ hipError_t launch_interp_rw(hipStream_t st, const SynthArgs& a, const int4* chun
         hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0)
       n_cu = 256;
   }
-  // persistent grid: 2 workgroups per CU (profiles/r01_sweep_interp_wpc.txt: 1 -> 1.06 ms, 2 -> 0.74, 3 -> 0.81)
-  const int64_t want = (int64_t)n_cu * 2;
+  // persistent grid: kInterpWPC workgroups per CU (16-TOA tiles, profiles/r01_sweep_interp_wpc.txt: 1 -> 1.06 ms,
+  // 2 -> 0.74, 3 -> 0.81; 32-TOA tiles: profiles/r02_interp_variants.txt)
+  const int64_t want = (int64_t)n_cu * kInterpWPC;
   const int64_t grid = std::min<int64_t>((tiles + 7) / 8 * 8, (want + 7) / 8 * 8);
   if (a.w_on)
-    hipLaunchKernelGGL((k_grid_interp_mfma<true, RW>), dim3((unsigned)grid), dim3(256), 0, st, a, chunks, n_chunks,
-                       (int32_t)tiles, gsegs, R_pad, a.out);
+    hipLaunchKernelGGL((k_grid_interp_mfma<true, RW>), dim3((unsigned)grid), dim3(256), 0, st, a, band,
+                       (int32_t)tiles, R_pad, a.out);
   else
-    hipLaunchKernelGGL((k_grid_interp_mfma<false, RW>), dim3((unsigned)grid), dim3(256), 0, st, a, chunks,
-                       n_chunks, (int32_t)tiles, gsegs, R_pad, a.out);
+    hipLaunchKernelGGL((k_grid_interp_mfma<false, RW>), dim3((unsigned)grid), dim3(256), 0, st, a, band,
+                       (int32_t)tiles, R_pad, a.out);
   return hipGetLastError();
-}
-
-hipError_t launch_grid_interp_mfma(hipStream_t st, const SynthArgs& a, const int4* chunks, int32_t n_chunks,
-                                   const GridSegs& gsegs, int32_t R_pad) {
-  if (n_chunks <= 0 || gsegs.n < 0 || gsegs.n > kGridMaxSeg) return hipErrorInvalidValue;
-  for (int s = 0; s < gsegs.n; ++s)
-    if (gsegs.s[s].rmax % 4 != 0 || gsegs.s[s].nf < 4) return hipErrorInvalidValue;
-  return launch_interp_rw<kInterpRW>(st, a, chunks, n_chunks, gsegs, R_pad);
 }
 
 }  // namespace fpta

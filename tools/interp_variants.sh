@@ -1,0 +1,24 @@
+#!/bin/bash
+# Build (build) or time (run) compile-time variants of k_grid_interp_mfma: realization tiles per wave (RW),
+# persistent workgroups per CU (WPC) and diagnostic cuts (DIAG 1: grid loads from one L1-resident row; 2: no
+# stores). Throwaway libraries in build/diag, loaded by tools/interp_diag.py through
+# FAKEPTA_AMD_LIB; never the product or the bench.
+S=fakepta_amd/csrc
+D=build/diag
+VARIANTS="8:2:0 8:2:1 8:2:2"
+if [ "$1" = build ]; then
+  mkdir -p $D
+  for v in $VARIANTS; do
+    IFS=: read rw wpc dg <<< "$v"
+    /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -Wall -Wno-unused-result -ffp-contract=fast \
+      -fno-gpu-rdc -DFPTA_INTERP_RW=$rw -DFPTA_INTERP_WPC=$wpc -DFPTA_INTERP_DIAG=$dg $S/kernels.hip $S/dense.hip $S/grid.hip \
+      $S/grid_mfma.hip $S/capi.hip -o $D/lib_rw${rw}_wpc${wpc}_d${dg}.so &
+  done
+  wait
+  exit 0
+fi
+set -o pipefail
+for v in $VARIANTS; do
+  IFS=: read rw wpc dg <<< "$v"
+  FAKEPTA_AMD_LIB=$D/lib_rw${rw}_wpc${wpc}_d${dg}.so timeout -k 5 120 python tools/interp_diag.py --label "rw$rw-wpc$wpc-d$dg" || exit 1
+done
