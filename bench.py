@@ -36,7 +36,10 @@ HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 SYNTH_KERNELS = {3: ("k_synth_valu_seeded<2,16>", "fp64-valu"), 2: ("k_synth_mfma<4,2>", "fp64-mfma"),
                  1: ("k_synth_direct", "fp64-valu")}
 GRID_INTERP = ("k_grid_interp_mfma<8>", "fp64-mfma")
-GRID_DFT = {True: "k_grid_dft_mfma<2,2>", False: "k_grid_dft<8>"}
+# layout tag of the gridded plan a PMC traffic record must carry to describe the shipped interpolation kernel
+# (32-TOA chunks, every signal's band back to back); untagged records describe round-1 kernels of the same name
+GRID_LAYOUT = "band32"
+GRID_DFT = {True: "k_grid_dft_mfma<2,4>", False: "k_grid_dft<8>"}
 
 
 def parse():
@@ -176,8 +179,9 @@ def cpu_baseline(sim, psrs, n_sample, seed):
                 vectorised_all_cores=vec)
 
 
-def pmc_traffic(kernel, info, R, path_arg):
-    """HBM bytes per launch from the matching profiles/*traffic.json PMC record (same kernel and shape)."""
+def pmc_traffic(kernel, info, R, path_arg, layout=None):
+    """HBM bytes per launch from the matching profiles/*traffic.json PMC record (same kernel, shape and, for the
+    gridded path, plan layout)."""
     candidates = ([path_arg] if path_arg else sorted(glob.glob(os.path.join(ROOT, "profiles", "*traffic.json"))))
     for cand in candidates:
         try:
@@ -186,7 +190,7 @@ def pmc_traffic(kernel, info, R, path_arg):
         except (OSError, ValueError):
             continue
         if (tr.get("K") == info["K"] and tr.get("n_real") == R and tr.get("n_toa") == info["n_toa"]
-                and kernel.startswith(tr.get("kernel", "?"))):
+                and kernel.startswith(tr.get("kernel", "?")) and tr.get("layout") == layout):
             return tr.get("hbm_bytes_per_launch"), os.path.relpath(cand, ROOT)
     return None, None
 
@@ -298,8 +302,7 @@ def main():
     out_bytes = 8.0 * info["n_toa"] * n_launch_real
     if path == 4:
         kernel, pipe = GRID_INTERP
-        kernel = kernel.format(w=gi["width"])
-        traffic, traffic_src = pmc_traffic(kernel, info, R, args.traffic)
+        traffic, traffic_src = pmc_traffic(kernel, info, R, args.traffic, GRID_LAYOUT)
         achieved = out_bytes / synth_avg_s / 1e9
         R_pad = -(-int(n_launch_real) // 128) * 128
         impl_bytes = out_bytes + 8.0 * gi["grid_vals"] * R_pad + gi["weight_bytes"]

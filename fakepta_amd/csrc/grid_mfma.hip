@@ -149,9 +149,9 @@ __device__ __forceinline__ void mfma_white_pair(int64_t t, int64_t g, uint32_t k
 // out[r][t] = sum_v W[chunk][v][tt] G[row(chunk, v)][r] over the chunk's band rows v < V: every signal's band
 // back to back (host plan), so one flat loop of V / 4 MFMA steps covers all signals. Per step A = grid values
 // (realization, row), B = weights (row, TOA):
-//  * the grid rows of a step come from the chunk's row table with one scalar 16-byte load (4 rows, any
-//    signal: each lane group loads its own row), so signals need no separate pipeline fill and the band is
-//    padded to 4 rows once per chunk, not per signal;
+//  * the grid rows of a chunk sit in registers (lane l holds band row l + 64 i in rr[i], V <= kGridVMax) and a
+//    step's 4 rows come from one ds_bpermute, so signals need no separate pipeline fill and the band is padded to
+//    4 rows once per chunk, not per signal;
 //  * the chunk's even and odd TOAs are two B-tiles (column j = TOA 2j, 2j + 1) over the same rows, so one set
 //    of grid loads feeds both. Lane (lr, lg) loads W[v = 4q + lg][2 lr .. 2 lr + 1] with one 16-byte load
 //    (.x even tile, .y odd tile);
@@ -162,98 +162,33 @@ __device__ __forceinline__ void mfma_white_pair(int64_t t, int64_t g, uint32_t k
 //    the two TOA parities of a lane are adjacent samples of one realization row (one 16-byte store, 256-byte
 //    runs per row), and the two tiles of a realization pair sit in the same lane and register (one Philox call
 //    per pair for the white epilogue).
-// Wave tile = chunk x 16 RW realizations; the next step's operands are loaded before the current step's MFMAs
-// (two register sets, unrolled by 2; the last prefetch re-reads the final step, the odd last step is skipped by
-// a uniform branch).
-template <bool WHITE, int RW>
-__device__ __forceinline__ void interp_tile(const SynthArgs& a, const GridBand& band, int32_t R_pad,
-                                            double* __restrict__ out, int tile) {
-  static_assert(RW % 2 == 0, "realization tiles come in pairs");
-  static_assert(kGridTT == 32, "two 16-TOA B-tiles per chunk");
+// Wave tile = chunk x 16 RW realizations. Software pipeline: a step's operands are loaded two steps ahead (two
+// register sets), and a wave sets up its NEXT tile and issues that tile's first two steps of loads before it
+// stores the current tile. Loads and stores retire through one in-order counter (vmcnt), so loads issued after
+// the 32 stores of an epilogue would wait for them; issued before, the next tile's first 32 MFMAs run while the
+// stores drain (profiles/r02_interp_diag2.txt: without stores the kernel takes 0.42 ms, with them 0.63).
+template <int RW>
+struct InterpTile {
+  int c, p, r0, nq, cnt, y;
+  int rr[kGridVMax / 64];
+  const double* G0;
+  const double* Wp;
+};
+
+// White noise + ECORR added to the tile's sums in registers (before the next tile's operands are loaded: the
+// Philox rounds and those operands do not fit in the register budget together).
+template <int RW>
+__device__ __forceinline__ void interp_white(const SynthArgs& a, const InterpTile<RW>& t, d4 (&acc)[2][RW]) {
   constexpr int NP = RW / 2;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const int lr = lane & 15, lg = lane >> 4;
-  const int rb = __builtin_amdgcn_readfirstlane(tile / band.n_chunks);  // realization block of 64 RW
-  const int c = __builtin_amdgcn_readfirstlane(tile - rb * band.n_chunks);
-  const int r0 = (rb * 4 + wave) * 16 * RW;
-  if (r0 >= R_pad) return;
-  FPTA_DCHECK(r0 + 16 * RW <= R_pad, "k_grid_interp_mfma realization block", r0 + 16 * RW, R_pad + 1);
-  const int4 ci = band.chunks[c];
-  const int p = __builtin_amdgcn_readfirstlane(ci.x);
-  const int nq = __builtin_amdgcn_readfirstlane(ci.w) >> 2;
-  FPTA_DCHECK(4 * nq <= band.vmax, "k_grid_interp_mfma band rows", 4 * nq, band.vmax + 1);
-  const int64_t base = a.offs[p];
-
-  d4 acc[2][RW];  // [TOA parity][realization tile]
-#pragma unroll
-  for (int e = 0; e < 2; ++e)
-#pragma unroll
-    for (int i = 0; i < RW; ++i) acc[e][i] = d4{0.0, 0.0, 0.0, 0.0};
-
-  // the chunk's row table in registers: lane l holds band row l + 64 i in rr[i] (V <= kGridVMax = 256, host
-  // plan); a step's rows then come from one ds_bpermute (no address-unit work, no vmcnt wait on the grid
-  // prefetch). A per-step scalar load of the table compiled to a vector load + vmcnt(0) behind the epilogue's
-  // stores.
-  const int32_t* __restrict__ rt = band.rows + (int64_t)c * band.vmax;
-  const int V = 4 * nq;
-  int rr[kGridVMax / 64];
-#pragma unroll
-  for (int i = 0; i < kGridVMax / 64; ++i) rr[i] = rt[min(64 * i + lane, V - 1)];
-  const double* __restrict__ G0 = band.g + r0 + 2 * lr;
-  const double* __restrict__ Wp = band.wd + ((int64_t)c * band.vmax + lg) * kGridTT + 2 * lr;
-  dbl2 a0[NP], a1[NP], b0, b1;
-  auto row_of = [&](int qq) {  // grid row of this lane's k index in step qq
-    const int blk = qq >> 4;     // 64-row block of the step's rows (uniform)
-    const int src = blk == 0 ? rr[0] : (blk == 1 ? rr[1] : (blk == 2 ? rr[2] : rr[3]));
-    return __builtin_amdgcn_ds_bpermute(((4 * qq + lg) & 63) << 2, src);
-  };
-  auto load = [&](int qq, int row, dbl2(&av)[NP], dbl2& bv) {
-    FPTA_DCHECK(row >= 0 && row < band.grid_rows, "k_grid_interp_mfma grid row", row, band.grid_rows);
-#if FPTA_INTERP_DIAG == 1  // diagnostic build only (tools/interp_variants.sh): every step reads one L1-resident row
-    const double* __restrict__ gr = G0 + (int64_t)(row & 3) * R_pad;
-#else
-    const double* __restrict__ gr = G0 + (int64_t)row * R_pad;
-#endif
-#pragma unroll
-    for (int m = 0; m < NP; ++m) av[m] = *(const dbl2*)(gr + 32 * m);
-    bv = *(const dbl2*)(Wp + 4 * kGridTT * qq);
-  };
-  auto mfma = [&](const dbl2(&av)[NP], const dbl2& bv) {
-#pragma unroll
-    for (int m = 0; m < NP; ++m) {
-      acc[0][2 * m] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m].x, bv.x, acc[0][2 * m], 0, 0, 0);
-      acc[0][2 * m + 1] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m].y, bv.x, acc[0][2 * m + 1], 0, 0, 0);
-      acc[1][2 * m] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m].x, bv.y, acc[1][2 * m], 0, 0, 0);
-      acc[1][2 * m + 1] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m].y, bv.y, acc[1][2 * m + 1], 0, 0, 0);
-    }
-  };
-  // rows are looked up one step ahead of their loads, loads one step ahead of their MFMAs; the scheduling
-  // barriers keep each step's loads issued before the MFMAs of the step before (else the first MFMA, hoisted
-  // above them, waits for every outstanding load)
-  int row1 = row_of(min(1, nq - 1));
-  load(0, row_of(0), a0, b0);
-  for (int q = 0; q < nq; q += 2) {
-    const int row2 = row_of(min(q + 2, nq - 1));
-    load(min(q + 1, nq - 1), row1, a1, b1);
-    __builtin_amdgcn_sched_barrier(0);
-    mfma(a0, b0);
-    __builtin_amdgcn_sched_barrier(0);
-    row1 = row_of(min(q + 3, nq - 1));
-    load(min(q + 2, nq - 1), row2, a0, b0);
-    __builtin_amdgcn_sched_barrier(0);
-    if (q + 1 < nq) mfma(a1, b1);  // odd step count: skip the re-read last step (wave-uniform branch)
-    __builtin_amdgcn_sched_barrier(0);
-  }
-
-  const int cnt = __builtin_amdgcn_readfirstlane(ci.z);
   const int tt = 2 * lr;  // this lane's even TOA in the chunk; tt + 1 the odd one
-  if (tt >= cnt) return;
-  const int64_t tg = base + ci.y + tt;
-  if constexpr (WHITE) {
+  if (tt >= t.cnt) return;
+  const int64_t tg = a.offs[t.p] + t.y + tt;
+  {
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
-      if (tt + e >= cnt) break;
+      if (tt + e >= t.cnt) break;
       const int64_t te = tg + e;
       const double sg = a.w_sigma ? a.w_sigma[te] : 0.0;
       const int ep = a.w_block_of ? a.w_block_of[te] : -1;
@@ -262,7 +197,7 @@ __device__ __forceinline__ void interp_tile(const SynthArgs& a, const GridBand& 
       for (int m = 0; m < NP; ++m) {
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-          const int rl = r0 + 32 * m + 2 * (lg + 4 * g);  // batch index of acc[e][2m][g]; acc[e][2m + 1][g]: rl + 1
+          const int rl = t.r0 + 32 * m + 2 * (lg + 4 * g);  // batch index of acc[e][2m][g]; acc[e][2m + 1][g]: rl + 1
           double x0 = acc[e][2 * m][g], x1 = acc[e][2 * m + 1][g];
           if (a.w_sigma) {
             const int64_t g0 = a.real0 + rl;  // parity uniform over the launch (rl even)
@@ -288,20 +223,37 @@ __device__ __forceinline__ void interp_tile(const SynthArgs& a, const GridBand& 
       }
     }
   }
+}
+
+template <int RW>
+__device__ __forceinline__ void interp_store(const SynthArgs& a, double* __restrict__ out, const InterpTile<RW>& t,
+                                             const d4 (&acc)[2][RW]) {
+  const int lane = threadIdx.x & 63;
+  const int lr = lane & 15, lg = lane >> 4;
+  const int tt = 2 * lr;  // this lane's even TOA in the chunk; tt + 1 the odd one
+  if (tt >= t.cnt) return;
+  const int64_t tg = a.offs[t.p] + t.y + tt;
+#if FPTA_INTERP_DIAG == 2  // diagnostic build only: no stores (one conditional store keeps every sum live)
+  {
+    double s = 0.0;
+#pragma unroll
+    for (int e = 0; e < 2; ++e)
+#pragma unroll
+      for (int i = 0; i < RW; ++i) s += acc[e][i][0] + acc[e][i][1] + acc[e][i][2] + acc[e][i][3];
+    if (s == 12345.678) out[tg] = s;
+    return;
+  }
+#endif
   // one 16-byte store per (lane, realization) when both TOAs exist and the row offset r * ldo + tg keeps 16-byte
   // alignment (ldo and tg even), else the pair is stored as two 8-byte stores
-#if FPTA_INTERP_DIAG == 2  // diagnostic build only: no stores (one conditional store keeps the sums live)
-  if (acc[0][0][0] == 12345.678) out[tg] = acc[0][RW - 1][3] + acc[1][RW - 1][3];
-  return;
-#endif
   double* __restrict__ ocol = out + tg;
-  const bool pair = tt + 1 < cnt;
+  const bool pair = tt + 1 < t.cnt;
   const bool vec = pair && ((((uintptr_t)ocol) | ((uintptr_t)a.ldo << 3)) & 15) == 0;
 #pragma unroll
   for (int i = 0; i < RW; ++i) {
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
-      const int r = r0 + 32 * (i >> 1) + 2 * (lg + 4 * g) + (i & 1);
+      const int r = t.r0 + 32 * (i >> 1) + 2 * (lg + 4 * g) + (i & 1);
       if (r < a.n_real) {
         double* o = ocol + (int64_t)r * a.ldo;
         double v0 = acc[0][i][g], v1 = acc[1][i][g];
@@ -324,15 +276,117 @@ __device__ __forceinline__ void interp_tile(const SynthArgs& a, const GridBand& 
 // b runs on XCD b % 8 and walks that XCD's contiguous range of tiles (consecutive chunks: their grid rows
 // overlap, so they stay in the XCD's L2). One tile per short-lived workgroup instead left the CUs mostly
 // empty (SQ_WAVE_CYCLES ~ 0.7 resident waves per SIMD): workgroup dispatch, not the memory system, paced it.
+// Every wave of a workgroup walks the same tiles (its own 16 RW realizations of each); a wave whose realization
+// block lies past R_pad exits at once (no barrier in the kernel).
 template <bool WHITE, int RW>
 __global__ __launch_bounds__(256, FPTA_INTERP_WPC) void k_grid_interp_mfma(SynthArgs a, GridBand band, int32_t n_tiles,
                                                                          int32_t R_pad, double* __restrict__ out) {
+  static_assert(RW % 2 == 0, "realization tiles come in pairs");
+  static_assert(kGridTT == 32, "two 16-TOA B-tiles per chunk");
+  constexpr int NP = RW / 2;
   const int per = (n_tiles + 7) >> 3;
   const int x = blockIdx.x & 7;
-  const int step = gridDim.x >> 3;
+  const int stride = gridDim.x >> 3;
   const int end = min(n_tiles, (x + 1) * per);
-  for (int tile = x * per + (int)(blockIdx.x >> 3); tile < end; tile += step)
-    interp_tile<WHITE, RW>(a, band, R_pad, out, tile);
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int lr = lane & 15, lg = lane >> 4;
+
+  auto setup = [&](int tile, InterpTile<RW>& t) {
+    const int rb = __builtin_amdgcn_readfirstlane(tile / band.n_chunks);  // realization block of 64 RW
+    t.c = __builtin_amdgcn_readfirstlane(tile - rb * band.n_chunks);
+    t.r0 = (rb * 4 + wave) * 16 * RW;
+    const int4 ci = band.chunks[t.c];
+    t.p = __builtin_amdgcn_readfirstlane(ci.x);
+    t.y = __builtin_amdgcn_readfirstlane(ci.y);
+    t.cnt = __builtin_amdgcn_readfirstlane(ci.z);
+    t.nq = __builtin_amdgcn_readfirstlane(ci.w) >> 2;
+    FPTA_DCHECK(4 * t.nq <= band.vmax && t.nq > 0, "k_grid_interp_mfma band rows", 4 * t.nq, band.vmax + 1);
+    const int32_t* __restrict__ rt = band.rows + (int64_t)t.c * band.vmax;
+#pragma unroll
+    for (int i = 0; i < kGridVMax / 64; ++i) t.rr[i] = rt[min(64 * i + lane, 4 * t.nq - 1)];
+    t.G0 = band.g + t.r0 + 2 * lr;
+    t.Wp = band.wd + ((int64_t)t.c * band.vmax + lg) * kGridTT + 2 * lr;
+  };
+  auto load = [&](const InterpTile<RW>& t, int qq, dbl2(&av)[NP], dbl2& bv) {
+    const int blk = qq >> 4;  // 64-row block of the step's rows (uniform)
+    const int src = blk == 0 ? t.rr[0] : (blk == 1 ? t.rr[1] : (blk == 2 ? t.rr[2] : t.rr[3]));
+    const int row = __builtin_amdgcn_ds_bpermute(((4 * qq + lg) & 63) << 2, src);
+    FPTA_DCHECK(row >= 0 && row < band.grid_rows, "k_grid_interp_mfma grid row", row, band.grid_rows);
+#if FPTA_INTERP_DIAG == 1  // diagnostic build only (tools/interp_variants.sh): every step reads one L1-resident row
+    const double* __restrict__ gr = t.G0 + (int64_t)(row & 3) * R_pad;
+#else
+    const double* __restrict__ gr = t.G0 + (int64_t)row * R_pad;
+#endif
+#pragma unroll
+    for (int m = 0; m < NP; ++m) av[m] = *(const dbl2*)(gr + 32 * m);
+    bv = *(const dbl2*)(t.Wp + 4 * kGridTT * qq);
+  };
+  d4 acc[2][RW];  // [TOA parity][realization tile]
+  auto mfma = [&](const dbl2(&av)[NP], const dbl2& bv) {
+#pragma unroll
+    for (int m = 0; m < NP; ++m) {
+      acc[0][2 * m] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m].x, bv.x, acc[0][2 * m], 0, 0, 0);
+      acc[0][2 * m + 1] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m].y, bv.x, acc[0][2 * m + 1], 0, 0, 0);
+      acc[1][2 * m] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m].x, bv.y, acc[1][2 * m], 0, 0, 0);
+      acc[1][2 * m + 1] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m].y, bv.y, acc[1][2 * m + 1], 0, 0, 0);
+    }
+  };
+
+  int tile = x * per + (int)(blockIdx.x >> 3);
+  if (tile >= end) return;
+  InterpTile<RW> cur;
+  setup(tile, cur);
+  if (cur.r0 >= R_pad) return;  // this wave's realization block is padding for every tile of the launch
+  FPTA_DCHECK(cur.r0 + 16 * RW <= R_pad, "k_grid_interp_mfma realization block", cur.r0 + 16 * RW, R_pad + 1);
+  dbl2 a0[NP], a1[NP], b0, b1;
+  load(cur, 0, a0, b0);
+  load(cur, min(1, cur.nq - 1), a1, b1);
+  while (true) {
+#pragma unroll
+    for (int e = 0; e < 2; ++e)
+#pragma unroll
+      for (int i = 0; i < RW; ++i) acc[e][i] = d4{0.0, 0.0, 0.0, 0.0};
+    // steps q (in a0) and q + 1 (in a1) are loaded; each set is refilled two steps ahead right after its MFMAs
+    for (int q = 0; q < cur.nq; q += 2) {
+      __builtin_amdgcn_sched_barrier(0);
+      mfma(a0, b0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (q + 2 < cur.nq) load(cur, q + 2, a0, b0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (q + 1 < cur.nq) {
+        mfma(a1, b1);
+        __builtin_amdgcn_sched_barrier(0);
+        if (q + 3 < cur.nq) load(cur, q + 3, a1, b1);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (WHITE) {
+      // the Philox rounds of the white epilogue and a second tile's operands do not fit in the register budget
+      // together: this variant stores first, then starts the next tile
+      interp_white<RW>(a, cur, acc);
+      interp_store<RW>(a, out, cur, acc);
+      tile += stride;
+      if (tile >= end) break;
+      setup(tile, cur);
+      load(cur, 0, a0, b0);
+      load(cur, min(1, cur.nq - 1), a1, b1);
+    } else {
+      // next tile: its first two steps are in flight before this tile's stores enter the vmcnt queue
+      tile += stride;
+      const bool more = tile < end;
+      InterpTile<RW> nxt = cur;
+      if (more) {
+        setup(tile, nxt);
+        load(nxt, 0, a0, b0);
+        load(nxt, min(1, nxt.nq - 1), a1, b1);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      interp_store<RW>(a, out, cur, acc);
+      if (!more) break;
+      cur = nxt;
+    }
+  }
 }
 
 constexpr int kDftMJ = 2, kDftMR = 4;  // k_grid_dft_mfma wave tile: 32 grid rows x 64 realizations

@@ -74,7 +74,7 @@ def c3(total):
     from fakepta import correlated_noises as cn
     from fakepta_amd.batch import BatchSimulator
     ctx = _capi.Context(0)
-    psrs = bench.build_c2(100, 2000)
+    psrs = bench.build_array(100, 2000, "c2")
     sim = BatchSimulator(psrs, signals=["gw_common"], white=False, ctx=ctx)
     B = 4096
     nb = (total + B - 1) // B

@@ -7,7 +7,7 @@ sys.path.insert(0, __file__.rsplit("/tools/", 1)[0])
 from tools.pmc_summary import load  # noqa: E402
 
 
-def main(d, out, K, n_toa, n_real, kernel="k_synth_valu_seeded"):
+def main(d, out, K, n_toa, n_real, kernel="k_synth_valu_seeded", layout=None):
     fetch, write = [], []
     for r in load(d):
         if kernel not in r["Kernel_Name"]:
@@ -22,6 +22,8 @@ def main(d, out, K, n_toa, n_real, kernel="k_synth_valu_seeded"):
                hbm_write_bytes_per_launch=wr, hbm_bytes_per_launch=rd + wr,
                algorithmic_write_bytes=8 * n_toa * n_real, launches=len(fetch),
                note="FETCH_SIZE x2 (gfx950 half-counting of wide streaming reads), WRITE_SIZE x1; KiB units")
+    if layout:
+        res["layout"] = layout  # gridded plan layout (bench.py GRID_LAYOUT)
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1)
     print(json.dumps(res))
@@ -29,4 +31,4 @@ def main(d, out, K, n_toa, n_real, kernel="k_synth_valu_seeded"):
 
 if __name__ == "__main__":
     main(sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4]), int(sys.argv[5]),
-         *(sys.argv[6:7] or []))
+         *(sys.argv[6:8] or []))
