@@ -51,6 +51,7 @@ _SIGS = [
     ("fpta_batch_download", _c_int, [_ctx_p, _i32, _i32, _vp]),
     ("fpta_batch_device_out", _c_int, [_ctx_p, ctypes.POINTER(_vp), ctypes.POINTER(_i64), ctypes.POINTER(_i32)]),
     ("fpta_batch_checksums", _c_int, [_ctx_p, _vp]),
+    ("fpta_batch_synth_checksums", _c_int, [_ctx_p, _u64, _i64, _i64, _i32, _vp]),
     ("fpta_batch_correlations", _c_int, [_ctx_p, _i32, _vp]),
     ("fpta_batch_info", _c_int, [_ctx_p, _vp]),
     ("fpta_batch_grid_info", _c_int, [_ctx_p, _vp]),
@@ -82,9 +83,9 @@ for _name, _res, _args in _SIGS:
 EXPORTED = [s[0] for s in _SIGS]
 
 OPT_SYNTH_PATH, OPT_MFMA_MIN_REAL, OPT_PROFILE, OPT_ANCHOR, OPT_VALU_VARIANT, OPT_FUSE_WHITE = 1, 2, 3, 4, 5, 6
-OPT_GRID_WIDTH, OPT_GRID_SIGMA, OPT_GRID_MFMA = 7, 8, 9
+OPT_GRID_WIDTH, OPT_GRID_SIGMA, OPT_GRID_MFMA, OPT_FUSE_CHECKSUMS = 7, 8, 9, 10
 OPTIONS = (OPT_SYNTH_PATH, OPT_MFMA_MIN_REAL, OPT_PROFILE, OPT_ANCHOR, OPT_VALU_VARIANT, OPT_FUSE_WHITE,
-           OPT_GRID_WIDTH, OPT_GRID_SIGMA, OPT_GRID_MFMA)
+           OPT_GRID_WIDTH, OPT_GRID_SIGMA, OPT_GRID_MFMA, OPT_FUSE_CHECKSUMS)
 K_GEN, K_MIX, K_SYNTH, K_WHITE, K_DENSE, K_GRID = 0, 1, 2, 3, 4, 5
 BUILD_DEBUG = 1
 
@@ -350,6 +351,14 @@ class Context:
         s = np.empty((nr, 2))
         self._check(_lib.fpta_batch_checksums(self._h, _ptr(s)), "fpta_batch_checksums")
         return s
+
+    def batch_synth_checksums(self, seed, real0, n_real, batch=4096):
+        """Realizations real0 .. real0 + n_real - 1 streamed in batches of <= batch with no host round trip in
+        between; returns their checksums [n_real, 2] (fpta_batch_synth_checksums)."""
+        out = np.empty((int(n_real), 2))
+        self._check(_lib.fpta_batch_synth_checksums(self._h, int(seed) & 0xFFFFFFFFFFFFFFFF, int(real0), int(n_real),
+                                                    int(batch), _ptr(out)), "fpta_batch_synth_checksums")
+        return out
 
     # --------------------------------------------------------------- tuning / profiling
     def set_option(self, key, value):

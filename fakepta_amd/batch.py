@@ -273,11 +273,26 @@ def simulate_sharded(sim, n_real, seed=0, real0=0, batch=4096, comm=None, on_bat
     G = comm.world
     lo, hi = shard_bounds(n_real, comm.rank, G)
     sums = np.empty((hi - lo, 2))
-    for first in range(lo, hi, batch):
-        n = min(batch, hi - first)
-        sim.synth(n, seed=seed, real0=real0 + first, to_host=False)
-        if on_batch is not None:
-            on_batch(sim, real0 + first, n)
-        sums[first - lo:first - lo + n] = sim.checksums()
+    # checksums from the gridded interpolation's partial sums (FPTA_OPT_FUSE_CHECKSUMS): no second pass over
+    # each resident block; the context's own setting is restored afterwards
+    ctx = getattr(sim, "ctx", None)
+    fuse = None
+    if ctx is not None:
+        from fakepta_amd import _capi
+        fuse = ctx.get_option(_capi.OPT_FUSE_CHECKSUMS)
+        ctx.set_option(_capi.OPT_FUSE_CHECKSUMS, 1)
+    try:
+        if ctx is not None and on_batch is None and hi > lo:
+            # no per-batch consumer: the whole shard streams inside the library, batches back to back
+            sums[:] = ctx.batch_synth_checksums(seed, real0 + lo, hi - lo, batch)
+        for first in range(lo, hi, batch) if ctx is None or on_batch is not None else ():
+            n = min(batch, hi - first)
+            sim.synth(n, seed=seed, real0=real0 + first, to_host=False)
+            if on_batch is not None:
+                on_batch(sim, real0 + first, n)
+            sums[first - lo:first - lo + n] = sim.checksums()
+    finally:
+        if fuse is not None:
+            ctx.set_option(_capi.OPT_FUSE_CHECKSUMS, fuse)
     sizes = [shard_bounds(n_real, g, G)[1] - shard_bounds(n_real, g, G)[0] for g in range(G)]
     return comm.gather_to_root(sums, sizes)

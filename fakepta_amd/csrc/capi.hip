@@ -160,6 +160,10 @@ struct fpta_ctx {
   int anchor = 0;  // 0: phasor recurrence anchored once per segment
   int valu_variant = 1;  // seeded (MT 2, NT 16): fastest on C2 (profiles/r01_sweep_*.txt)
   int fuse_white = 1;    // add white/ECORR in the seeded kernel's epilogue
+  int fuse_sums = 0;     // gridded path: interpolation writes partial checksums (FPTA_OPT_FUSE_CHECKSUMS)
+  DevBuf part, part_tmp; // partial checksums [n_chunks][R_pad][2] of the last block, reduction scratch
+  bool part_ready = false;  // part holds the partials of the current block (c->out, out_R)
+  int32_t part_chunks = 0, part_rpad = 0;
   int last_path = 0;     // synthesis path of the last batch (1 direct, 2 MFMA, 3 VALU, 4 gridded)
   std::string path_reason;  // why the last batch did not take the gridded path (empty if it did)
   // gridded path defaults: w = 16 at sigma = 1.5. Flat-spectrum worst case at real-MJD epochs 1.4e-12 (100 modes)
@@ -727,10 +731,20 @@ int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad) {
                               : launch_grid_dft(c->stream, gsegs, L.P, a.coef, a.K, R_pad),
            "k_grid_dft launch");
   }
+  // partial checksums of a batch block (written into the context's own block, not accumulated)
+  if (c->fuse_sums && a.out == c->out.as<double>() && !a.accumulate) {
+    HIPCHK(c, c->part.ensure(sizeof(double) * 2 * (size_t)G.n_chunks * R_pad), "partial checksums alloc");
+    a.part = c->part.as<double>();
+  }
   KTimer kt(c, FPTA_K_SYNTH);
   GridBand band{G.chunks.as<int4>(), G.rows.as<int32_t>(), G.wd.as<double>(), G.g.as<double>(), G.n_chunks, G.vmax,
                 G.grid_rows};
   HIPCHK(c, launch_grid_interp_mfma(c->stream, a, band, R_pad), "k_grid_interp_mfma launch");
+  if (a.part) {
+    c->part_ready = true;
+    c->part_chunks = G.n_chunks;
+    c->part_rpad = R_pad;
+  }
   return FPTA_OK;
 }
 
@@ -1058,8 +1072,11 @@ int fpta_set_option(fpta_ctx* c, int32_t key, int64_t value) {
       c->fuse_white = value ? 1 : 0;
       return FPTA_OK;
     case FPTA_OPT_GRID_MFMA:
-      if (value < 0 || value > 3) return fail(c, FPTA_EINVAL, "grid MFMA mask must be in [0, 3]");
+      if (value < 0 || value > 1) return fail(c, FPTA_EINVAL, "grid MFMA mask must be 0 or 1");
       c->grid_mfma = (int)value;
+      return FPTA_OK;
+    case FPTA_OPT_FUSE_CHECKSUMS:
+      c->fuse_sums = value ? 1 : 0;
       return FPTA_OK;
     case FPTA_OPT_VALU_VARIANT:
       if (value < 0 || value >= kNumValuVariants) return fail(c, FPTA_EINVAL, "unknown VALU variant");
@@ -1091,6 +1108,7 @@ int fpta_get_option(fpta_ctx* c, int32_t key, int64_t* value) {
     case FPTA_OPT_GRID_WIDTH: *value = c->grid_w; return FPTA_OK;
     case FPTA_OPT_GRID_SIGMA: *value = c->grid_sigma100; return FPTA_OK;
     case FPTA_OPT_GRID_MFMA: *value = c->grid_mfma; return FPTA_OK;
+    case FPTA_OPT_FUSE_CHECKSUMS: *value = c->fuse_sums; return FPTA_OK;
   }
   return fail(c, FPTA_EINVAL, "get_option: unknown key");
 }
@@ -1419,6 +1437,7 @@ static int batch_common(fpta_ctx* c, uint64_t seed, int64_t real0, int32_t n_rea
   HIPCHK(c, c->out.ensure(out_bytes), "out alloc");
   c->out_R = n_real;
   c->out_ld = L.n_toa;
+  c->part_ready = false;  // set by the gridded interpolation when it writes this block's partial checksums
   const bool do_white = white && (c->has_sigma || c->has_blocks);
   const uint32_t k0 = (uint32_t)(seed & 0xFFFFFFFFull), k1 = (uint32_t)(seed >> 32);
   WhiteCfg wc{};
@@ -1450,6 +1469,7 @@ static int batch_common(fpta_ctx* c, uint64_t seed, int64_t real0, int32_t n_rea
       return rc;
   }
   if (do_white && !fused) {
+    c->part_ready = false;  // the separate pass changes the block after the partials were taken
     KTimer kt(c, FPTA_K_WHITE);
     HIPCHK(c,
            launch_white_pairs(c->stream, wc.sigma, wc.block_of, wc.esig, wc.nblocks, wc.zb, c->out.as<double>(),
@@ -1508,13 +1528,29 @@ int fpta_batch_device_out(fpta_ctx* c, double** dptr, int64_t* ld, int32_t* n_re
   return FPTA_OK;
 }
 
+// Per-realization {sum, sum of squares} of the context's last block into c->sums (device), on the ctx stream:
+// from the interpolation's partial checksums when it wrote them for this block, else one pass over the block.
+static int launch_block_checksums(fpta_ctx* c) {
+  HIPCHK(c, c->sums.ensure(sizeof(double) * 2 * c->out_R), "sums alloc");
+  if (c->part_ready) {
+    HIPCHK(c, c->part_tmp.ensure(sizeof(double) * 2 * (size_t)kPartSegs * c->part_rpad), "partials scratch alloc");
+    HIPCHK(c,
+           launch_part_checksums(c->stream, c->part.as<double>(), c->part_chunks, c->part_rpad, c->out_R,
+                                 c->part_tmp.as<double>(), c->sums.as<double>()),
+           "k_part_reduce launch");
+  } else {
+    HIPCHK(c, launch_checksums(c->stream, c->out.as<double>(), c->out_ld, c->out_ld, c->out_R, c->sums.as<double>()),
+           "k_checksums launch");
+  }
+  return FPTA_OK;
+}
+
 int fpta_batch_checksums(fpta_ctx* c, double* sums) {
   if (!c || !sums) return fail(c, FPTA_EINVAL, "checksums: bad arguments");
   if (!c->out_R) return fail(c, FPTA_ESTATE, "checksums: nothing synthesized yet");
   HIPCHK(c, hipSetDevice(c->device), "hipSetDevice");
-  HIPCHK(c, c->sums.ensure(sizeof(double) * 2 * c->out_R), "sums alloc");
-  HIPCHK(c, launch_checksums(c->stream, c->out.as<double>(), c->out_ld, c->out_ld, c->out_R, c->sums.as<double>()),
-         "k_checksums launch");
+  int rc = launch_block_checksums(c);
+  if (rc) return rc;
   HIPCHK(c, hipMemcpyAsync(sums, c->sums.p, sizeof(double) * 2 * c->out_R, hipMemcpyDeviceToHost, c->stream),
          "sums download");
   HIPCHK(c, hipStreamSynchronize(c->stream), "checksums sync");
@@ -1633,9 +1669,8 @@ int multi_fail(fpta_multi* m, int i, int rc) {
 
 // k_checksums of the context's last block -> host (pinned) dst [n_real][2], asynchronously on the ctx stream.
 int checksums_async(fpta_ctx* c, double* dst) {
-  HIPCHK(c, c->sums.ensure(sizeof(double) * 2 * c->out_R), "sums alloc");
-  HIPCHK(c, launch_checksums(c->stream, c->out.as<double>(), c->out_ld, c->out_ld, c->out_R, c->sums.as<double>()),
-         "k_checksums launch");
+  int rc = launch_block_checksums(c);
+  if (rc) return rc;
   HIPCHK(c, hipMemcpyAsync(dst, c->sums.p, sizeof(double) * 2 * c->out_R, hipMemcpyDeviceToHost, c->stream),
          "sums download");
   return FPTA_OK;
@@ -1715,17 +1750,12 @@ int fpta_multi_set_option(fpta_multi* m, int32_t key, int64_t value) {
   return FPTA_OK;
 }
 
-int fpta_multi_synth(fpta_multi* m, uint64_t seed, int64_t real0, int64_t n_real, int32_t batch,
-                     double* checksums_out) {
-  if (!m) return fail(nullptr, FPTA_EINVAL, "null multi");
-  if (n_real <= 0 || real0 < 0 || batch <= 0 || !checksums_out) {
-    m->err = "multi_synth: bad arguments";
-    return fail(nullptr, FPTA_EINVAL, m->err);
-  }
-  if (real0 + n_real > ((int64_t)1 << 32)) {
-    m->err = "multi_synth: realization index exceeds the 32-bit Philox counter word";
-    return fail(nullptr, FPTA_EINVAL, m->err);
-  }
+// Realizations real0 .. real0 + n_real - 1 split over m's contexts (context g: [g n / G, (g + 1) n / G)),
+// streamed in batches of <= `batch` round-robin over the devices; per-realization checksums (from the gridded
+// interpolation's partial sums where it runs) are copied asynchronously into pinned staging, one sync per
+// device at the end: no host round trip between batches.
+static int stream_checksums(fpta_multi* m, uint64_t seed, int64_t real0, int64_t n_real, int32_t batch,
+                            double* checksums_out) {
   const int64_t G = (int64_t)m->ctx.size();
   std::vector<int64_t> beg(G + 1);
   for (int64_t g = 0; g <= G; ++g) beg[g] = g * n_real / G;
@@ -1739,6 +1769,12 @@ int fpta_multi_synth(fpta_multi* m, uint64_t seed, int64_t real0, int64_t n_real
     hipError_t e = hipSetDevice(c->device);
     if (e == hipSuccess) e = hipHostMalloc((void**)&stage[g], sizeof(double) * 2 * n, hipHostMallocDefault);
     if (e != hipSuccess) rc = multi_fail(m, (int)g, hip_fail(c, e, "multi_synth staging"));
+  }
+  // a checksums-only job: the gridded interpolation writes partial checksums (no second pass over each block)
+  std::vector<int> fuse(G);
+  for (int64_t g = 0; g < G; ++g) {
+    fuse[g] = m->ctx[g]->fuse_sums;
+    m->ctx[g]->fuse_sums = 1;
   }
   // round-robin: batch k of every device, then batch k + 1 (each device's stream orders its own work)
   for (int64_t k = 0; !rc; ++k) {
@@ -1764,7 +1800,34 @@ int fpta_multi_synth(fpta_multi* m, uint64_t seed, int64_t real0, int64_t n_real
     if (!rc) std::memcpy(checksums_out + 2 * (beg[g] - 0), stage[g], sizeof(double) * 2 * (beg[g + 1] - beg[g]));
     (void)hipHostFree(stage[g]);
   }
+  for (int64_t g = 0; g < G; ++g) m->ctx[g]->fuse_sums = fuse[g];
   return rc;
+}
+
+int fpta_multi_synth(fpta_multi* m, uint64_t seed, int64_t real0, int64_t n_real, int32_t batch,
+                     double* checksums_out) {
+  if (!m) return fail(nullptr, FPTA_EINVAL, "null multi");
+  if (n_real <= 0 || real0 < 0 || batch <= 0 || !checksums_out) {
+    m->err = "multi_synth: bad arguments";
+    return fail(nullptr, FPTA_EINVAL, m->err);
+  }
+  if (real0 + n_real > ((int64_t)1 << 32)) {
+    m->err = "multi_synth: realization index exceeds the 32-bit Philox counter word";
+    return fail(nullptr, FPTA_EINVAL, m->err);
+  }
+  return stream_checksums(m, seed, real0, n_real, batch, checksums_out);
+}
+
+int fpta_batch_synth_checksums(fpta_ctx* c, uint64_t seed, int64_t real0, int64_t n_real, int32_t batch,
+                               double* sums) {
+  if (!c) return fail(nullptr, FPTA_EINVAL, "null ctx");
+  if (n_real <= 0 || real0 < 0 || batch <= 0 || !sums)
+    return fail(c, FPTA_EINVAL, "batch_synth_checksums: bad arguments");
+  if (real0 + n_real > ((int64_t)1 << 32))
+    return fail(c, FPTA_EINVAL, "batch_synth_checksums: realization index exceeds the 32-bit Philox counter word");
+  fpta_multi one;
+  one.ctx.push_back(c);
+  return stream_checksums(&one, seed, real0, n_real, batch, sums);  // a failing step set c's last error
 }
 
 }  // extern "C"

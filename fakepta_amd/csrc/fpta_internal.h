@@ -51,6 +51,9 @@ struct SynthArgs {
   // realization tile the tile table was built for (0 when the kernel takes no tile table)
   int64_t coef_len;
   int32_t tile_toa, tile_real;
+  // gridded interpolation: per-(chunk, realization) partial checksums {sum, sum of squares} [n_chunks][R_pad]
+  // of the stored block, or null (FPTA_OPT_FUSE_CHECKSUMS)
+  double* part;
 };
 
 // MFMA tile geometry
@@ -109,6 +112,11 @@ struct GridBand {
   int64_t grid_rows;
 };
 hipError_t launch_grid_interp_mfma(hipStream_t st, const SynthArgs& a, const GridBand& band, int32_t R_pad);
+// checksums [n_real][2] from the interpolation's partials [n_chunks][R_pad][2], summed over chunks in a fixed
+// order (tmp: kPartSegs * R_pad * 2 doubles)
+constexpr int kPartSegs = 64;
+hipError_t launch_part_checksums(hipStream_t st, const double* part, int32_t n_chunks, int32_t R_pad, int32_t n_real,
+                                 double* tmp, double* sums);
 
 hipError_t launch_seeds(hipStream_t st, const SegDesc* segs, int32_t n_seg, const int32_t* psr_of,
                         const double* toas, const double* nu, int64_t n_toa, double4* seeds);

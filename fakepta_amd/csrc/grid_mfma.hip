@@ -225,12 +225,60 @@ __device__ __forceinline__ void interp_white(const SynthArgs& a, const InterpTil
   }
 }
 
+// Sum of x over the 16 lanes of a DPP row (the lanes lr = 0..15 of one lane group): every lane ends with the
+// row's sum, added in the same order whatever realization the row holds (rotations by 8, 4, 2, 1; 64-bit values
+// move as two 32-bit halves).
+template <int N>
+__device__ __forceinline__ double row_ror(double x) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(x), 0x120 + N, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(x), 0x120 + N, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double row_sum16(double x) {
+  x += row_ror<8>(x);
+  x += row_ror<4>(x);
+  x += row_ror<2>(x);
+  x += row_ror<1>(x);
+  return x;
+}
+
 template <int RW>
 __device__ __forceinline__ void interp_store(const SynthArgs& a, double* __restrict__ out, const InterpTile<RW>& t,
                                              const d4 (&acc)[2][RW]) {
   const int lane = threadIdx.x & 63;
   const int lr = lane & 15, lg = lane >> 4;
   const int tt = 2 * lr;  // this lane's even TOA in the chunk; tt + 1 the odd one
+  if (a.part) {
+    // partial checksums of this chunk: per realization the sum and sum of squares over the chunk's TOAs (lanes
+    // without a TOA add 0). After the row sums every lane of a row holds all of them; lane lr = 4 m + g then
+    // writes the adjacent realizations of tiles (2m, 2m + 1) at register g: two 16-byte stores per lane, two
+    // store instructions per wave (one lane per realization would take RW * 4)
+    static_assert(RW == 8, "16 lanes of a row = 4 realization pairs x 4 registers");
+    double* __restrict__ pp = a.part + ((int64_t)t.c * a.R_pad + t.r0) * 2;
+    const bool ok0 = tt < t.cnt, ok1 = tt + 1 < t.cnt;
+    const int mm = lr >> 2, gg = lr & 3;
+    double s0 = 0.0, q0 = 0.0, s1 = 0.0, q1 = 0.0;
+#pragma unroll
+    for (int i = 0; i < RW; ++i) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const double v0 = ok0 ? acc[0][i][g] : 0.0, v1 = ok1 ? acc[1][i][g] : 0.0;
+        const double sv = row_sum16(v0 + v1), qv = row_sum16(fma(v0, v0, v1 * v1));
+        if ((i >> 1) == mm && g == gg) {
+          if (i & 1) {
+            s1 = sv;
+            q1 = qv;
+          } else {
+            s0 = sv;
+            q0 = qv;
+          }
+        }
+      }
+    }
+    const int rl = 32 * mm + 2 * (lg + 4 * gg);  // realization of (tile 2mm, register gg); rl + 1: tile 2mm + 1
+    *(dbl2*)(pp + 2 * rl) = dbl2{s0, q0};
+    *(dbl2*)(pp + 2 * rl + 2) = dbl2{s1, q1};
+  }
   if (tt >= t.cnt) return;
   const int64_t tg = a.offs[t.p] + t.y + tt;
 #if FPTA_INTERP_DIAG == 2  // diagnostic build only: no stores (one conditional store keeps every sum live)
@@ -432,6 +480,51 @@ hipError_t launch_grid_interp_mfma(hipStream_t st, const SynthArgs& a, const Gri
   else
     hipLaunchKernelGGL((k_grid_interp_mfma<false, RW>), dim3((unsigned)grid), dim3(256), 0, st, a, band,
                        (int32_t)tiles, R_pad, a.out);
+  return hipGetLastError();
+}
+
+// ----------------------------------------------------------------------------- partial checksums
+// Two fixed-order passes over the interpolation's partials: segment s of kPartSegs sums chunks
+// [s L, (s + 1) L) per realization, then the segments are summed in order. Threads run over realizations, so
+// every pass reads consecutive 16-byte {sum, sumsq} pairs.
+__global__ __launch_bounds__(256) void k_part_reduce(const double* __restrict__ part, int32_t n_chunks, int32_t R_pad,
+                                                     int32_t L, double* __restrict__ tmp) {
+  const int r = blockIdx.x * 256 + threadIdx.x;
+  if (r >= R_pad) return;
+  const int s = blockIdx.y;
+  const int c1 = min(n_chunks, (s + 1) * L);
+  double a = 0.0, b = 0.0;
+  for (int c = s * L; c < c1; ++c) {
+    const dbl2 v = *(const dbl2*)(part + ((int64_t)c * R_pad + r) * 2);
+    a += v.x;
+    b += v.y;
+  }
+  *(dbl2*)(tmp + ((int64_t)s * R_pad + r) * 2) = dbl2{a, b};
+}
+
+__global__ __launch_bounds__(256) void k_part_final(const double* __restrict__ tmp, int32_t n_seg, int32_t R_pad,
+                                                    int32_t n_real, double* __restrict__ sums) {
+  const int r = blockIdx.x * 256 + threadIdx.x;
+  if (r >= n_real) return;
+  double a = 0.0, b = 0.0;
+  for (int s = 0; s < n_seg; ++s) {
+    const dbl2 v = *(const dbl2*)(tmp + ((int64_t)s * R_pad + r) * 2);
+    a += v.x;
+    b += v.y;
+  }
+  sums[2 * r] = a;
+  sums[2 * r + 1] = b;
+}
+
+hipError_t launch_part_checksums(hipStream_t st, const double* part, int32_t n_chunks, int32_t R_pad, int32_t n_real,
+                                 double* tmp, double* sums) {
+  if (n_chunks <= 0 || n_real <= 0 || n_real > R_pad) return hipErrorInvalidValue;
+  const int32_t L = (n_chunks + kPartSegs - 1) / kPartSegs;
+  const int32_t n_seg = (n_chunks + L - 1) / L;
+  hipLaunchKernelGGL(k_part_reduce, dim3((unsigned)((R_pad + 255) / 256), (unsigned)n_seg), dim3(256), 0, st, part,
+                     n_chunks, R_pad, L, tmp);
+  hipLaunchKernelGGL(k_part_final, dim3((unsigned)((n_real + 255) / 256)), dim3(256), 0, st, tmp, n_seg, R_pad, n_real,
+                     sums);
   return hipGetLastError();
 }
 

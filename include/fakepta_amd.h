@@ -182,6 +182,13 @@ int fpta_batch_device_out(fpta_ctx* ctx, double** dptr, int64_t* ld, int32_t* n_
 /* Per-realization sum and sum of squares of the last block, computed on device
  * (deterministic order). sums: host [n_real][2]. */
 int fpta_batch_checksums(fpta_ctx* ctx, double* sums);
+/* Realizations real0 .. real0 + n_real - 1 streamed through this context in batches of <= batch (the context's
+ * block then holds the last batch) with their checksums written to sums [n_real][2] (as fpta_batch_checksums,
+ * from the gridded interpolation's partial sums where it runs): batches are queued back to back with no host
+ * synchronisation in between (pinned staging, one sync at the end). The single-device form of
+ * fpta_multi_synth; fakepta_amd.batch.simulate_sharded uses it when no per-batch consumer is given. */
+int fpta_batch_synth_checksums(fpta_ctx* ctx, uint64_t seed, int64_t real0, int64_t n_real, int32_t batch,
+                               double* sums);
 /* Correlation statistics of the last block, the estimator of
  * fakepta/correlated_noises.py:14-34 (C_r[a][b] = dot(res_a, res_b) / n) for arrays whose pulsars
  * all have n TOAs (FPTA_EINVAL otherwise):
@@ -248,6 +255,11 @@ int fpta_multi_synth(fpta_multi* m, uint64_t seed, int64_t real0, int64_t n_real
 #define FPTA_OPT_GRID_SIGMA 8     /* gridded path: grid oversampling x 100 (default 150) */
 #define FPTA_OPT_GRID_MFMA 9      /* gridded path: bit 0 runs the DFT on fp64 MFMA (else fp64 VALU); the
                                      interpolation always runs on fp64 MFMA. Default 1. */
+#define FPTA_OPT_FUSE_CHECKSUMS 10 /* 1: the gridded interpolation also writes per-(chunk, realization) partial
+                                     sums (sum, sum of squares) of the block it stores, and
+                                     fpta_batch_checksums reduces those (in a fixed order: deterministic, batch-
+                                     split invariant) instead of re-reading the block. Default 0; other paths
+                                     always take the full pass. */
 int fpta_set_option(fpta_ctx* ctx, int32_t key, int64_t value);
 /* Current value of option `key` (same keys as fpta_set_option). */
 int fpta_get_option(fpta_ctx* ctx, int32_t key, int64_t* value);

@@ -81,3 +81,27 @@ def test_c3_multi_device_driver_matches(c3):
         assert m.context(1).batch_grid_info()["last_path"] == 4
     finally:
         m.close()
+
+
+def test_fused_checksums_match_full_pass(c3):
+    """FPTA_OPT_FUSE_CHECKSUMS: the interpolation's partial checksums, reduced in a fixed order, agree with a full
+    pass over the resident block (rounding only), including a ragged realization count and the white epilogue."""
+    from fakepta_amd import _capi
+    psrs, sim, ctx = c3
+    try:
+        for n, white in ((1808, False), (333, True)):
+            if white:
+                ctx.batch_set_white(np.full(sim.n_toa, 1e-7), [], [])
+            ctx.set_option(_capi.OPT_FUSE_CHECKSUMS, 0)
+            sim.synth(n, seed=SEED, real0=77, to_host=False)
+            full = ctx.batch_checksums()
+            ctx.set_option(_capi.OPT_FUSE_CHECKSUMS, 1)
+            sim.synth(n, seed=SEED, real0=77, to_host=False)
+            fused = ctx.batch_checksums()
+            assert ctx.batch_grid_info()["last_path"] == 4
+            np.testing.assert_allclose(fused[:, 1], full[:, 1], rtol=1e-12)
+            np.testing.assert_allclose(fused[:, 0], full[:, 0], rtol=1e-9, atol=1e-12 * np.abs(full[:, 0]).max())
+            assert not np.array_equal(fused, full) or n < 2  # the fused route ran (different summation order)
+    finally:
+        ctx.set_option(_capi.OPT_FUSE_CHECKSUMS, 0)
+        ctx.batch_set_white(None, [], [])
