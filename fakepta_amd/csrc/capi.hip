@@ -55,7 +55,7 @@ struct Seg {
   SegDesc d{};
   int32_t nm_orig = 0;
   std::vector<double> h_w0;  // first angular frequency per row ([P] for kind 0, [1] for kind 1)
-  DevBuf w, amp, L, mask;
+  DevBuf w, amp, L, LT, mask;
 };
 
 // Gridded-synthesis tables of one signal (grid.hip): real-DFT table E; its grid block starts at row rowoff of
@@ -161,6 +161,7 @@ struct fpta_ctx {
   int valu_variant = 1;  // seeded (MT 2, NT 16): fastest on C2 (profiles/r01_sweep_*.txt)
   int fuse_white = 1;    // add white/ECORR in the seeded kernel's epilogue
   int fuse_sums = 0;     // gridded path: interpolation writes partial checksums (FPTA_OPT_FUSE_CHECKSUMS)
+  int mix_mfma = 1;      // ORF mixing of large arrays on fp64 MFMA (k_mix_mfma) or VALU (k_mix_tiled)
   DevBuf part, part_tmp; // partial checksums [n_chunks][R_pad][2] of the last block, reduction scratch
   bool part_ready = false;  // part holds the partials of the current block (c->out, out_R)
   int32_t part_chunks = 0, part_rpad = 0;
@@ -334,6 +335,21 @@ int layout_add_signal(fpta_ctx* c, Layout& L, int32_t kind, int32_t nm, const do
     delete s;
     return rc;
   }
+  // L^T zero-padded to whole 64-pulsar tiles (columns) plus one 16-row block of k-steps: every k_mix_mfma
+  // operand load is a 16-byte pair inside the buffer, and pad rows / columns weigh 0
+  int32_t lt_ld = 0, lt_rows = 0;
+  if (kind == 1) {
+    lt_ld = (P + 63) / 64 * 64;
+    lt_rows = lt_ld + 16;
+    std::vector<double> lt((size_t)lt_rows * lt_ld, 0.0);
+    for (int32_t p = 0; p < P; ++p)
+      for (int32_t q = 0; q < P; ++q) lt[(size_t)q * lt_ld + p] = Lmat[(size_t)p * P + q];
+    if ((rc = upload(c, s->LT, lt.data(), sizeof(double) * lt.size(), "add_signal L^T"))) {
+      delete s;
+      return rc;
+    }
+    HIPCHK(c, hipStreamSynchronize(c->stream), "add_signal L^T sync");  // lt goes out of scope
+  }
   if (mask && (rc = upload(c, s->mask, mask, (size_t)L.n_toa, "add_signal mask"))) {
     delete s;
     return rc;
@@ -342,6 +358,9 @@ int layout_add_signal(fpta_ctx* c, Layout& L, int32_t kind, int32_t nm, const do
   d.w = s->w.as<double>();
   d.amp = s->amp.as<double>();
   d.L = kind == 1 ? s->L.as<double>() : nullptr;
+  d.LT = kind == 1 ? s->LT.as<double>() : nullptr;
+  d.lt_ld = lt_ld;
+  d.lt_rows = lt_rows;
   d.mask = mask ? s->mask.as<uint8_t>() : nullptr;
   d.w_pstride = kind == 0 ? nmp : 0;
   d.idx = idx;
@@ -415,7 +434,10 @@ int run_coefficients(fpta_ctx* c, Layout& L, uint64_t seed, int64_t real0, int32
     }
     if (d.kind == 1) {
       KTimer kt(c, FPTA_K_MIX);
-      if (P >= kMixTiledMinP && R_pad % 128 == 0)
+      if (P >= kMixTiledMinP && R_pad % 128 == 0 && c->mix_mfma)
+        HIPCHK(c, launch_mix_mfma(c->stream, d, P, R_pad, c->zbuf.as<double>(), c->coef.as<double>(), L.K, x_out),
+               "k_mix_mfma launch");
+      else if (P >= kMixTiledMinP && R_pad % 128 == 0)
         HIPCHK(c, launch_mix_tiled(c->stream, d, P, R_pad, c->zbuf.as<double>(), c->coef.as<double>(), L.K, x_out),
                "k_mix_tiled launch");
       else
@@ -1078,6 +1100,9 @@ int fpta_set_option(fpta_ctx* c, int32_t key, int64_t value) {
     case FPTA_OPT_FUSE_CHECKSUMS:
       c->fuse_sums = value ? 1 : 0;
       return FPTA_OK;
+    case FPTA_OPT_MIX_MFMA:
+      c->mix_mfma = value ? 1 : 0;
+      return FPTA_OK;
     case FPTA_OPT_VALU_VARIANT:
       if (value < 0 || value >= kNumValuVariants) return fail(c, FPTA_EINVAL, "unknown VALU variant");
       c->valu_variant = (int)value;
@@ -1109,6 +1134,7 @@ int fpta_get_option(fpta_ctx* c, int32_t key, int64_t* value) {
     case FPTA_OPT_GRID_SIGMA: *value = c->grid_sigma100; return FPTA_OK;
     case FPTA_OPT_GRID_MFMA: *value = c->grid_mfma; return FPTA_OK;
     case FPTA_OPT_FUSE_CHECKSUMS: *value = c->fuse_sums; return FPTA_OK;
+    case FPTA_OPT_MIX_MFMA: *value = c->mix_mfma; return FPTA_OK;
   }
   return fail(c, FPTA_EINVAL, "get_option: unknown key");
 }

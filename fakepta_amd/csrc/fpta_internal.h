@@ -10,6 +10,8 @@ struct SegDesc {
   const double* w;      // angular frequencies 2*pi*f: kind 0 -> [P][nm], kind 1 -> [nm]
   const double* amp;    // coefficient std-devs sqrt(S*df): same shape as w
   const double* L;      // kind 1: ORF factor [P][P] row-major (x = L z); else null
+  const double* LT;     // kind 1: L transposed, zero-padded [lt_rows][lt_ld] (k_mix_mfma operand); else null
+  int32_t lt_ld, lt_rows;
   const uint8_t* mask;  // [n_toa_total] or null
   int64_t w_pstride;    // nm (kind 0) or 0 (kind 1)
   double idx;           // chromatic index
@@ -128,6 +130,9 @@ hipError_t launch_gen(hipStream_t st, const SegDesc& sd, int32_t seg_id, int32_t
                       int32_t zin_nseg, int32_t zin_nm, double* coef, int32_t K, double* zbuf);
 hipError_t launch_mix(hipStream_t st, const SegDesc& sd, int32_t P, int32_t R_pad, const double* zbuf,
                       double* coef, int32_t K, double* x_out);
+// the same product on v_mfma_f64_16x16x4_f64 (grid_mfma.hip), the large-array path
+hipError_t launch_mix_mfma(hipStream_t st, const SegDesc& sd, int32_t P, int32_t R_pad, const double* zbuf,
+                           double* coef, int32_t K, double* x_out);
 hipError_t launch_mix_tiled(hipStream_t st, const SegDesc& sd, int32_t P, int32_t R_pad, const double* zbuf,
                             double* coef, int32_t K, double* x_out);
 hipError_t launch_epoch_normals(hipStream_t st, int64_t n_blocks, int32_t n_real, int64_t real0, uint32_t k0,

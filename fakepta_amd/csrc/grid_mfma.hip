@@ -310,7 +310,11 @@ __device__ __forceinline__ void interp_store(const SynthArgs& a, double* __restr
           if (pair) v1 += o[1];
         }
         if (vec) {
+#if FPTA_INTERP_DIAG == 3  // diagnostic build only: non-temporal (streaming) stores
+          __builtin_nontemporal_store(dbl2{v0, v1}, (dbl2*)o);
+#else
           *(dbl2*)o = dbl2{v0, v1};
+#endif
         } else {
           o[0] = v0;
           if (pair) o[1] = v1;
@@ -480,6 +484,111 @@ hipError_t launch_grid_interp_mfma(hipStream_t st, const SynthArgs& a, const Gri
   else
     hipLaunchKernelGGL((k_grid_interp_mfma<false, RW>), dim3((unsigned)grid), dim3(256), 0, st, a, band,
                        (int32_t)tiles, R_pad, a.out);
+  return hipGetLastError();
+}
+
+// ----------------------------------------------------------------------------- k_mix_mfma
+// ORF mixing of a common signal on the fp64 matrix cores (large arrays, P >= kMixTiledMinP):
+//   C[p][m] = sum_q L[p][q] Z[q][m],  m = jc R_pad + r (jc = 2 mode + cos/sin), coef[p][col0 + jc][r] = amp C,
+// A = L (pulsar, q) from the zero-padded transpose L^T, B = Z (q, column), D[pulsar][column]. Both operands come
+// in tile pairs from one 16-byte load: lane (lr, lg) loads L^T[q][p0 + 32 u + 2 lr .. + 1] (.x pulsar tile 2u,
+// .y tile 2u + 1) and Z[q][m0 + 32 b + 2 lr .. + 1] (.x column tile 2b, .y tile 2b + 1) for q = q0 + lg. D of
+// (pulsar tile 2u + e, column tile 2b + h): lane (lr, lg) register g = pulsar p0 + 32 u + 2 (lg + 4 g) + e,
+// column m0 + 32 b + 2 lr + h, so one 16-byte store per (lane, pulsar) writes 256 contiguous bytes of a
+// coefficient row. Wave tile 32 NU pulsars x 32 NB columns; workgroup = 4 waves along the columns.
+// Grid: every pulsar tile of a column block runs on one XCD (block b: XCD b % 8), so the block's Z columns
+// (P x 256 doubles) are read from HBM once and served to the other pulsar tiles from that XCD's L2. A lower-
+// triangular factor (Cholesky of a positive-definite ORF) stops the q loop at the tile's last pulsar.
+template <int NU, int NB>
+__global__ __launch_bounds__(256, 2) void k_mix_mfma(const double* __restrict__ LT, int32_t lt_ld,
+                                                     const double* __restrict__ amp, int32_t P, int64_t M,
+                                                     int32_t R_pad, int32_t lower, int32_t n_pt, int32_t n_cb,
+                                                     const double* __restrict__ zbuf, double* __restrict__ coef,
+                                                     int32_t K, int32_t col0, double* __restrict__ x_out) {
+  const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
+  const int cb = (slot / n_pt) * 8 + xcd;
+  const int pt = slot - (slot / n_pt) * n_pt;
+  if (cb >= n_cb) return;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int lr = lane & 15, lg = lane >> 4;
+  const int p0 = pt * 32 * NU;
+  const int64_t m0 = ((int64_t)cb * 4 + wave) * 32 * NB;
+  const int qend = lower ? min(P, p0 + 32 * NU) : P;
+  d4 acc[2 * NU][2 * NB];
+#pragma unroll
+  for (int u = 0; u < 2 * NU; ++u)
+#pragma unroll
+    for (int i = 0; i < 2 * NB; ++i) acc[u][i] = d4{0.0, 0.0, 0.0, 0.0};
+  struct Ops {
+    dbl2 a[NU], b[NB];
+  };
+  // q rows past P: L^T rows are zero there (padding); Z's row is clamped to P - 1 (finite x 0)
+  auto load = [&](int q0, Ops& o) {
+    const int q = q0 + lg;
+    const double* __restrict__ lt = LT + (int64_t)q * lt_ld + p0 + 2 * lr;
+#pragma unroll
+    for (int u = 0; u < NU; ++u) o.a[u] = *(const dbl2*)(lt + 32 * u);
+    const double* __restrict__ z = zbuf + (int64_t)min(q, P - 1) * M + m0 + 2 * lr;
+#pragma unroll
+    for (int b = 0; b < NB; ++b) o.b[b] = *(const dbl2*)(z + 32 * b);
+  };
+  auto mfma = [&](const Ops& o) {
+#pragma unroll
+    for (int u = 0; u < NU; ++u)
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        acc[2 * u][2 * b] = __builtin_amdgcn_mfma_f64_16x16x4f64(o.a[u].x, o.b[b].x, acc[2 * u][2 * b], 0, 0, 0);
+        acc[2 * u][2 * b + 1] = __builtin_amdgcn_mfma_f64_16x16x4f64(o.a[u].x, o.b[b].y, acc[2 * u][2 * b + 1], 0, 0, 0);
+        acc[2 * u + 1][2 * b] = __builtin_amdgcn_mfma_f64_16x16x4f64(o.a[u].y, o.b[b].x, acc[2 * u + 1][2 * b], 0, 0, 0);
+        acc[2 * u + 1][2 * b + 1] =
+            __builtin_amdgcn_mfma_f64_16x16x4f64(o.a[u].y, o.b[b].y, acc[2 * u + 1][2 * b + 1], 0, 0, 0);
+      }
+  };
+  Ops o0, o1;
+  load(0, o0);
+  for (int q0 = 0; q0 < qend; q0 += 8) {
+    load(q0 + 4, o1);
+    mfma(o0);
+    load(q0 + 8, o0);
+    if (q0 + 4 < qend) mfma(o1);
+  }
+#pragma unroll
+  for (int u = 0; u < NU; ++u)
+#pragma unroll
+    for (int e = 0; e < 2; ++e)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int p = p0 + 32 * u + 2 * (lg + 4 * g) + e;
+        if (p >= P) continue;
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+          const int64_t m = m0 + 32 * b + 2 * lr;  // columns m, m + 1 share jc (R_pad is even)
+          const int jc = (int)(m / R_pad);
+          const int r = (int)(m - (int64_t)jc * R_pad);
+          const double a = amp[jc >> 1];
+          const double v0 = acc[2 * u + e][2 * b][g], v1 = acc[2 * u + e][2 * b + 1][g];
+          *(dbl2*)(coef + ((int64_t)p * K + col0 + jc) * R_pad + r) = dbl2{a * v0, a * v1};
+          if (x_out) *(dbl2*)(x_out + (int64_t)p * M + m) = dbl2{v0, v1};
+        }
+      }
+}
+
+constexpr int kMixNU = 2, kMixNB = 2;  // k_mix_mfma wave tile: 64 pulsars x 64 columns
+
+hipError_t launch_mix_mfma(hipStream_t st, const SegDesc& sd, int32_t P, int32_t R_pad, const double* zbuf,
+                           double* coef, int32_t K, double* x_out) {
+  const int64_t M = (int64_t)2 * sd.nm * R_pad;  // a multiple of 256: R_pad is a multiple of 128
+  constexpr int kCols = 4 * 32 * kMixNB, kRows = 32 * kMixNU;
+  if (P <= 0 || !sd.LT || M % kCols != 0) return hipErrorInvalidValue;
+  const int64_t n_cb = M / kCols;
+  const int32_t n_pt = (P + kRows - 1) / kRows;
+  // operand loads stay inside L^T: pulsar columns up to n_pt * kRows, q rows up to the last k-step's + 4
+  if (sd.lt_ld < n_pt * kRows || sd.lt_rows < (P + 7) / 8 * 8 + 4) return hipErrorInvalidValue;
+  const int64_t blocks = (n_cb + 7) / 8 * 8 * n_pt;
+  if (blocks > 0x7FFFFFFF || n_cb > 0x7FFFFFFF) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((k_mix_mfma<kMixNU, kMixNB>), dim3((unsigned)blocks), dim3(256), 0, st, sd.LT, sd.lt_ld, sd.amp,
+                     P, M, R_pad, sd.l_lower, n_pt, (int32_t)n_cb, zbuf, coef, K, sd.col0, x_out);
   return hipGetLastError();
 }
 

@@ -418,9 +418,13 @@ def test_batch_split_invariance_bitwise(ctx):
     np.testing.assert_array_equal(full, again)
 
 
+@pytest.mark.parametrize("mix_mfma", [1, 0], ids=["mfma", "valu"])
 @pytest.mark.parametrize("factor", ["cholesky", "svd"])
-def test_tiled_mix_vs_oracle(ctx, factor):
-    """P >= 64 takes the tiled GEMM mix (triangular when L is a Cholesky factor)."""
+def test_tiled_mix_vs_oracle(ctx, capi, factor, mix_mfma):
+    """P >= 64 takes the GEMM mix: k_mix_mfma (default) or the register-tiled VALU k_mix_tiled
+    (FPTA_OPT_MIX_MFMA 0), triangular when L is a Cholesky factor; P = 150 is not a multiple of the 64-pulsar
+    tile. Both against the oracle, and the two mixes' coefficients against each other."""
+    ctx.set_option(capi.OPT_MIX_MFMA, mix_mfma)
     from fakepta_amd.batch import batch_factor
     rng = np.random.default_rng(21)
     P = 150
@@ -434,10 +438,17 @@ def test_tiled_mix_vs_oracle(ctx, factor):
     f2, a2 = per_psr_signal(rng, offs, toas, 5)
     ctx.batch_add_signal(0, f2, a2, idx=4.0)
     segs = [O.Segment(1, 2 * np.pi * f, amp, 0.0, L=L), O.Segment(0, 2 * np.pi * f2, a2, 4.0)]
-    for real0, R in ((0, 130), (77, 5)):
-        got = ctx.batch_synth(31, real0, R)
-        want = O.batch_synth(offs, toas, nu, segs, 31, real0, R)
-        assert_parity(got, want, TOL)
+    try:
+        for real0, R in ((0, 130), (77, 5)):
+            got = ctx.batch_synth(31, real0, R)
+            want = O.batch_synth(offs, toas, nu, segs, 31, real0, R)
+            assert_parity(got, want, TOL)
+        _, co = ctx.batch_synth(31, 0, 130, coeffs=True)
+        ctx.set_option(capi.OPT_MIX_MFMA, 1 - mix_mfma)
+        _, co_other = ctx.batch_synth(31, 0, 130, coeffs=True)
+        assert_parity(co, co_other, 1e-13)
+    finally:
+        ctx.set_option(capi.OPT_MIX_MFMA, 1)
 
 
 def test_checksums_device(ctx):
