@@ -162,6 +162,20 @@ struct fpta_ctx {
   int fuse_white = 1;    // add white/ECORR in the seeded kernel's epilogue
   int fuse_sums = 0;     // gridded path: interpolation writes partial checksums (FPTA_OPT_FUSE_CHECKSUMS)
   int mix_mfma = 1;      // ORF mixing of large arrays on fp64 MFMA (k_mix_mfma) or VALU (k_mix_tiled)
+  // batch coefficients on a side stream (FPTA_OPT_OVERLAP): gen / mix of signal i run there and signal i's
+  // consumer on the ctx stream waits for ev_sig[i] only, so the gridded DFT of one signal overlaps the draws of
+  // the next (VALU Philox beside fp64 MFMA). ev_begin orders the side stream after everything queued before.
+  int overlap = 1;
+  hipStream_t side = nullptr;
+  hipEvent_t ev_begin = nullptr;
+  std::vector<hipEvent_t> ev_sig;
+  bool coef_side = false;  // the last coefficients were made on the side stream and are not all waited for
+  // recorded on the ctx stream right after the last reader of the coefficient buffer was queued (the gridded
+  // DFT, or the coefficient download): the next block's draws wait for it instead of for the whole previous
+  // block, so they overlap that block's interpolation
+  hipEvent_t ev_coef_free = nullptr;
+  bool coef_free_set = false;
+  bool coef_copy_pending = false;  // the block's coefficients are still to be downloaded after the synthesis
   DevBuf part, part_tmp; // partial checksums [n_chunks][R_pad][2] of the last block, reduction scratch
   bool part_ready = false;  // part holds the partials of the current block (c->out, out_R)
   int32_t part_chunks = 0, part_rpad = 0;
@@ -234,17 +248,18 @@ hipEvent_t get_event(fpta_ctx* c) {
 struct KTimer {
   fpta_ctx* c;
   int which;
+  hipStream_t st;
   hipEvent_t a = nullptr, b = nullptr;
-  KTimer(fpta_ctx* c_, int w) : c(c_), which(w) {
+  KTimer(fpta_ctx* c_, int w, hipStream_t s = nullptr) : c(c_), which(w), st(s ? s : c_->stream) {
     if (c->profile) {
       a = get_event(c);
       b = get_event(c);
-      if (a) (void)hipEventRecord(a, c->stream);
+      if (a) (void)hipEventRecord(a, st);
     }
   }
   ~KTimer() {
     if (c->profile && a && b) {
-      (void)hipEventRecord(b, c->stream);
+      (void)hipEventRecord(b, st);
       c->pending.push_back({which, a, b});
     }
   }
@@ -414,9 +429,43 @@ int layout_finalize(fpta_ctx* c, Layout& L) {
 int32_t pad_to(int32_t x, int32_t m) { return (x + m - 1) / m * m; }
 
 // Draw + mix every segment into c->coef [P][K][R_pad].
+// The ctx stream waits for signal i's coefficients (side-stream draws), or for all of them.
+int wait_coef(fpta_ctx* c, size_t i) {
+  if (c->coef_side && i < c->ev_sig.size()) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_sig[i], 0), "coef wait");
+  return FPTA_OK;
+}
+int wait_coef_all(fpta_ctx* c) {
+  if (!c->coef_side) return FPTA_OK;
+  for (size_t i = 0; i < c->ev_sig.size(); ++i) {
+    int rc = wait_coef(c, i);
+    if (rc) return rc;
+  }
+  c->coef_side = false;
+  return FPTA_OK;
+}
+
 int run_coefficients(fpta_ctx* c, Layout& L, uint64_t seed, int64_t real0, int32_t R, int32_t R_pad,
-                     const double* zin, int32_t zin_nm, double* x_out) {
+                     const double* zin, int32_t zin_nm, double* x_out, bool side = false) {
   const int32_t P = L.P;
+  int rc0 = wait_coef_all(c);  // a previous block's draws are fully ordered before this one's
+  if (rc0) return rc0;
+  hipStream_t st = c->stream;
+  if (!(side && L.segs.size() > 1)) c->coef_free_set = false;  // coef is written on the ctx stream from here on
+  if (side && L.segs.size() > 1) {
+    if (!c->side) HIPCHK(c, hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking), "side stream create");
+    if (!c->ev_begin) HIPCHK(c, hipEventCreateWithFlags(&c->ev_begin, hipEventDisableTiming), "event create");
+    while (c->ev_sig.size() < L.segs.size()) {
+      hipEvent_t e = nullptr;
+      HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming), "event create");
+      c->ev_sig.push_back(e);
+    }
+    // the previous block's last reader of coef (its DFT or download) comes first; without one recorded,
+    // everything queued on the ctx stream
+    if (!c->coef_free_set) HIPCHK(c, hipEventRecord(c->ev_begin, c->stream), "event record");
+    HIPCHK(c, hipStreamWaitEvent(c->side, c->coef_free_set ? c->ev_coef_free : c->ev_begin, 0), "side wait");
+    c->coef_free_set = false;
+    st = c->side;
+  }
   HIPCHK(c, c->coef.ensure(sizeof(double) * (size_t)P * std::max(L.K, 1) * R_pad), "coef alloc");
   size_t zb = 0;
   for (Seg* s : L.segs)
@@ -426,25 +475,27 @@ int run_coefficients(fpta_ctx* c, Layout& L, uint64_t seed, int64_t real0, int32
   for (size_t i = 0; i < L.segs.size(); ++i) {
     const SegDesc& d = L.segs[i]->d;
     {
-      KTimer kt(c, FPTA_K_GEN);
+      KTimer kt(c, FPTA_K_GEN, st);
       HIPCHK(c,
-             launch_gen(c->stream, d, (int32_t)i, P, R, R_pad, real0, k0, k1, zin, (int32_t)L.segs.size(),
-                        zin_nm, c->coef.as<double>(), L.K, c->zbuf.as<double>()),
+             launch_gen(st, d, (int32_t)i, P, R, R_pad, real0, k0, k1, zin, (int32_t)L.segs.size(), zin_nm,
+                        c->coef.as<double>(), L.K, c->zbuf.as<double>()),
              "k_gen launch");
     }
     if (d.kind == 1) {
-      KTimer kt(c, FPTA_K_MIX);
+      KTimer kt(c, FPTA_K_MIX, st);
       if (P >= kMixTiledMinP && R_pad % 128 == 0 && c->mix_mfma)
-        HIPCHK(c, launch_mix_mfma(c->stream, d, P, R_pad, c->zbuf.as<double>(), c->coef.as<double>(), L.K, x_out),
+        HIPCHK(c, launch_mix_mfma(st, d, P, R_pad, c->zbuf.as<double>(), c->coef.as<double>(), L.K, x_out),
                "k_mix_mfma launch");
       else if (P >= kMixTiledMinP && R_pad % 128 == 0)
-        HIPCHK(c, launch_mix_tiled(c->stream, d, P, R_pad, c->zbuf.as<double>(), c->coef.as<double>(), L.K, x_out),
+        HIPCHK(c, launch_mix_tiled(st, d, P, R_pad, c->zbuf.as<double>(), c->coef.as<double>(), L.K, x_out),
                "k_mix_tiled launch");
       else
-        HIPCHK(c, launch_mix(c->stream, d, P, R_pad, c->zbuf.as<double>(), c->coef.as<double>(), L.K, x_out),
+        HIPCHK(c, launch_mix(st, d, P, R_pad, c->zbuf.as<double>(), c->coef.as<double>(), L.K, x_out),
                "k_mix launch");
     }
+    if (st != c->stream) HIPCHK(c, hipEventRecord(c->ev_sig[i], st), "event record");
   }
+  c->coef_side = st != c->stream;
   return FPTA_OK;
 }
 
@@ -748,10 +799,32 @@ int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad) {
       g.col0 = d.col0;
       g.ntab = gs->ntab;
     }
-    HIPCHK(c,
-           (c->grid_mfma & 1) ? launch_grid_dft_mfma(c->stream, gsegs, L.P, a.coef, a.K, R_pad)
-                              : launch_grid_dft(c->stream, gsegs, L.P, a.coef, a.K, R_pad),
-           "k_grid_dft launch");
+    const bool early_free = c->coef_side && !c->coef_copy_pending;
+    if (c->coef_side) {
+      // one DFT launch per signal, each after that signal's draws only (they run on the side stream)
+      for (int32_t s = 0; s < gsegs.n; ++s) {
+        GridSegs one{};
+        one.s[0] = gsegs.s[s];
+        one.n = 1;
+        int rc = wait_coef(c, (size_t)s);
+        if (rc) return rc;
+        HIPCHK(c,
+               (c->grid_mfma & 1) ? launch_grid_dft_mfma(c->stream, one, L.P, a.coef, a.K, R_pad)
+                                  : launch_grid_dft(c->stream, one, L.P, a.coef, a.K, R_pad),
+               "k_grid_dft launch");
+      }
+      c->coef_side = false;
+    } else {
+      HIPCHK(c,
+             (c->grid_mfma & 1) ? launch_grid_dft_mfma(c->stream, gsegs, L.P, a.coef, a.K, R_pad)
+                                : launch_grid_dft(c->stream, gsegs, L.P, a.coef, a.K, R_pad),
+             "k_grid_dft launch");
+    }
+    if (early_free) {  // the DFT was the last reader of coef: the next block may draw during the interpolation
+      if (!c->ev_coef_free) HIPCHK(c, hipEventCreateWithFlags(&c->ev_coef_free, hipEventDisableTiming), "event create");
+      HIPCHK(c, hipEventRecord(c->ev_coef_free, c->stream), "event record");
+      c->coef_free_set = true;
+    }
   }
   // partial checksums of a batch block (written into the context's own block, not accumulated)
   if (c->fuse_sums && a.out == c->out.as<double>() && !a.accumulate) {
@@ -849,6 +922,10 @@ int run_synth(fpta_ctx* c, Layout& L, int32_t R, int32_t R_pad, double* out, int
   if (c->coef.cap < sizeof(double) * (size_t)L.P * std::max(L.K, 1) * R_pad)
     return fail(c, FPTA_ESTATE, "synth: coefficient buffer smaller than P*K*R_pad");
   c->last_path = path;
+  if (path != 4) {
+    int rc = wait_coef_all(c);  // only the gridded DFT consumes side-stream draws signal by signal
+    if (rc) return rc;
+  }
   if (path == 4) {
     if (white && white->on && c->fuse_white) {
       a.w_on = 1;
@@ -1068,6 +1145,13 @@ int fpta_destroy(fpta_ctx* c) {
     (void)hipEventDestroy(p.b);
   }
   for (auto e : c->pool) (void)hipEventDestroy(e);
+  if (c->side) {
+    (void)hipStreamSynchronize(c->side);
+    (void)hipStreamDestroy(c->side);
+  }
+  if (c->ev_begin) (void)hipEventDestroy(c->ev_begin);
+  if (c->ev_coef_free) (void)hipEventDestroy(c->ev_coef_free);
+  for (auto e : c->ev_sig) (void)hipEventDestroy(e);
   (void)hipStreamDestroy(c->stream);
   delete c;
   return FPTA_OK;
@@ -1103,6 +1187,9 @@ int fpta_set_option(fpta_ctx* c, int32_t key, int64_t value) {
     case FPTA_OPT_MIX_MFMA:
       c->mix_mfma = value ? 1 : 0;
       return FPTA_OK;
+    case FPTA_OPT_OVERLAP:
+      c->overlap = value ? 1 : 0;
+      return FPTA_OK;
     case FPTA_OPT_VALU_VARIANT:
       if (value < 0 || value >= kNumValuVariants) return fail(c, FPTA_EINVAL, "unknown VALU variant");
       c->valu_variant = (int)value;
@@ -1135,6 +1222,7 @@ int fpta_get_option(fpta_ctx* c, int32_t key, int64_t* value) {
     case FPTA_OPT_GRID_MFMA: *value = c->grid_mfma; return FPTA_OK;
     case FPTA_OPT_FUSE_CHECKSUMS: *value = c->fuse_sums; return FPTA_OK;
     case FPTA_OPT_MIX_MFMA: *value = c->mix_mfma; return FPTA_OK;
+    case FPTA_OPT_OVERLAP: *value = c->overlap; return FPTA_OK;
   }
   return fail(c, FPTA_EINVAL, "get_option: unknown key");
 }
@@ -1489,7 +1577,8 @@ static int batch_common(fpta_ctx* c, uint64_t seed, int64_t real0, int32_t n_rea
   if (L.segs.empty()) {
     HIPCHK(c, hipMemsetAsync(c->out.p, 0, out_bytes, c->stream), "out memset");
   } else {
-    if ((rc = run_coefficients(c, L, seed, real0, n_real, R_pad, zin, zin_nm, nullptr))) return rc;
+    c->coef_copy_pending = coeffs_out != nullptr;
+    if ((rc = run_coefficients(c, L, seed, real0, n_real, R_pad, zin, zin_nm, nullptr, c->overlap != 0))) return rc;
     if ((rc = run_synth(c, L, n_real, R_pad, c->out.as<double>(), L.n_toa, 0, true, do_white ? &wc : nullptr,
                         &fused)))
       return rc;

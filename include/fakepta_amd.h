@@ -262,6 +262,9 @@ int fpta_multi_synth(fpta_multi* m, uint64_t seed, int64_t real0, int64_t n_real
                                      always take the full pass. */
 #define FPTA_OPT_MIX_MFMA 11      /* ORF mixing of common signals for P >= 64 pulsars: 1 (default) on fp64 MFMA
                                      (k_mix_mfma), 0 the register-tiled fp64 VALU GEMM (k_mix_tiled) */
+#define FPTA_OPT_OVERLAP 12       /* batch synthesis with several signals: 1 (default) draws each signal's
+                                     coefficients on a second stream so the gridded DFT of one signal overlaps
+                                     the draws of the next; 0 one stream. Results are identical. */
 int fpta_set_option(fpta_ctx* ctx, int32_t key, int64_t value);
 /* Current value of option `key` (same keys as fpta_set_option). */
 int fpta_get_option(fpta_ctx* ctx, int32_t key, int64_t* value);

@@ -244,3 +244,38 @@ def test_c2_full_size_gridded_vs_seeded(ctx, capi):
             want[sl] += ch * (np.cos(ph) @ a[0::2] + np.sin(ph) @ a[1::2])
         col += 2 * s.n_modes
     assert_parity(grid[1], want, TOL)
+
+
+@pytest.mark.parametrize("path", [4, 3, 1])
+def test_side_stream_draws_are_bitwise_identical(ctx, capi, shipped, path):
+    """FPTA_OPT_OVERLAP: coefficients drawn on the side stream (consumers wait per signal) give bit-identical
+    blocks and coefficients to the single-stream order, on the gridded, exact and direct paths, across
+    consecutive batches (the side stream must not overwrite a block's coefficients while it is still read)."""
+    rng = np.random.default_rng(31)
+    offs, toas, nu = random_layout(rng, 70, (40, 120))
+    ctx.batch_set_toas(offs, toas, nu)
+    f, a = per_psr_signal(rng, offs, toas, 30)
+    ctx.batch_add_signal(0, f, a, idx=0.0)
+    f, a = per_psr_signal(rng, offs, toas, 50)
+    ctx.batch_add_signal(0, f, a, idx=2.0)
+    f, a, L, _ = common_signal(rng, offs, toas, 20)
+    ctx.batch_add_signal(1, f, a, L=L)
+    try:
+        ctx.set_option(capi.OPT_SYNTH_PATH, path)
+        runs, blocks = {}, {}
+        for ov in (0, 1):
+            ctx.set_option(capi.OPT_OVERLAP, ov)
+            runs[ov] = [ctx.batch_synth(99, r0, 200, coeffs=True) for r0 in (0, 200, 400)]
+            # device-only batches back to back: the next block's draws overlap this block's interpolation
+            blk = []
+            for r0 in (600, 800, 1000, 1200):
+                ctx.batch_synth(99, r0, 200, to_host=False)
+                blk.append(ctx.batch_download(0, 200))
+            blocks[ov] = blk
+        for (o0, c0), (o1, c1) in zip(runs[0], runs[1]):
+            np.testing.assert_array_equal(o0, o1)
+            np.testing.assert_array_equal(c0, c1)
+        for b0, b1 in zip(blocks[0], blocks[1]):
+            np.testing.assert_array_equal(b0, b1)
+    finally:
+        ctx.set_options(shipped)
