@@ -46,7 +46,7 @@ constexpr int kInterpWPC = FPTA_INTERP_WPC;
 // is zero-padded to ntab (multiple of 8) modes and lde (multiple of 16 MJ) rows; padded coefficient modes
 // re-read the signal's last mode (finite) against zero table rows.
 template <int MJ, int MR>
-__global__ __launch_bounds__(256, 2) void k_grid_dft_mfma(GridSegs gsegs, const double* __restrict__ coef,
+__global__ __launch_bounds__(256, 3) void k_grid_dft_mfma(GridSegs gsegs, const double* __restrict__ coef,
                                                           int32_t K, int32_t R_pad) {
   static_assert(MJ % 2 == 0 && MR % 2 == 0, "operands come in tile pairs");
   constexpr int PJ = MJ / 2, PR = MR / 2;
@@ -387,6 +387,10 @@ __global__ __launch_bounds__(256, FPTA_INTERP_WPC) void k_grid_interp_mfma(Synth
 
   int tile = x * per + (int)(blockIdx.x >> 3);
   if (tile >= end) return;
+#if FPTA_INTERP_DIAG == 5  // diagnostic build only: every other workgroup starts half a tile late (phase stagger)
+  if ((blockIdx.x >> 3) & 1)
+    for (int i = 0; i < 2; ++i) __builtin_amdgcn_s_sleep(127);
+#endif
   InterpTile<RW> cur;
   setup(tile, cur);
   if (cur.r0 >= R_pad) return;  // this wave's realization block is padding for every tile of the launch
@@ -400,7 +404,11 @@ __global__ __launch_bounds__(256, FPTA_INTERP_WPC) void k_grid_interp_mfma(Synth
 #pragma unroll
       for (int i = 0; i < RW; ++i) acc[e][i] = d4{0.0, 0.0, 0.0, 0.0};
     // steps q (in a0) and q + 1 (in a1) are loaded; each set is refilled two steps ahead right after its MFMAs
+#if FPTA_INTERP_DIAG == 4  // diagnostic build only: no band loop (the epilogue stores zeros): the store stream alone
+    for (int q = cur.nq; q < cur.nq; q += 2) {
+#else
     for (int q = 0; q < cur.nq; q += 2) {
+#endif
       __builtin_amdgcn_sched_barrier(0);
       mfma(a0, b0);
       __builtin_amdgcn_sched_barrier(0);

@@ -27,6 +27,7 @@ def main():
     psrs = bench.build_array(100, 2000, "c2")
     sim = BatchSimulator(psrs, white=False, ctx=ctx)
     ctx.set_option(_capi.OPT_SYNTH_PATH, 4)
+    ctx.set_option(_capi.OPT_OVERLAP, 0)  # the kernels alone (no co-running draws of the next batch)
     if args.grid_mfma >= 0:
         ctx.set_option(_capi.OPT_GRID_MFMA, args.grid_mfma)
     if args.width:

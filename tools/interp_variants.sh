@@ -1,12 +1,13 @@
 #!/bin/bash
 # Build (build) or time (run) compile-time variants of k_grid_interp_mfma: realization tiles per wave (RW),
 # persistent workgroups per CU (WPC), diagnostic cuts (DIAG 1: grid loads from one L1-resident row; 2: no
-# stores; 3: non-temporal stores). VARIANTS entries are RW:WPC:DIAG. Throwaway libraries in build/diag, loaded by tools/interp_diag.py
+# stores; 3: non-temporal stores; 4: no band loop, the store stream alone; 5: every other workgroup starts
+# ~7 us late). VARIANTS entries are RW:WPC:DIAG. Throwaway libraries in build/diag, loaded by tools/interp_diag.py
 # through FAKEPTA_AMD_LIB; never the product or the bench. Results: profiles/r02_interp_diag*.txt (a single
 # operand set at 3 workgroups per CU measured 0.70 ms against 0.66 for the shipped 2-deep pipeline at 2).
 S=fakepta_amd/csrc
 D=build/diag
-VARIANTS="8:2:0 8:2:3 8:2:2"
+VARIANTS="8:2:0 8:2:5"
 if [ "$1" = build ]; then
   mkdir -p $D
   for v in $VARIANTS; do
