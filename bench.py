@@ -35,7 +35,7 @@ FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 matrix (= vector) peak, AMD datasheet (M
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 SYNTH_KERNELS = {3: ("k_synth_valu_seeded<2,16>", "fp64-valu"), 2: ("k_synth_mfma<4,2>", "fp64-mfma"),
                  1: ("k_synth_direct", "fp64-valu")}
-GRID_INTERP = ("k_grid_interp_mfma<8>", "fp64-mfma")
+GRID_INTERP = ("k_grid_interp_mfma<false, false, 8>", "fp64-mfma")
 # layout tag of the gridded plan a PMC traffic record must carry to describe the shipped interpolation kernel
 # (32-TOA chunks, every signal's band back to back); untagged records describe round-1 kernels of the same name
 GRID_LAYOUT = "band32"

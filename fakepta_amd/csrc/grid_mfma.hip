@@ -225,60 +225,81 @@ __device__ __forceinline__ void interp_white(const SynthArgs& a, const InterpTil
   }
 }
 
-// Sum of x over the 16 lanes of a DPP row (the lanes lr = 0..15 of one lane group): every lane ends with the
-// row's sum, added in the same order whatever realization the row holds (rotations by 8, 4, 2, 1; 64-bit values
-// move as two 32-bit halves).
-template <int N>
-__device__ __forceinline__ double row_ror(double x) {
-  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(x), 0x120 + N, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(x), 0x120 + N, 0xF, 0xF, false);
+// 64-bit DPP move within a row of 16 lanes (two 32-bit halves); CTRL: row_mirror 0x140 (lane l <- 15 - l),
+// row_half_mirror 0x141 (l <- 7 - l within each 8), quad_perm 0x4E (l <- l ^ 2), 0xB1 (l <- l ^ 1). Every pairing
+// is symmetric, so each step of a reduce-scatter exchanges complementary halves between two lanes.
+template <int CTRL>
+__device__ __forceinline__ double dpp64(double x) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(x), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(x), CTRL, 0xF, 0xF, false);
   return __hiloint2double(hi, lo);
 }
-__device__ __forceinline__ double row_sum16(double x) {
-  x += row_ror<8>(x);
-  x += row_ror<4>(x);
-  x += row_ror<2>(x);
-  x += row_ror<1>(x);
-  return x;
+
+// One reduce-scatter step: the lane keeps half `up` (0: x[0 .. H), 1: x[H .. 2H)) of its 2H values plus the
+// partner's copy of that half, and hands the partner the other half.
+template <int CTRL, int H>
+__device__ __forceinline__ void rs_step(double (&x)[2 * H], bool up) {
+#pragma unroll
+  for (int j = 0; j < H; ++j) {
+    const double keep = up ? x[j + H] : x[j], send = up ? x[j] : x[j + H];
+    x[j] = keep + dpp64<CTRL>(send);
+  }
 }
 
+// Partial checksums of the tile's chunk, after its stores (the accumulators then die as the first
+// reduce-scatter step consumes them).
 template <int RW>
-__device__ __forceinline__ void interp_store(const SynthArgs& a, double* __restrict__ out, const InterpTile<RW>& t,
-                                             const d4 (&acc)[2][RW]) {
+__device__ __forceinline__ void interp_partials(const SynthArgs& a, const InterpTile<RW>& t, const d4 (&acc)[2][RW]) {
   const int lane = threadIdx.x & 63;
   const int lr = lane & 15, lg = lane >> 4;
-  const int tt = 2 * lr;  // this lane's even TOA in the chunk; tt + 1 the odd one
-  if (a.part) {
+  const int tt = 2 * lr;
+  {
     // partial checksums of this chunk: per realization the sum and sum of squares over the chunk's TOAs (lanes
-    // without a TOA add 0). After the row sums every lane of a row holds all of them; lane lr = 4 m + g then
-    // writes the adjacent realizations of tiles (2m, 2m + 1) at register g: two 16-byte stores per lane, two
-    // store instructions per wave (one lane per realization would take RW * 4)
+    // without a TOA add 0), reduced over the 16 lanes of each row by a reduce-scatter (row_mirror, half_mirror,
+    // xor 2, xor 1). Value k = 2 c + {0: sum, 1: sumsq} of combination c = 2 (4 m + g) + h (tile 2m + h,
+    // register g); lane lr ends with k in [4 lr, 4 lr + 4): the realization pair of tiles (2m, 2m + 1) at
+    // register g for m = lr >> 2, g = lr & 3, stored with two 16-byte stores (two store instructions per wave)
     static_assert(RW == 8, "16 lanes of a row = 4 realization pairs x 4 registers");
     double* __restrict__ pp = a.part + ((int64_t)t.c * a.R_pad + t.r0) * 2;
     const bool ok0 = tt < t.cnt, ok1 = tt + 1 < t.cnt;
-    const int mm = lr >> 2, gg = lr & 3;
-    double s0 = 0.0, q0 = 0.0, s1 = 0.0, q1 = 0.0;
+    double x[32];
+    {
+      // first step straight from the accumulators (the 64 values are never all live): lanes 8..15 keep
+      // combinations 16..31, lanes 0..7 combinations 0..15
+      const bool up = lr >= 8;
 #pragma unroll
-    for (int i = 0; i < RW; ++i) {
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const double v0 = ok0 ? acc[0][i][g] : 0.0, v1 = ok1 ? acc[1][i][g] : 0.0;
-        const double sv = row_sum16(v0 + v1), qv = row_sum16(fma(v0, v0, v1 * v1));
-        if ((i >> 1) == mm && g == gg) {
-          if (i & 1) {
-            s1 = sv;
-            q1 = qv;
-          } else {
-            s0 = sv;
-            q0 = qv;
-          }
-        }
+      for (int j = 0; j < 32; ++j) {
+        const int k0 = j, k1 = j + 32;  // the two values of this slot: kept or sent
+        auto value = [&](int k) {
+          const int c = k >> 1, h = c & 1, mg = c >> 1, m = mg >> 2, g = mg & 3;
+          const double v0 = ok0 ? acc[0][2 * m + h][g] : 0.0, v1 = ok1 ? acc[1][2 * m + h][g] : 0.0;
+          return (k & 1) ? fma(v0, v0, v1 * v1) : v0 + v1;
+        };
+        const double lo = value(k0), hi = value(k1);
+        x[j] = (up ? hi : lo) + dpp64<0x140>(up ? lo : hi);
       }
     }
+    {
+      double (&y)[32] = x;
+      rs_step<0x141, 16>(y, (lr & 7) >= 4);
+      double (&z)[16] = *reinterpret_cast<double(*)[16]>(&y[0]);
+      rs_step<0x4E, 8>(z, (lr & 3) >= 2);
+      double (&w)[8] = *reinterpret_cast<double(*)[8]>(&z[0]);
+      rs_step<0xB1, 4>(w, (lr & 1) != 0);
+    }
+    const int mm = lr >> 2, gg = lr & 3;
     const int rl = 32 * mm + 2 * (lg + 4 * gg);  // realization of (tile 2mm, register gg); rl + 1: tile 2mm + 1
-    *(dbl2*)(pp + 2 * rl) = dbl2{s0, q0};
-    *(dbl2*)(pp + 2 * rl + 2) = dbl2{s1, q1};
+    *(dbl2*)(pp + 2 * rl) = dbl2{x[0], x[1]};
+    *(dbl2*)(pp + 2 * rl + 2) = dbl2{x[2], x[3]};
   }
+}
+
+template <int RW>
+__device__ __forceinline__ void interp_store_rows(const SynthArgs& a, double* __restrict__ out,
+                                                  const InterpTile<RW>& t, const d4 (&acc)[2][RW]) {
+  const int lane = threadIdx.x & 63;
+  const int lr = lane & 15, lg = lane >> 4;
+  const int tt = 2 * lr;  // this lane's even TOA in the chunk; tt + 1 the odd one
   if (tt >= t.cnt) return;
   const int64_t tg = a.offs[t.p] + t.y + tt;
 #if FPTA_INTERP_DIAG == 2  // diagnostic build only: no stores (one conditional store keeps every sum live)
@@ -324,13 +345,21 @@ __device__ __forceinline__ void interp_store(const SynthArgs& a, double* __restr
   }
 }
 
+// The tile's epilogue: its block rows, then (FPTA_OPT_FUSE_CHECKSUMS) its partial checksums.
+template <bool PART, int RW>
+__device__ __forceinline__ void interp_store(const SynthArgs& a, double* __restrict__ out, const InterpTile<RW>& t,
+                                             const d4 (&acc)[2][RW]) {
+  interp_store_rows<RW>(a, out, t, acc);
+  if constexpr (PART) interp_partials<RW>(a, t, acc);
+}
+
 // Persistent launch: gridDim.x (a multiple of 8) workgroups, about as many as are co-resident; workgroup
 // b runs on XCD b % 8 and walks that XCD's contiguous range of tiles (consecutive chunks: their grid rows
 // overlap, so they stay in the XCD's L2). One tile per short-lived workgroup instead left the CUs mostly
 // empty (SQ_WAVE_CYCLES ~ 0.7 resident waves per SIMD): workgroup dispatch, not the memory system, paced it.
 // Every wave of a workgroup walks the same tiles (its own 16 RW realizations of each); a wave whose realization
 // block lies past R_pad exits at once (no barrier in the kernel).
-template <bool WHITE, int RW>
+template <bool WHITE, bool PART, int RW>
 __global__ __launch_bounds__(256, FPTA_INTERP_WPC) void k_grid_interp_mfma(SynthArgs a, GridBand band, int32_t n_tiles,
                                                                          int32_t R_pad, double* __restrict__ out) {
   static_assert(RW % 2 == 0, "realization tiles come in pairs");
@@ -425,7 +454,7 @@ __global__ __launch_bounds__(256, FPTA_INTERP_WPC) void k_grid_interp_mfma(Synth
       // the Philox rounds of the white epilogue and a second tile's operands do not fit in the register budget
       // together: this variant stores first, then starts the next tile
       interp_white<RW>(a, cur, acc);
-      interp_store<RW>(a, out, cur, acc);
+      interp_store<PART, RW>(a, out, cur, acc);
       tile += stride;
       if (tile >= end) break;
       setup(tile, cur);
@@ -442,7 +471,7 @@ __global__ __launch_bounds__(256, FPTA_INTERP_WPC) void k_grid_interp_mfma(Synth
         load(nxt, min(1, nxt.nq - 1), a1, b1);
       }
       __builtin_amdgcn_sched_barrier(0);
-      interp_store<RW>(a, out, cur, acc);
+      interp_store<PART, RW>(a, out, cur, acc);
       if (!more) break;
       cur = nxt;
     }
@@ -486,12 +515,10 @@ hipError_t launch_grid_interp_mfma(hipStream_t st, const SynthArgs& a, const Gri
   // 2 -> 0.74, 3 -> 0.81; 32-TOA tiles: profiles/r02_interp_variants.txt)
   const int64_t want = (int64_t)n_cu * kInterpWPC;
   const int64_t grid = std::min<int64_t>((tiles + 7) / 8 * 8, (want + 7) / 8 * 8);
-  if (a.w_on)
-    hipLaunchKernelGGL((k_grid_interp_mfma<true, RW>), dim3((unsigned)grid), dim3(256), 0, st, a, band,
-                       (int32_t)tiles, R_pad, a.out);
-  else
-    hipLaunchKernelGGL((k_grid_interp_mfma<false, RW>), dim3((unsigned)grid), dim3(256), 0, st, a, band,
-                       (int32_t)tiles, R_pad, a.out);
+  // partial checksums are a separate instantiation: their reduce-scatter registers never weigh on the plain kernel
+  auto kernel = a.w_on ? (a.part ? k_grid_interp_mfma<true, true, RW> : k_grid_interp_mfma<true, false, RW>)
+                       : (a.part ? k_grid_interp_mfma<false, true, RW> : k_grid_interp_mfma<false, false, RW>);
+  hipLaunchKernelGGL(kernel, dim3((unsigned)grid), dim3(256), 0, st, a, band, (int32_t)tiles, R_pad, a.out);
   return hipGetLastError();
 }
 

@@ -26,5 +26,5 @@ cat ${o}_bench_c3.log
 timeout -k 10 300 python -u bench.py --path 3 --cpu-sample 0 > ${o}_bench_exact.log 2>&1 || { tail -20 ${o}_bench_exact.log; exit 1; }
 timeout -k 10 300 python -u tools/bench_configs.py c1 c3 c4 c5 > ${o}_configs.jsonl 2>&1 || { tail -20 ${o}_configs.jsonl; exit 1; }
 cat ${o}_configs.jsonl
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d ${o}_prof -o run -- python bench.py --steps 20 --cpu-sample 0 --exact-launches 0 > ${o}_prof.log 2>&1 || { tail -20 ${o}_prof.log; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d ${o}_prof -o run -- python bench.py --steps 20 --cpu-sample 0 --exact-launches 0 > ${o}_prof.log 2>&1 || { tail -20 ${o}_prof.log; exit 1; }
 find ${o}_prof -name "*kernel_stats.csv"
