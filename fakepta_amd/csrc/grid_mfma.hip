@@ -374,8 +374,11 @@ __global__ __launch_bounds__(256, FPTA_INTERP_WPC) void k_grid_interp_mfma(Synth
   const int lr = lane & 15, lg = lane >> 4;
 
   auto setup = [&](int tile, InterpTile<RW>& t) {
-    const int rb = __builtin_amdgcn_readfirstlane(tile / band.n_chunks);  // realization block of 64 RW
-    t.c = __builtin_amdgcn_readfirstlane(tile - rb * band.n_chunks);
+    // chunk-major tiles: the realization blocks of one chunk are consecutive tiles, so they run together on
+    // one XCD and the chunk's weights are read from HBM once (realization-block-major read them once per block)
+    const int n_rb = (R_pad + 64 * RW - 1) / (64 * RW);
+    t.c = __builtin_amdgcn_readfirstlane(tile / n_rb);
+    const int rb = __builtin_amdgcn_readfirstlane(tile - t.c * n_rb);  // realization block of 64 RW
     t.r0 = (rb * 4 + wave) * 16 * RW;
     const int4 ci = band.chunks[t.c];
     t.p = __builtin_amdgcn_readfirstlane(ci.x);
