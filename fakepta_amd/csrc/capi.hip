@@ -80,6 +80,11 @@ struct GridPlan {
   DevBuf rows;               // [n_chunks][vmax] int32 grid-buffer row of each band row (all signals back to back)
   DevBuf wd;                 // [n_chunks][vmax][kGridTT] interpolation weights (chromatic factor, mask folded in)
   DevBuf g;                  // [grid_rows][R_pad] grid values of the batch
+  // k_grid_interp_lds plan: groups int4 {first chunk, chunks, union rows U, offset into urows}; urows the grid-
+  // buffer rows of each group's union; lrows [n_chunks][vmax] the union slot of each band row
+  bool lds_ok = false;
+  int32_t n_groups = 0, lds_rows = 0;
+  DevBuf groups, urows, lrows;
   std::vector<GridSeg*> segs;
   double fma_grid = 0.0;     // FMAs per realization: DFT + interpolation
   double fma_dft = 0.0;      // FMAs per realization in k_grid_dft
@@ -96,6 +101,8 @@ struct GridPlan {
     built = ok = false;
     n_chunks = 0;
     vmax = 0;
+    lds_ok = false;
+    n_groups = lds_rows = 0;
     grid_rows = 0;
     g_rpad = 0;
     // the plan figures accumulate over signals in grid_build: a rebuilt plan must start from zero
@@ -166,6 +173,8 @@ struct fpta_ctx {
   // consumer on the ctx stream waits for ev_sig[i] only, so the gridded DFT of one signal overlaps the draws of
   // the next (VALU Philox beside fp64 MFMA). ev_begin orders the side stream after everything queued before.
   int overlap = 1;
+  int interp_lds = 0;    // gridded interpolation with the grid rows staged in LDS where the plan allows (measured
+                         // slower on C2: 0.745 vs 0.67 ms, profiles/r02g_*; kept as an option)
   hipStream_t side = nullptr;
   hipEvent_t ev_begin = nullptr;
   std::vector<hipEvent_t> ev_sig;
@@ -709,9 +718,71 @@ int grid_build(fpta_ctx* c, Layout& L) {
       }
     for (; v < vmax; ++v) r[v] = r[0];
   }
+  // LDS-staged interpolation (k_grid_interp_lds): groups of <= kLdsGroup consecutive chunks of one pulsar whose
+  // bands, over all signals, unite to <= kLdsRowsMax rows. Per group the union's grid-buffer rows (signal by
+  // signal, each signal's rows one contiguous unwrapped range), per chunk the union slot of each band row.
+  std::vector<int4> groups;
+  std::vector<int32_t> urows, lrt((size_t)n_chunks * vmax);
+  int32_t umax = 0;
+  bool lds_ok = true;
+  for (int32_t ci = 0; ci < n_chunks && lds_ok;) {
+    const int32_t p = chunks[ci].x;
+    auto union_rows = [&](int32_t n) {
+      int64_t u = 0;
+      for (int32_t s = 0; s < n_seg; ++s) {
+        int64_t lo = band_lo[s][ci], end = band_lo[s][ci] + band_n[s][ci];
+        for (int32_t k = 1; k < n; ++k) {
+          lo = std::min(lo, band_lo[s][ci + k]);
+          end = std::max(end, band_lo[s][ci + k] + (int64_t)band_n[s][ci + k]);
+        }
+        u += end - lo;
+      }
+      return u;
+    };
+    int32_t n = 1;
+    while (n < kLdsGroup && ci + n < n_chunks && chunks[ci + n].x == p && union_rows(n + 1) <= kLdsRowsMax) ++n;
+    const int64_t U = union_rows(n);
+    if (U > kLdsRowsMax) {
+      lds_ok = false;  // one chunk's bands alone exceed the LDS budget: the register-tiled kernel serves the layout
+      break;
+    }
+    groups.push_back(make_int4(ci, n, (int32_t)U, (int32_t)urows.size()));
+    umax = std::max(umax, (int32_t)U);
+    int32_t uoff = 0;
+    for (int32_t s = 0; s < n_seg; ++s) {
+      int64_t lo = band_lo[s][ci], end = band_lo[s][ci] + band_n[s][ci];
+      for (int32_t k = 1; k < n; ++k) {
+        lo = std::min(lo, band_lo[s][ci + k]);
+        end = std::max(end, band_lo[s][ci + k] + (int64_t)band_n[s][ci + k]);
+      }
+      for (int64_t j = lo; j < end; ++j)
+        urows.push_back((int32_t)(rowoff[s] + (int64_t)p * nf[s] + ((j % nf[s]) + nf[s]) % nf[s]));
+      for (int32_t k = 0; k < n; ++k) {  // chunk ci + k: signal s's band rows start at slot uoff + (its lo - lo)
+        int32_t v = 0;
+        for (int32_t s2 = 0; s2 < s; ++s2) v += band_n[s2][ci + k];
+        for (int32_t i = 0; i < band_n[s][ci + k]; ++i)
+          lrt[(size_t)(ci + k) * vmax + v + i] = uoff + (int32_t)(band_lo[s][ci + k] - lo) + i;
+      }
+      uoff += (int32_t)(end - lo);
+    }
+    for (int32_t k = 0; k < n; ++k) {  // pad rows: any valid slot (weight 0)
+      int32_t* r = lrt.data() + (size_t)(ci + k) * vmax;
+      int32_t v = 0;
+      for (int32_t s = 0; s < n_seg; ++s) v += band_n[s][ci + k];
+      for (; v < vmax; ++v) r[v] = r[0];
+    }
+    ci += n;
+  }
+  G.lds_ok = lds_ok && !groups.empty();
+  G.n_groups = (int32_t)groups.size();
+  G.lds_rows = umax;
   int rc;
   if ((rc = upload(c, G.chunks, chunks.data(), sizeof(int4) * chunks.size(), "grid chunks")) ||
       (rc = upload(c, G.rows, rt.data(), sizeof(int32_t) * rt.size(), "grid band rows")))
+    return rc;
+  if (G.lds_ok && ((rc = upload(c, G.groups, groups.data(), sizeof(int4) * groups.size(), "grid groups")) ||
+                   (rc = upload(c, G.urows, urows.data(), sizeof(int32_t) * urows.size(), "grid union rows")) ||
+                   (rc = upload(c, G.lrows, lrt.data(), sizeof(int32_t) * lrt.size(), "grid LDS rows"))))
     return rc;
   DevBuf d_chunk_of, d_tt_of, d_row, d_d;
   if ((rc = upload(c, d_chunk_of, chunk_of.data(), sizeof(int32_t) * N, "grid chunk_of")) ||
@@ -834,7 +905,12 @@ int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad) {
   KTimer kt(c, FPTA_K_SYNTH);
   GridBand band{G.chunks.as<int4>(), G.rows.as<int32_t>(), G.wd.as<double>(), G.g.as<double>(), G.n_chunks, G.vmax,
                 G.grid_rows};
-  HIPCHK(c, launch_grid_interp_mfma(c->stream, a, band, R_pad), "k_grid_interp_mfma launch");
+  if (c->interp_lds && G.lds_ok && !a.w_on) {
+    GridLds lds{G.groups.as<int4>(), G.urows.as<int32_t>(), G.lrows.as<int32_t>(), G.n_groups, G.lds_rows};
+    HIPCHK(c, launch_grid_interp_lds(c->stream, a, band, lds, R_pad), "k_grid_interp_lds launch");
+  } else {
+    HIPCHK(c, launch_grid_interp_mfma(c->stream, a, band, R_pad), "k_grid_interp_mfma launch");
+  }
   if (a.part) {
     c->part_ready = true;
     c->part_chunks = G.n_chunks;
@@ -1190,6 +1266,9 @@ int fpta_set_option(fpta_ctx* c, int32_t key, int64_t value) {
     case FPTA_OPT_OVERLAP:
       c->overlap = value ? 1 : 0;
       return FPTA_OK;
+    case FPTA_OPT_INTERP_LDS:
+      c->interp_lds = value ? 1 : 0;
+      return FPTA_OK;
     case FPTA_OPT_VALU_VARIANT:
       if (value < 0 || value >= kNumValuVariants) return fail(c, FPTA_EINVAL, "unknown VALU variant");
       c->valu_variant = (int)value;
@@ -1223,6 +1302,7 @@ int fpta_get_option(fpta_ctx* c, int32_t key, int64_t* value) {
     case FPTA_OPT_FUSE_CHECKSUMS: *value = c->fuse_sums; return FPTA_OK;
     case FPTA_OPT_MIX_MFMA: *value = c->mix_mfma; return FPTA_OK;
     case FPTA_OPT_OVERLAP: *value = c->overlap; return FPTA_OK;
+    case FPTA_OPT_INTERP_LDS: *value = c->interp_lds; return FPTA_OK;
   }
   return fail(c, FPTA_EINVAL, "get_option: unknown key");
 }

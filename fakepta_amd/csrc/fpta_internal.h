@@ -114,6 +114,17 @@ struct GridBand {
   int64_t grid_rows;
 };
 hipError_t launch_grid_interp_mfma(hipStream_t st, const SynthArgs& a, const GridBand& band, int32_t R_pad);
+// LDS-staged variant: the 4 waves of a workgroup take <= kLdsGroup consecutive chunks of one pulsar for the same
+// realizations; the union of their band rows (<= kLdsRowsMax) is loaded once into LDS
+constexpr int kLdsGroup = 4, kLdsRowsMax = 144;
+struct GridLds {
+  const int4* groups;   // [n_groups] {first chunk, chunks, union rows U, offset into urows}
+  const int32_t* urows; // grid-buffer rows of each group's union
+  const int32_t* lrows; // [n_chunks][vmax] union slot of each band row
+  int32_t n_groups, lds_rows;
+};
+hipError_t launch_grid_interp_lds(hipStream_t st, const SynthArgs& a, const GridBand& band, const GridLds& lds,
+                                  int32_t R_pad);
 // checksums [n_real][2] from the interpolation's partials [n_chunks][R_pad][2], summed over chunks in a fixed
 // order (tmp: kPartSegs * R_pad * 2 doubles)
 constexpr int kPartSegs = 64;

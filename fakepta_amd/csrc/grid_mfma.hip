@@ -481,6 +481,136 @@ __global__ __launch_bounds__(256, FPTA_INTERP_WPC) void k_grid_interp_mfma(Synth
   }
 }
 
+// ----------------------------------------------------------------------------- k_grid_interp_lds
+// The interpolation with the grid rows staged in LDS. A workgroup takes a group of <= 4 consecutive chunks of
+// one pulsar (host plan) for one block of 128 realizations; wave w computes chunk w of the group (the MFMA
+// structure of k_grid_interp_mfma: even/odd TOA B-tiles, realization tile pairs, 16-byte stores). The union of
+// the group's band rows over all signals (U <= kLdsRowsMax) is loaded once per workgroup with direct-to-LDS
+// 16-byte loads (one wave-instruction = one 1 KB row of 128 realizations), so a grid row shared by the group's
+// chunks (consecutive chunks' bands overlap by ~3/4) crosses the memory pipeline once instead of once per
+// chunk; A operands are then ds_read_b128 from LDS and only the weights come from global memory.
+constexpr int kLdsPitch = 130;  // doubles per LDS row: 1 KB of realizations + 16 B (rows start 4 banks apart)
+
+template <bool WHITE, bool PART>
+__global__ __launch_bounds__(256, 2) void k_grid_interp_lds(SynthArgs a, GridBand band, GridLds plan,
+                                                            int32_t n_tiles, int32_t R_pad, double* __restrict__ out) {
+  constexpr int RW = 8, NP = RW / 2;
+  extern __shared__ __attribute__((aligned(16))) double Gs[];  // [U][kLdsPitch]
+  const int per = (n_tiles + 7) >> 3;
+  const int x = blockIdx.x & 7;
+  const int stride = gridDim.x >> 3;
+  const int end = min(n_tiles, (x + 1) * per);
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int lr = lane & 15, lg = lane >> 4;
+  const int n_rb = R_pad / (16 * RW);
+  d4 acc[2][RW];
+  auto mfma = [&](const dbl2(&av)[NP], const dbl2& bv) {
+#pragma unroll
+    for (int m = 0; m < NP; ++m) {
+      acc[0][2 * m] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m].x, bv.x, acc[0][2 * m], 0, 0, 0);
+      acc[0][2 * m + 1] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m].y, bv.x, acc[0][2 * m + 1], 0, 0, 0);
+      acc[1][2 * m] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m].x, bv.y, acc[1][2 * m], 0, 0, 0);
+      acc[1][2 * m + 1] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m].y, bv.y, acc[1][2 * m + 1], 0, 0, 0);
+    }
+  };
+  for (int tile = x * per + (int)(blockIdx.x >> 3); tile < end; tile += stride) {
+    const int g = __builtin_amdgcn_readfirstlane(tile / n_rb);
+    const int rb = __builtin_amdgcn_readfirstlane(tile - g * n_rb);
+    const int4 gi = plan.groups[g];
+    const int c0 = __builtin_amdgcn_readfirstlane(gi.x), nc = __builtin_amdgcn_readfirstlane(gi.y);
+    const int U = __builtin_amdgcn_readfirstlane(gi.z), uoff = __builtin_amdgcn_readfirstlane(gi.w);
+    FPTA_DCHECK(U <= plan.lds_rows, "k_grid_interp_lds union rows", U, plan.lds_rows + 1);
+    const int r0 = rb * 16 * RW;
+    // the union's grid rows in registers (lane l: row l + 64 i), then wave w stages rows w, w + 4, ...
+    int ur[(kLdsRowsMax + 63) / 64];
+#pragma unroll
+    for (int i = 0; i < (kLdsRowsMax + 63) / 64; ++i) ur[i] = plan.urows[uoff + min(64 * i + lane, U - 1)];
+    __syncthreads();  // every wave is done reading the previous tile's rows
+    for (int row = wave; row < U; row += 4) {
+      const int blk = row >> 6;
+      const int src_reg = blk == 0 ? ur[0] : (blk == 1 ? ur[1] : ur[2]);
+      const int grow = __builtin_amdgcn_readlane(src_reg, row & 63);
+      FPTA_DCHECK(grow >= 0 && grow < band.grid_rows, "k_grid_interp_lds grid row", grow, band.grid_rows);
+      __builtin_amdgcn_global_load_lds((const void*)(band.g + (int64_t)grow * R_pad + r0 + 2 * lane),
+                                       (__attribute__((address_space(3))) void*)(Gs + row * kLdsPitch), 16, 0, 0);
+    }
+    __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0) expcnt(0) lgkmcnt(0): this wave's staged rows have landed
+    __syncthreads();
+    if (wave < nc) {
+      InterpTile<RW> t;
+      t.c = c0 + wave;
+      const int4 ci = band.chunks[t.c];
+      t.p = __builtin_amdgcn_readfirstlane(ci.x);
+      t.y = __builtin_amdgcn_readfirstlane(ci.y);
+      t.cnt = __builtin_amdgcn_readfirstlane(ci.z);
+      t.nq = __builtin_amdgcn_readfirstlane(ci.w) >> 2;
+      t.r0 = r0;
+      // the chunk's LDS slots in registers (lane l: band row l + 64 i), a step's 4 slots by one ds_bpermute
+      const int32_t* __restrict__ lt = plan.lrows + (int64_t)t.c * band.vmax;
+      const int V = 4 * t.nq;
+      const int rr0 = lt[min(lane, V - 1)], rr1 = lt[min(64 + lane, V - 1)];
+      const int rr2 = lt[min(128 + lane, V - 1)], rr3 = lt[min(192 + lane, V - 1)];
+      const double* __restrict__ Wp = band.wd + ((int64_t)t.c * band.vmax + lg) * kGridTT + 2 * lr;
+#pragma unroll
+      for (int e = 0; e < 2; ++e)
+#pragma unroll
+        for (int i = 0; i < RW; ++i) acc[e][i] = d4{0.0, 0.0, 0.0, 0.0};
+      auto load = [&](int qq, dbl2(&av)[NP], dbl2& bv) {
+        const int blk = qq >> 4;  // 64-row block of the step's rows (uniform)
+        const int src = blk == 0 ? rr0 : (blk == 1 ? rr1 : (blk == 2 ? rr2 : rr3));
+        const int slot = __builtin_amdgcn_ds_bpermute(((4 * qq + lg) & 63) << 2, src);
+        FPTA_DCHECK(slot >= 0 && slot < U, "k_grid_interp_lds slot", slot, U);
+        const double* gs = Gs + slot * kLdsPitch + 2 * lr;
+#pragma unroll
+        for (int m = 0; m < NP; ++m) av[m] = *(const dbl2*)(gs + 32 * m);
+        bv = *(const dbl2*)(Wp + 4 * kGridTT * qq);
+      };
+      // two operand sets, each refilled two steps ahead right after its MFMAs
+      dbl2 a0[NP], a1[NP], b0, b1;
+      load(0, a0, b0);
+      load(min(1, t.nq - 1), a1, b1);
+      for (int q = 0; q < t.nq; q += 2) {
+        mfma(a0, b0);
+        if (q + 2 < t.nq) load(q + 2, a0, b0);
+        if (q + 1 < t.nq) {
+          mfma(a1, b1);
+          if (q + 3 < t.nq) load(q + 3, a1, b1);
+        }
+      }
+      if constexpr (WHITE) interp_white<RW>(a, t, acc);
+      interp_store<PART, RW>(a, out, t, acc);
+    }
+  }
+}
+
+hipError_t launch_grid_interp_lds(hipStream_t st, const SynthArgs& a, const GridBand& band, const GridLds& lds,
+                                  int32_t R_pad) {
+  constexpr int RW = 8;
+  if (lds.n_groups <= 0 || lds.lds_rows <= 0 || lds.lds_rows > kLdsRowsMax || R_pad % (16 * RW) != 0 ||
+      band.vmax > kGridVMax)
+    return hipErrorInvalidValue;
+  const int64_t tiles = (int64_t)lds.n_groups * (R_pad / (16 * RW));
+  if (tiles > 0x7FFFFFFF) return hipErrorInvalidValue;
+  const size_t lds_bytes = sizeof(double) * (size_t)lds.lds_rows * kLdsPitch;
+  static int n_cu = 0;
+  if (!n_cu) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0)
+      n_cu = 256;
+  }
+  const int64_t per_cu = std::max<int64_t>(1, std::min<int64_t>(2, (int64_t)(160 * 1024) / (int64_t)lds_bytes));
+  const int64_t grid = std::min<int64_t>((tiles + 7) / 8 * 8, (n_cu * per_cu + 7) / 8 * 8);
+  // the white epilogue's Philox rounds do not fit beside the LDS kernel's registers (52 VGPRs spilled):
+  // white-noise blocks take k_grid_interp_mfma (launch_grid_interp_mfma)
+  if (a.w_on) return hipErrorInvalidValue;
+  auto kernel = a.part ? k_grid_interp_lds<false, true> : k_grid_interp_lds<false, false>;
+  hipLaunchKernelGGL(kernel, dim3((unsigned)grid), dim3(256), lds_bytes, st, a, band, lds, (int32_t)tiles, R_pad,
+                     a.out);
+  return hipGetLastError();
+}
+
 constexpr int kDftMJ = 2, kDftMR = 4;  // k_grid_dft_mfma wave tile: 32 grid rows x 64 realizations
 
 hipError_t launch_grid_dft_mfma(hipStream_t st, GridSegs gsegs, int32_t P, const double* coef, int32_t K,

@@ -265,6 +265,10 @@ int fpta_multi_synth(fpta_multi* m, uint64_t seed, int64_t real0, int64_t n_real
 #define FPTA_OPT_OVERLAP 12       /* batch synthesis with several signals: 1 (default) draws each signal's
                                      coefficients on a second stream so the gridded DFT of one signal overlaps
                                      the draws of the next; 0 one stream. Results are identical. */
+#define FPTA_OPT_INTERP_LDS 13    /* gridded interpolation: 1 stages each chunk group's grid rows in LDS
+                                     (k_grid_interp_lds) where every group fits and no white noise is fused;
+                                     0 (default, faster on MI355X) the register-tiled k_grid_interp_mfma.
+                                     Results are identical. */
 int fpta_set_option(fpta_ctx* ctx, int32_t key, int64_t value);
 /* Current value of option `key` (same keys as fpta_set_option). */
 int fpta_get_option(fpta_ctx* ctx, int32_t key, int64_t* value);

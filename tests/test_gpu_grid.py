@@ -279,3 +279,32 @@ def test_side_stream_draws_are_bitwise_identical(ctx, capi, shipped, path):
             np.testing.assert_array_equal(b0, b1)
     finally:
         ctx.set_options(shipped)
+
+
+@pytest.mark.parametrize("fuse", [0, 1])
+def test_lds_interpolation_is_bitwise_identical(ctx, capi, shipped, fuse):
+    """FPTA_OPT_INTERP_LDS: the LDS-staged interpolation (chunk groups, union rows staged once per workgroup)
+    returns the register-tiled kernel's block and checksums bit for bit, on a ragged multi-signal layout with
+    pulsar boundaries inside chunk groups and unsorted TOAs."""
+    rng = np.random.default_rng(41)
+    offs, toas, nu = random_layout(rng, 23, (31, 260))
+    perm = rng.permutation(offs[1] - offs[0])
+    toas[offs[0]:offs[1]] = toas[offs[0]:offs[1]][perm]  # one pulsar with TOAs out of order
+    ctx.batch_set_toas(offs, toas, nu)
+    f, a = per_psr_signal(rng, offs, toas, 30)
+    ctx.batch_add_signal(0, f, a, idx=0.0)
+    f, a = per_psr_signal(rng, offs, toas, 100)
+    ctx.batch_add_signal(0, f, a, idx=2.0)
+    f, a, L, _ = common_signal(rng, offs, toas, 30)
+    ctx.batch_add_signal(1, f, a, L=L)
+    try:
+        ctx.set_option(capi.OPT_SYNTH_PATH, 4)
+        ctx.set_option(capi.OPT_FUSE_CHECKSUMS, fuse)
+        res = {}
+        for lds in (0, 1):
+            ctx.set_option(capi.OPT_INTERP_LDS, lds)
+            res[lds] = (ctx.batch_synth(5, 300, 333), ctx.batch_checksums())
+        np.testing.assert_array_equal(res[0][0], res[1][0])
+        np.testing.assert_array_equal(res[0][1], res[1][1])
+    finally:
+        ctx.set_options(shipped)

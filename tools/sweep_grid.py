@@ -1,9 +1,9 @@
 """Interleaved A/B of the gridded-path kernels on the C2 workload (one process, HIP-event timing).
 
-    python tools/sweep_grid.py [--rounds 5] [--reps 5] [--real 1024] [--masks 0,1,2,3]
+    python tools/sweep_grid.py [--rounds 5] [--reps 5] [--real 1024] [--masks 0,1]
                                [--params 13:200,11:150,...]
 
-mask = FPTA_OPT_GRID_MFMA: bit 0 runs k_grid_dft on MFMA, bit 1 runs k_grid_interp on MFMA.
+mask = FPTA_OPT_GRID_MFMA: 1 runs k_grid_dft on MFMA, 0 on VALU (the interpolation always runs on MFMA).
 Prints per mask the median k_grid_dft and interpolation times, and the max relative deviation of
 the output from the exact seeded VALU path (path 3) on the same device coefficients.
 --params sweeps (kernel width w, oversampling sigma x 100) pairs instead, at the first mask.
@@ -24,7 +24,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--real", type=int, default=1024)
-    ap.add_argument("--masks", default="0,1,2,3")
+    ap.add_argument("--masks", default="0,1")
     ap.add_argument("--params", default="", help="w:sigma100 pairs, e.g. 13:200,11:150")
     args = ap.parse_args()
     import bench
@@ -39,7 +39,7 @@ def main():
     if args.params:  # (width, sigma) configurations at the first mask
         cfgs = [(masks[0],) + tuple(int(v) for v in p.split(":")) for p in args.params.split(",")]
     else:
-        cfgs = [(m, 13, 200) for m in masks]
+        cfgs = [(m, 15, 150) for m in masks]
 
     def apply(cfg):
         ctx.set_option(_capi.OPT_GRID_MFMA, cfg[0])
