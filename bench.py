@@ -315,7 +315,9 @@ def main():
                     "traffic_source": traffic_src,
                     "implementation_bytes_per_launch": impl_bytes,
                     "interp_fp64_TFLOPs": 2.0 * gi["fma_interp"] * R_pad / synth_avg_s / 1e12,
-                    "grid": {"width": gi["width"], "sigma": gi["sigma"], "err_bound": gi["err_bound"]},
+                    "grid": {"width": gi["width"], "sigma": gi["sigma"], "err_bound": gi["err_bound"],
+                             "signals": gi["signals"], "grid_signals": gi["grid_signals"],
+                             "band_rows_per_chunk": gi["band_rows_per_chunk"]},
                     "dft": {"kernel": GRID_DFT[bool(gi["grid_mfma"] & 1)], "avg_launch_ms": grid_avg_s * 1e3,
                             "flops_per_launch": dft_flops, "TFLOPs": dft_flops / max(grid_avg_s, 1e-12) / 1e12,
                             "frac_fp64_peak": dft_flops / max(grid_avg_s, 1e-12) / 1e12 / FP64_PEAK_TFLOPS}}

@@ -84,10 +84,10 @@ EXPORTED = [s[0] for s in _SIGS]
 
 OPT_SYNTH_PATH, OPT_MFMA_MIN_REAL, OPT_PROFILE, OPT_ANCHOR, OPT_VALU_VARIANT, OPT_FUSE_WHITE = 1, 2, 3, 4, 5, 6
 OPT_GRID_WIDTH, OPT_GRID_SIGMA, OPT_GRID_MFMA, OPT_FUSE_CHECKSUMS = 7, 8, 9, 10
-OPT_MIX_MFMA, OPT_OVERLAP, OPT_INTERP_LDS = 11, 12, 13
+OPT_MIX_MFMA, OPT_OVERLAP, OPT_INTERP_LDS, OPT_GRID_COALESCE, OPT_INTERP_WS = 11, 12, 13, 14, 15
 OPTIONS = (OPT_SYNTH_PATH, OPT_MFMA_MIN_REAL, OPT_PROFILE, OPT_ANCHOR, OPT_VALU_VARIANT, OPT_FUSE_WHITE,
            OPT_GRID_WIDTH, OPT_GRID_SIGMA, OPT_GRID_MFMA, OPT_FUSE_CHECKSUMS, OPT_MIX_MFMA, OPT_OVERLAP,
-           OPT_INTERP_LDS)
+           OPT_INTERP_LDS, OPT_GRID_COALESCE, OPT_INTERP_WS)
 K_GEN, K_MIX, K_SYNTH, K_WHITE, K_DENSE, K_GRID = 0, 1, 2, 3, 4, 5
 BUILD_DEBUG = 1
 
@@ -295,15 +295,17 @@ class Context:
     def batch_grid_info(self):
         """Gridded-path plan figures, the path of the last batch and why it was not the gridded path
         (fpta_batch_grid_info, fpta_batch_path_reason)."""
-        g = np.zeros(12, dtype=np.float64)
+        g = np.zeros(16, dtype=np.float64)
         self._check(_lib.fpta_batch_grid_info(self._h, _ptr(g)), "fpta_batch_grid_info")
         keys = ("last_path", "ok", "n_chunks", "fma_dft", "fma_interp", "fma_direct", "grid_vals", "weight_bytes",
-                "grid_mfma", "err_bound", "width", "sigma")
+                "grid_mfma", "err_bound", "width", "sigma", "grid_signals", "signals", "band_rows_per_chunk")
         d = dict(zip(keys, g.tolist()))
         d["last_path"] = int(d["last_path"])
         d["ok"] = bool(d["ok"])
         d["grid_mfma"] = int(d["grid_mfma"])
         d["width"] = int(d["width"])
+        d["grid_signals"] = int(d["grid_signals"])
+        d["signals"] = int(d["signals"])
         d["path_reason"] = _lib.fpta_batch_path_reason(self._h).decode()
         return d
 

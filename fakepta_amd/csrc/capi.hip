@@ -55,6 +55,7 @@ struct Seg {
   SegDesc d{};
   int32_t nm_orig = 0;
   std::vector<double> h_w0;  // first angular frequency per row ([P] for kind 0, [1] for kind 1)
+  std::vector<uint8_t> h_mask;  // host copy of the TOA mask (empty: none), for grid coalescing
   DevBuf w, amp, L, LT, mask;
 };
 
@@ -79,13 +80,20 @@ struct GridPlan {
   int64_t grid_rows = 0;     // rows of the grid buffer: sum over signals of P nf
   DevBuf rows;               // [n_chunks][vmax] int32 grid-buffer row of each band row (all signals back to back)
   DevBuf wd;                 // [n_chunks][vmax][kGridTT] interpolation weights (chromatic factor, mask folded in)
-  DevBuf g;                  // [grid_rows][R_pad] grid values of the batch
+  DevBuf g, g2;              // [grid_rows][R_pad] grid values of the batch (two buffers when pipelined)
   // k_grid_interp_lds plan: groups int4 {first chunk, chunks, union rows U, offset into urows}; urows the grid-
   // buffer rows of each group's union; lrows [n_chunks][vmax] the union slot of each band row
   bool lds_ok = false;
   int32_t n_groups = 0, lds_rows = 0;
   DevBuf groups, urows, lrows;
-  std::vector<GridSeg*> segs;
+  std::vector<GridSeg*> segs;  // one per grid signal
+  // grid signals (FPTA_OPT_GRID_COALESCE): members (layout signal indices, ascending), the anchor (the member with
+  // the most modes: its coefficient columns receive the others' and its grid/weights serve the group) and the last
+  // member (the group's coefficients are complete once it is drawn)
+  std::vector<std::vector<int32_t>> members;
+  std::vector<int32_t> anchor, last;
+  bool merges = false;       // some grid signal has > 1 member
+  double mean_v = 0.0;       // mean band rows per chunk
   double fma_grid = 0.0;     // FMAs per realization: DFT + interpolation
   double fma_dft = 0.0;      // FMAs per realization in k_grid_dft
   double fma_interp = 0.0;   // FMAs per realization in k_grid_interp (dense band, padded TOA slots)
@@ -105,6 +113,11 @@ struct GridPlan {
     n_groups = lds_rows = 0;
     grid_rows = 0;
     g_rpad = 0;
+    members.clear();
+    anchor.clear();
+    last.clear();
+    merges = false;
+    mean_v = 0.0;
     // the plan figures accumulate over signals in grid_build: a rebuilt plan must start from zero
     fma_grid = fma_dft = fma_interp = grid_vals = weight_bytes = fma_direct = 0.0;
     err_bound = 1.0;
@@ -118,7 +131,7 @@ struct Layout {
   int64_t n_toa = 0;
   int64_t max_np = 0;
   std::vector<int64_t> h_offs;
-  std::vector<double> h_toas;
+  std::vector<double> h_toas, h_nu;
   DevBuf offs, toas, nu, psr_of;
   std::vector<Seg*> segs;
   DevBuf segdesc;
@@ -173,6 +186,8 @@ struct fpta_ctx {
   // consumer on the ctx stream waits for ev_sig[i] only, so the gridded DFT of one signal overlaps the draws of
   // the next (VALU Philox beside fp64 MFMA). ev_begin orders the side stream after everything queued before.
   int overlap = 1;
+  int interp_ws = 1;      // gridded interpolation on the warp-specialised kernel (FPTA_OPT_INTERP_WS)
+  int grid_coalesce = 1;  // gridded path: signals sharing w0 and the chromatic weight share one grid (FPTA_OPT_GRID_COALESCE)
   int interp_lds = 0;    // gridded interpolation with the grid rows staged in LDS where the plan allows (measured
                          // slower on C2: 0.745 vs 0.67 ms, profiles/r02g_*; kept as an option)
   hipStream_t side = nullptr;
@@ -184,6 +199,16 @@ struct fpta_ctx {
   // block, so they overlap that block's interpolation
   hipEvent_t ev_coef_free = nullptr;
   bool coef_free_set = false;
+  // pipelined gridded batches (FPTA_OPT_OVERLAP, path 4): the draws, merges and DFT of a block all run on the side
+  // stream, into one of two grid buffers, so they overlap the previous block's interpolation on the ctx stream.
+  // ev_gready: the block's DFT is done (its interpolation waits); ev_gfree[i]: the interpolation reading grid
+  // buffer i is done (the DFT that next writes buffer i waits); coef_last_side: the last reader of coef was a
+  // side-stream DFT, so the next block's draws need no ctx-stream wait.
+  hipEvent_t ev_gready = nullptr;
+  hipEvent_t ev_gfree[2] = {nullptr, nullptr};
+  bool gfree_set[2] = {false, false};
+  int gbuf = 0;
+  bool coef_last_side = false;
   bool coef_copy_pending = false;  // the block's coefficients are still to be downloaded after the synthesis
   DevBuf part, part_tmp; // partial checksums [n_chunks][R_pad][2] of the last block, reduction scratch
   bool part_ready = false;  // part holds the partials of the current block (c->out, out_R)
@@ -298,6 +323,7 @@ int layout_set_toas(fpta_ctx* c, Layout& L, int32_t P, const int64_t* offs, cons
   L.max_np = mx;
   L.h_offs.assign(offs, offs + P + 1);
   L.h_toas.assign(toas, toas + N);
+  L.h_nu.assign(nu, nu + N);
   std::vector<int32_t> psr_of(N);
   for (int32_t p = 0; p < P; ++p)
     for (int64_t t = offs[p]; t < offs[p + 1]; ++t) psr_of[t] = p;
@@ -349,6 +375,7 @@ int layout_add_signal(fpta_ctx* c, Layout& L, int32_t kind, int32_t nm, const do
   Seg* s = new Seg();
   s->nm_orig = nm;
   for (int32_t r = 0; r < rows; ++r) s->h_w0.push_back(w[(size_t)r * nmp]);
+  if (mask) s->h_mask.assign(mask, mask + L.n_toa);
   int rc;
   if ((rc = upload(c, s->w, w.data(), sizeof(double) * w.size(), "add_signal w")) ||
       (rc = upload(c, s->amp, a.data(), sizeof(double) * a.size(), "add_signal amp"))) {
@@ -453,14 +480,24 @@ int wait_coef_all(fpta_ctx* c) {
   return FPTA_OK;
 }
 
+// merge: the gridded plan of L coalesces signals (GridPlan::members): after the last member of a grid signal is
+// drawn, k_coef_merge adds the other members' columns into the anchor's. coef_host (optional, with merge): the
+// per-signal coefficients [P][K][R] are downloaded before any merge and *coef_done is set.
+// pipe: a pipelined gridded block (side stream even for one signal; grid_run runs its DFT there too).
 int run_coefficients(fpta_ctx* c, Layout& L, uint64_t seed, int64_t real0, int32_t R, int32_t R_pad,
-                     const double* zin, int32_t zin_nm, double* x_out, bool side = false) {
+                     const double* zin, int32_t zin_nm, double* x_out, bool side = false, bool merge = false,
+                     double* coef_host = nullptr, bool* coef_done = nullptr, bool pipe = false) {
   const int32_t P = L.P;
   int rc0 = wait_coef_all(c);  // a previous block's draws are fully ordered before this one's
   if (rc0) return rc0;
   hipStream_t st = c->stream;
-  if (!(side && L.segs.size() > 1)) c->coef_free_set = false;  // coef is written on the ctx stream from here on
-  if (side && L.segs.size() > 1) {
+  const bool use_side = side && (L.segs.size() > 1 || pipe);
+  const bool last_side = c->coef_last_side;
+  c->coef_last_side = false;
+  if (!use_side) c->coef_free_set = false;  // coef is written on the ctx stream from here on
+  const size_t coef_bytes = sizeof(double) * (size_t)P * std::max(L.K, 1) * R_pad;
+  if (c->side && c->coef.cap < coef_bytes) HIPCHK(c, hipStreamSynchronize(c->side), "side sync");  // before a regrow
+  if (use_side) {
     if (!c->side) HIPCHK(c, hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking), "side stream create");
     if (!c->ev_begin) HIPCHK(c, hipEventCreateWithFlags(&c->ev_begin, hipEventDisableTiming), "event create");
     while (c->ev_sig.size() < L.segs.size()) {
@@ -469,18 +506,37 @@ int run_coefficients(fpta_ctx* c, Layout& L, uint64_t seed, int64_t real0, int32
       c->ev_sig.push_back(e);
     }
     // the previous block's last reader of coef (its DFT or download) comes first; without one recorded,
-    // everything queued on the ctx stream
-    if (!c->coef_free_set) HIPCHK(c, hipEventRecord(c->ev_begin, c->stream), "event record");
-    HIPCHK(c, hipStreamWaitEvent(c->side, c->coef_free_set ? c->ev_coef_free : c->ev_begin, 0), "side wait");
+    // everything queued on the ctx stream. A pipelined block whose DFT (on this stream) was that reader needs no
+    // wait, unless the draws read a ctx-stream upload (zin)
+    if (!(pipe && last_side && !c->coef_free_set && !zin)) {
+      if (!c->coef_free_set) HIPCHK(c, hipEventRecord(c->ev_begin, c->stream), "event record");
+      HIPCHK(c, hipStreamWaitEvent(c->side, c->coef_free_set ? c->ev_coef_free : c->ev_begin, 0), "side wait");
+    }
     c->coef_free_set = false;
     st = c->side;
   }
-  HIPCHK(c, c->coef.ensure(sizeof(double) * (size_t)P * std::max(L.K, 1) * R_pad), "coef alloc");
+  HIPCHK(c, c->coef.ensure(coef_bytes), "coef alloc");
   size_t zb = 0;
   for (Seg* s : L.segs)
     if (s->d.kind == 1) zb = std::max(zb, sizeof(double) * (size_t)P * 2 * s->d.nm * R_pad);
   if (zb) HIPCHK(c, c->zbuf.ensure(zb), "zbuf alloc");
   const uint32_t k0 = (uint32_t)(seed & 0xFFFFFFFFull), k1 = (uint32_t)(seed >> 32);
+  const GridPlan& G = L.grid;
+  merge = merge && G.built && G.ok && G.merges;
+  // the download of per-signal coefficients must precede every merge: then all events wait for the end
+  const bool defer = merge && coef_host;
+  auto merge_group = [&](size_t g) -> int {
+    CoefMerge m{};
+    m.dst = L.segs[G.anchor[g]]->d.col0;
+    for (int32_t i : G.members[g])
+      if (i != G.anchor[g]) {
+        m.src[m.n] = L.segs[i]->d.col0;
+        m.ncol[m.n++] = 2 * L.segs[i]->d.nm;
+      }
+    KTimer kt(c, FPTA_K_GEN, st);
+    HIPCHK(c, launch_coef_merge(st, m, P, L.K, R_pad, c->coef.as<double>()), "k_coef_merge launch");
+    return FPTA_OK;
+  };
   for (size_t i = 0; i < L.segs.size(); ++i) {
     const SegDesc& d = L.segs[i]->d;
     {
@@ -502,9 +558,29 @@ int run_coefficients(fpta_ctx* c, Layout& L, uint64_t seed, int64_t real0, int32
         HIPCHK(c, launch_mix(st, d, P, R_pad, c->zbuf.as<double>(), c->coef.as<double>(), L.K, x_out),
                "k_mix launch");
     }
-    if (st != c->stream) HIPCHK(c, hipEventRecord(c->ev_sig[i], st), "event record");
+    if (merge && !defer)
+      for (size_t g = 0; g < G.members.size(); ++g)
+        if (G.members[g].size() > 1 && G.last[g] == (int32_t)i) {
+          int rc = merge_group(g);
+          if (rc) return rc;
+        }
+    if (st != c->stream && !defer && !pipe) HIPCHK(c, hipEventRecord(c->ev_sig[i], st), "event record");
   }
-  c->coef_side = st != c->stream;
+  if (defer) {
+    HIPCHK(c,
+           hipMemcpy2DAsync(coef_host, sizeof(double) * R, c->coef.p, sizeof(double) * R_pad, sizeof(double) * R,
+                            (size_t)P * L.K, hipMemcpyDeviceToHost, st),
+           "coef download");
+    if (coef_done) *coef_done = true;
+    for (size_t g = 0; g < G.members.size(); ++g)
+      if (G.members[g].size() > 1) {
+        int rc = merge_group(g);
+        if (rc) return rc;
+      }
+    if (st != c->stream && !pipe)
+      for (size_t i = 0; i < L.segs.size(); ++i) HIPCHK(c, hipEventRecord(c->ev_sig[i], st), "event record");
+  }
+  c->coef_side = st != c->stream && !pipe;  // pipelined: the DFT follows on the same stream, no per-signal events
   return FPTA_OK;
 }
 
@@ -593,9 +669,8 @@ int grid_build(fpta_ctx* c, Layout& L) {
   G.w = c->grid_w;
   G.sigma = c->grid_sigma100 / 100.0;
   G.err_bound = std::exp(-M_PI * G.w * std::sqrt(1.0 - 1.0 / G.sigma));
-  const int32_t n_seg = (int32_t)L.segs.size();
-  if (n_seg == 0 || n_seg > kGridMaxSeg) {
-    G.why = "gridded path: needs 1.." + std::to_string(kGridMaxSeg) + " signals";
+  if (L.segs.empty()) {
+    G.why = "gridded path: no signals";
     return FPTA_OK;
   }
   for (Seg* sg : L.segs)
@@ -603,6 +678,58 @@ int grid_build(fpta_ctx* c, Layout& L) {
       G.why = "gridded path: every signal needs a harmonic grid f_k = k f_1";
       return FPTA_OK;
     }
+  // grid signals: with FPTA_OPT_GRID_COALESCE, a signal joins the first earlier grid signal with the same base
+  // frequency w0 on every pulsar and the same chromatic weight (factor x mask) on every TOA. Their sums
+  // ch(t) sum_k c_k cos(k w0 t) + s_k sin(k w0 t) then add in coefficient space (k_coef_merge): one DFT, one band.
+  {
+    const int32_t n_layout = (int32_t)L.segs.size();
+    std::vector<std::vector<double>> chv(n_layout);
+    auto ch_of = [&](int32_t i) -> const std::vector<double>& {
+      if (chv[i].empty()) {
+        const SegDesc& d = L.segs[i]->d;
+        const std::vector<uint8_t>& m = L.segs[i]->h_mask;
+        chv[i].resize(L.n_toa);
+        for (int64_t t = 0; t < L.n_toa; ++t) {
+          double ch = 1.0;  // chrom_factor (device_common.h), same operations
+          if (d.idx != 0.0) {
+            const double x = d.freqf / L.h_nu[t];
+            ch = d.idx == 2.0 ? x * x : d.idx == 1.0 ? x : std::pow(x, d.idx);
+          }
+          chv[i][t] = (!m.empty() && !m[t]) ? 0.0 : ch;
+        }
+      }
+      return chv[i];
+    };
+    auto w0_of = [&](int32_t i, int32_t p) { return L.segs[i]->h_w0[L.segs[i]->d.kind == 0 ? p : 0]; };
+    for (int32_t i = 0; i < n_layout; ++i) {
+      int32_t join = -1;
+      for (size_t g = 0; c->grid_coalesce && g < G.members.size() && join < 0; ++g) {
+        const int32_t f = G.members[g][0];
+        bool same = true;
+        for (int32_t p = 0; p < L.P && same; ++p) same = w0_of(i, p) == w0_of(f, p);
+        if (same) same = ch_of(i) == ch_of(f);
+        if (same) join = (int32_t)g;
+      }
+      if (join < 0) {
+        G.members.push_back({i});
+      } else {
+        G.members[join].push_back(i);
+        G.merges = true;
+      }
+    }
+    for (const std::vector<int32_t>& m : G.members) {
+      int32_t a = m[0];
+      for (int32_t i : m)
+        if (L.segs[i]->d.nm > L.segs[a]->d.nm) a = i;
+      G.anchor.push_back(a);
+      G.last.push_back(m.back());
+    }
+  }
+  const int32_t n_seg = (int32_t)G.members.size();  // grid signals from here on
+  if (n_seg > kGridMaxSeg) {
+    G.why = "gridded path: needs 1.." + std::to_string(kGridMaxSeg) + " grid signals (after coalescing)";
+    return FPTA_OK;
+  }
   const int32_t w = G.w;
   // shape parameter of the exponential-of-semicircle kernel for oversampling sigma (2.31 w at sigma = 2)
   const double beta = 0.98 * M_PI * w * (1.0 - 0.5 / G.sigma), hw = 0.5 * w;
@@ -612,13 +739,14 @@ int grid_build(fpta_ctx* c, Layout& L) {
   std::vector<std::vector<double>> D(n_seg, std::vector<double>(N));
   std::vector<int32_t> nf(n_seg);
   for (int32_t s = 0; s < n_seg; ++s) {
-    const SegDesc& d = L.segs[s]->d;
+    const Seg* sg = L.segs[G.anchor[s]];
+    const SegDesc& d = sg->d;
     int32_t n = (int32_t)std::ceil(G.sigma * (2.0 * d.nm + 1.0));
     n += n & 1;
     nf[s] = std::max(n, 2 * w + 2);
     const double h = 2.0 * M_PI / nf[s];
     for (int32_t p = 0; p < L.P; ++p) {
-      const double w0 = L.segs[s]->h_w0[d.kind == 0 ? p : 0];
+      const double w0 = sg->h_w0[d.kind == 0 ? p : 0];
       for (int64_t t = L.h_offs[p]; t < L.h_offs[p + 1]; ++t) {
         const double u = (w0 * L.h_toas[t]) / h;
         if (!std::isfinite(u) || std::fabs(u) > 1e15) {
@@ -796,10 +924,14 @@ int grid_build(fpta_ctx* c, Layout& L) {
   G.fma_direct = 0.0;
   G.fma_grid = 0.0;
   G.fma_interp = 0.0;
+  G.fma_dft = 0.0;
+  G.grid_vals = 0.0;
   for (int32_t ci = 0; ci < n_chunks; ++ci) G.fma_interp += (double)chunks[ci].w * kGridTT;
+  G.mean_v = G.fma_interp / kGridTT / std::max(n_chunks, 1);
   G.weight_bytes = (double)wbytes;
+  for (Seg* sg : L.segs) G.fma_direct += 2.0 * sg->d.nm * (double)N;
   for (int32_t s = 0; s < n_seg; ++s) {
-    const SegDesc& d = L.segs[s]->d;
+    const SegDesc& d = L.segs[G.anchor[s]]->d;
     GridSeg* gs = new GridSeg();
     G.segs.push_back(gs);
     gs->nf = nf[s];
@@ -836,7 +968,6 @@ int grid_build(fpta_ctx* c, Layout& L) {
                                d_row.as<int32_t>(), d_d.as<double>(), w, beta, vmax, G.wd.as<double>()),
            "k_grid_weights launch");
     HIPCHK(c, hipStreamSynchronize(c->stream), "grid weights sync");  // d_row / d_d are reused
-    G.fma_direct += 2.0 * d.nm * (double)N;
     G.fma_dft += (double)L.P * (gs->half + 1) * 2.0 * d.nm;
     G.grid_vals += (double)L.P * gs->nf;
     G.fma_grid = G.fma_dft + G.fma_interp;
@@ -845,24 +976,38 @@ int grid_build(fpta_ctx* c, Layout& L) {
   return FPTA_OK;
 }
 
-// Run the gridded synthesis: one DFT launch per signal, then one interpolation launch for all.
-int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad) {
+// Run the gridded synthesis: one DFT launch per grid signal, then one interpolation launch for all.
+// pipe (run_coefficients drew this block on the side stream in pipelined mode): the DFTs follow there, into grid
+// buffer c->gbuf, and the interpolation on the ctx stream waits only for them.
+int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad, bool pipe = false) {
   GridPlan& G = L.grid;
   GridSegs gsegs{};
   gsegs.n = (int32_t)G.segs.size();
-  if (G.g_rpad != R_pad) {
-    HIPCHK(c, G.g.ensure(sizeof(double) * (size_t)G.grid_rows * R_pad), "grid alloc");
+  const size_t gbytes = sizeof(double) * (size_t)G.grid_rows * R_pad;
+  if (G.g_rpad != R_pad || (pipe && G.g2.cap < gbytes)) {
+    if (c->side) HIPCHK(c, hipStreamSynchronize(c->side), "side sync");  // no reader of a buffer being regrown
+    HIPCHK(c, hipStreamSynchronize(c->stream), "grid regrow sync");
+    HIPCHK(c, G.g.ensure(gbytes), "grid alloc");
+    if (pipe) HIPCHK(c, G.g2.ensure(gbytes), "grid alloc");
     G.g_rpad = R_pad;
   }
+  const int gi = pipe ? c->gbuf : 0;
+  double* const gbase = gi ? G.g2.as<double>() : G.g.as<double>();
+  if (pipe) {
+    for (hipEvent_t* e : {&c->ev_gready, &c->ev_gfree[0], &c->ev_gfree[1]})
+      if (!*e) HIPCHK(c, hipEventCreateWithFlags(e, hipEventDisableTiming), "event create");
+    // the DFT overwrites buffer gi: the interpolation that last read it (two blocks back) must be done
+    if (c->gfree_set[gi]) HIPCHK(c, hipStreamWaitEvent(c->side, c->ev_gfree[gi], 0), "grid buffer wait");
+  }
   {
-    KTimer kt(c, FPTA_K_GRID);
+    KTimer kt(c, FPTA_K_GRID, pipe ? c->side : c->stream);
     for (size_t s = 0; s < G.segs.size(); ++s) {
       GridSeg* gs = G.segs[s];
-      const SegDesc& d = L.segs[s]->d;
+      const SegDesc& d = L.segs[G.anchor[s]]->d;  // a coalesced grid signal reads its anchor's merged columns
       GridSegDev& g = gsegs.s[s];
       g.ecos = gs->ecos.as<double>();
       g.esin = gs->esin.as<double>();
-      g.g = G.g.as<double>() + gs->rowoff * R_pad;
+      g.g = gbase + gs->rowoff * R_pad;
       g.nf = gs->nf;
       g.half = gs->half;
       g.lde = gs->lde;
@@ -871,13 +1016,22 @@ int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad) {
       g.ntab = gs->ntab;
     }
     const bool early_free = c->coef_side && !c->coef_copy_pending;
-    if (c->coef_side) {
-      // one DFT launch per signal, each after that signal's draws only (they run on the side stream)
-      for (int32_t s = 0; s < gsegs.n; ++s) {
+    if (pipe) {
+      HIPCHK(c,
+             (c->grid_mfma & 1) ? launch_grid_dft_mfma(c->side, gsegs, L.P, a.coef, a.K, R_pad)
+                                : launch_grid_dft(c->side, gsegs, L.P, a.coef, a.K, R_pad),
+             "k_grid_dft launch");
+    } else if (c->coef_side) {
+      // one DFT launch per grid signal, each after that signal's draws (and merge) only (side stream); in the
+      // order their draws complete
+      std::vector<int32_t> order(gsegs.n);
+      for (int32_t s = 0; s < gsegs.n; ++s) order[s] = s;
+      std::stable_sort(order.begin(), order.end(), [&](int32_t x, int32_t y) { return G.last[x] < G.last[y]; });
+      for (int32_t s : order) {
         GridSegs one{};
         one.s[0] = gsegs.s[s];
         one.n = 1;
-        int rc = wait_coef(c, (size_t)s);
+        int rc = wait_coef(c, (size_t)G.last[s]);
         if (rc) return rc;
         HIPCHK(c,
                (c->grid_mfma & 1) ? launch_grid_dft_mfma(c->stream, one, L.P, a.coef, a.K, R_pad)
@@ -891,7 +1045,10 @@ int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad) {
                                 : launch_grid_dft(c->stream, gsegs, L.P, a.coef, a.K, R_pad),
              "k_grid_dft launch");
     }
-    if (early_free) {  // the DFT was the last reader of coef: the next block may draw during the interpolation
+    if (pipe) {
+      HIPCHK(c, hipEventRecord(c->ev_gready, c->side), "event record");
+      c->coef_last_side = !c->coef_copy_pending;  // else the download on the ctx stream is the last reader
+    } else if (early_free) {  // the DFT was the last reader of coef: the next block may draw during the interpolation
       if (!c->ev_coef_free) HIPCHK(c, hipEventCreateWithFlags(&c->ev_coef_free, hipEventDisableTiming), "event create");
       HIPCHK(c, hipEventRecord(c->ev_coef_free, c->stream), "event record");
       c->coef_free_set = true;
@@ -902,14 +1059,22 @@ int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad) {
     HIPCHK(c, c->part.ensure(sizeof(double) * 2 * (size_t)G.n_chunks * R_pad), "partial checksums alloc");
     a.part = c->part.as<double>();
   }
+  if (pipe) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_gready, 0), "grid ready wait");
   KTimer kt(c, FPTA_K_SYNTH);
-  GridBand band{G.chunks.as<int4>(), G.rows.as<int32_t>(), G.wd.as<double>(), G.g.as<double>(), G.n_chunks, G.vmax,
+  GridBand band{G.chunks.as<int4>(), G.rows.as<int32_t>(), G.wd.as<double>(), gbase, G.n_chunks, G.vmax,
                 G.grid_rows};
-  if (c->interp_lds && G.lds_ok && !a.w_on) {
+  if (c->interp_ws && !c->interp_lds && !a.w_on && !a.accumulate) {
+    HIPCHK(c, launch_grid_interp_ws(c->stream, a, band, R_pad), "k_grid_interp_ws launch");
+  } else if (c->interp_lds && G.lds_ok && !a.w_on) {
     GridLds lds{G.groups.as<int4>(), G.urows.as<int32_t>(), G.lrows.as<int32_t>(), G.n_groups, G.lds_rows};
     HIPCHK(c, launch_grid_interp_lds(c->stream, a, band, lds, R_pad), "k_grid_interp_lds launch");
   } else {
     HIPCHK(c, launch_grid_interp_mfma(c->stream, a, band, R_pad), "k_grid_interp_mfma launch");
+  }
+  if (pipe) {  // buffer gi is free once this interpolation is done; the next block's DFT writes the other one
+    HIPCHK(c, hipEventRecord(c->ev_gfree[gi], c->stream), "event record");
+    c->gfree_set[gi] = true;
+    c->gbuf = gi ^ 1;
   }
   if (a.part) {
     c->part_ready = true;
@@ -931,33 +1096,15 @@ struct WhiteCfg {
   uint32_t k0 = 0, k1 = 0;
 };
 
-// *fused is set when the kernel that ran also added `white` (only the seeded VALU kernel does).
-int run_synth(fpta_ctx* c, Layout& L, int32_t R, int32_t R_pad, double* out, int64_t ldo, int accumulate,
-              bool allow_mfma, const WhiteCfg* white = nullptr, bool* fused = nullptr) {
-  if (fused) *fused = false;
-  SynthArgs a{};
-  a.offs = L.offs.as<int64_t>();
-  a.psr_of = L.psr_of.as<int32_t>();
-  a.toas = L.toas.as<double>();
-  a.nu = L.nu.as<double>();
-  a.segs = L.segdesc.as<SegDesc>();
-  a.n_seg = (int32_t)L.segs.size();
-  a.P = L.P;
-  a.n_toa = L.n_toa;
-  a.coef = c->coef.as<double>();
-  a.K = L.K;
-  a.R_pad = R_pad;
-  a.out = out;
-  a.ldo = ldo;
-  a.n_real = R;
-  a.accumulate = accumulate;
-  a.anchor = c->anchor;
-  a.coef_len = (int64_t)L.P * std::max(L.K, 1) * R_pad;
+// Synthesis path of a batch (before its coefficients are drawn: a gridded plan that coalesces signals merges
+// their coefficient columns, run_coefficients).
+int select_path(fpta_ctx* c, Layout& L, int32_t R, bool allow_mfma, int* out_path) {
   // path: 1 direct, 2 MFMA, 3 VALU, 4 gridded; auto (0) = gridded when its plan needs fewer than
   // kGridAutoRatio of the direct FMAs and its a-priori error bound is within kGridAutoMaxErr, else VALU,
   // for R >= mfma_min_real; direct below. c->path_reason says why auto did not take the gridded path.
   int path = c->synth_path;
   c->path_reason.clear();
+  *out_path = 0;
   if (!allow_mfma) {
     path = 1;
     c->path_reason = "single-realization drop-in call: direct path (exact phases)";
@@ -990,6 +1137,38 @@ int run_synth(fpta_ctx* c, Layout& L, int32_t R, int32_t R_pad, double* out, int
         path = 4;
     }
   }
+  *out_path = path;
+  return FPTA_OK;
+}
+
+// *fused is set when the kernel that ran also added `white` (the seeded VALU and gridded kernels do).
+// path: the select_path result for this batch, or -1 to select here.
+int run_synth(fpta_ctx* c, Layout& L, int32_t R, int32_t R_pad, double* out, int64_t ldo, int accumulate,
+              bool allow_mfma, const WhiteCfg* white = nullptr, bool* fused = nullptr, int path = -1,
+              bool pipe = false) {
+  if (fused) *fused = false;
+  SynthArgs a{};
+  a.offs = L.offs.as<int64_t>();
+  a.psr_of = L.psr_of.as<int32_t>();
+  a.toas = L.toas.as<double>();
+  a.nu = L.nu.as<double>();
+  a.segs = L.segdesc.as<SegDesc>();
+  a.n_seg = (int32_t)L.segs.size();
+  a.P = L.P;
+  a.n_toa = L.n_toa;
+  a.coef = c->coef.as<double>();
+  a.K = L.K;
+  a.R_pad = R_pad;
+  a.out = out;
+  a.ldo = ldo;
+  a.n_real = R;
+  a.accumulate = accumulate;
+  a.anchor = c->anchor;
+  a.coef_len = (int64_t)L.P * std::max(L.K, 1) * R_pad;
+  if (path < 0) {
+    int rc = select_path(c, L, R, allow_mfma, &path);
+    if (rc) return rc;
+  }
   // host-side guards of what the tiled kernels assume (every tile's realization block lies inside
   // the coefficient padding; the coefficient buffer holds P*K*R_pad values)
   if (R_pad % kRealPad != 0 || R > R_pad || kRealPad % kTileReal != 0 ||
@@ -1015,7 +1194,7 @@ int run_synth(fpta_ctx* c, Layout& L, int32_t R, int32_t R_pad, double* out, int
       a.k1 = white->k1;
       if (fused) *fused = true;
     }
-    return grid_run(c, L, a, R_pad);
+    return grid_run(c, L, a, R_pad, pipe);
   } else if (path == 2) {
     int rc = build_tiles(c, L, R, kTileToa, kTileReal);
     if (rc || (rc = check_tiles(c, L, R, kTileToa, kTileReal, a))) return rc;
@@ -1227,6 +1406,8 @@ int fpta_destroy(fpta_ctx* c) {
   }
   if (c->ev_begin) (void)hipEventDestroy(c->ev_begin);
   if (c->ev_coef_free) (void)hipEventDestroy(c->ev_coef_free);
+  for (hipEvent_t e : {c->ev_gready, c->ev_gfree[0], c->ev_gfree[1]})
+    if (e) (void)hipEventDestroy(e);
   for (auto e : c->ev_sig) (void)hipEventDestroy(e);
   (void)hipStreamDestroy(c->stream);
   delete c;
@@ -1269,6 +1450,13 @@ int fpta_set_option(fpta_ctx* c, int32_t key, int64_t value) {
     case FPTA_OPT_INTERP_LDS:
       c->interp_lds = value ? 1 : 0;
       return FPTA_OK;
+    case FPTA_OPT_GRID_COALESCE:
+      c->grid_coalesce = value ? 1 : 0;
+      c->batch.grid.clear();
+      return FPTA_OK;
+    case FPTA_OPT_INTERP_WS:
+      c->interp_ws = value ? 1 : 0;
+      return FPTA_OK;
     case FPTA_OPT_VALU_VARIANT:
       if (value < 0 || value >= kNumValuVariants) return fail(c, FPTA_EINVAL, "unknown VALU variant");
       c->valu_variant = (int)value;
@@ -1303,6 +1491,8 @@ int fpta_get_option(fpta_ctx* c, int32_t key, int64_t* value) {
     case FPTA_OPT_MIX_MFMA: *value = c->mix_mfma; return FPTA_OK;
     case FPTA_OPT_OVERLAP: *value = c->overlap; return FPTA_OK;
     case FPTA_OPT_INTERP_LDS: *value = c->interp_lds; return FPTA_OK;
+    case FPTA_OPT_GRID_COALESCE: *value = c->grid_coalesce; return FPTA_OK;
+    case FPTA_OPT_INTERP_WS: *value = c->interp_ws; return FPTA_OK;
   }
   return fail(c, FPTA_EINVAL, "get_option: unknown key");
 }
@@ -1617,6 +1807,7 @@ int fpta_batch_set_white(fpta_ctx* c, const double* sigma, int64_t n_blocks, con
 
 static int batch_common(fpta_ctx* c, uint64_t seed, int64_t real0, int32_t n_real, const double* zin,
                         int32_t zin_nm, double* out, double* coeffs_out, bool white) {
+  double* const coeffs_host = coeffs_out;
   if (!c) return fail(nullptr, FPTA_EINVAL, "null ctx");
   Layout& L = c->batch;
   if (L.P <= 0) return fail(c, FPTA_ESTATE, "batch_synth: set_toas first");
@@ -1657,10 +1848,19 @@ static int batch_common(fpta_ctx* c, uint64_t seed, int64_t real0, int32_t n_rea
   if (L.segs.empty()) {
     HIPCHK(c, hipMemsetAsync(c->out.p, 0, out_bytes, c->stream), "out memset");
   } else {
+    int path = 0;
+    if ((rc = select_path(c, L, n_real, true, &path))) return rc;
+    bool coef_done = false;
+    // pipelined gridded block: draws, merges and DFT on the side stream, overlapping the previous block's
+    // interpolation (not for zin blocks: their draws read an upload queued on the ctx stream)
+    const bool pipe = c->overlap != 0 && path == 4 && !zin;
+    if ((rc = run_coefficients(c, L, seed, real0, n_real, R_pad, zin, zin_nm, nullptr, c->overlap != 0, path == 4,
+                               coeffs_out, &coef_done, pipe)))
+      return rc;
+    if (coef_done) coeffs_out = nullptr;  // downloaded before the coalesced grid signals were merged
     c->coef_copy_pending = coeffs_out != nullptr;
-    if ((rc = run_coefficients(c, L, seed, real0, n_real, R_pad, zin, zin_nm, nullptr, c->overlap != 0))) return rc;
     if ((rc = run_synth(c, L, n_real, R_pad, c->out.as<double>(), L.n_toa, 0, true, do_white ? &wc : nullptr,
-                        &fused)))
+                        &fused, path, pipe)))
       return rc;
   }
   if (do_white && !fused) {
@@ -1679,7 +1879,7 @@ static int batch_common(fpta_ctx* c, uint64_t seed, int64_t real0, int32_t n_rea
                             sizeof(double) * n_real, (size_t)L.P * L.K, hipMemcpyDeviceToHost, c->stream),
            "coef download");
   }
-  if (out || coeffs_out) HIPCHK(c, hipStreamSynchronize(c->stream), "batch sync");
+  if (out || coeffs_out || coeffs_host) HIPCHK(c, hipStreamSynchronize(c->stream), "batch sync");
   return FPTA_OK;
 }
 
@@ -1806,6 +2006,10 @@ int fpta_batch_grid_info(fpta_ctx* c, double* out) {
   out[9] = std::exp(-M_PI * c->grid_w * std::sqrt(1.0 - 100.0 / c->grid_sigma100));
   out[10] = c->grid_w;
   out[11] = c->grid_sigma100 / 100.0;
+  out[12] = ok ? (double)G.segs.size() : 0.0;
+  out[13] = (double)c->batch.segs.size();
+  out[14] = ok ? G.mean_v : 0.0;
+  out[15] = 0.0;
   return FPTA_OK;
 }
 

@@ -96,6 +96,16 @@ struct GridSegs {
   int32_t n;
 };
 
+// Coalesced grid signal (FPTA_OPT_GRID_COALESCE): coef[p][dst + j][r] += sum_i coef[p][src_i + j][r], j < ncol_i,
+// in source order (deterministic), before the DFT of the group reads columns dst ..
+struct CoefMerge {
+  int32_t dst;               // first coefficient column of the group's anchor (largest mode count)
+  int32_t n;                 // other members
+  int32_t src[kGridMaxSeg];  // first column of each other member
+  int32_t ncol[kGridMaxSeg]; // its columns (2 x padded modes)
+};
+hipError_t launch_coef_merge(hipStream_t st, const CoefMerge& m, int32_t P, int32_t K, int32_t R_pad, double* coef);
+
 hipError_t launch_grid_weights(hipStream_t st, const SegDesc& sd, int64_t n_toa, const double* nu,
                                const int32_t* chunk_of, const int32_t* tt_of, const int32_t* row_of,
                                const double* d_of, int32_t w, double beta, int32_t vmax, double* wd);
@@ -114,6 +124,9 @@ struct GridBand {
   int64_t grid_rows;
 };
 hipError_t launch_grid_interp_mfma(hipStream_t st, const SynthArgs& a, const GridBand& band, int32_t R_pad);
+// Warp-specialised variant (producer waves stage operands in an LDS ring, compute waves never load from global memory,
+// so their stores never hold up an operand); no white epilogue, no accumulate
+hipError_t launch_grid_interp_ws(hipStream_t st, const SynthArgs& a, const GridBand& band, int32_t R_pad);
 // LDS-staged variant: the 4 waves of a workgroup take <= kLdsGroup consecutive chunks of one pulsar for the same
 // realizations; the union of their band rows (<= kLdsRowsMax) is loaded once into LDS
 constexpr int kLdsGroup = 4, kLdsRowsMax = 144;

@@ -18,6 +18,19 @@ namespace fpta {
 
 typedef double dbl2 __attribute__((ext_vector_type(2)));
 
+// A wave-uniform read of a table the kernel never writes, through the constant address space: a scalar load
+// (lgkmcnt). A plain load of it is a vector load once the kernel has stores the compiler cannot rule out as aliasing,
+// and waiting for it (vmcnt) then also waits for every store issued before it.
+template <class T>
+__device__ __forceinline__ T ld_uniform(const T* p) {
+  return *(const __attribute__((address_space(4))) T*)p;
+}
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ int4 ld_uniform4(const void* p) {
+  const i32x4 v = ld_uniform((const i32x4*)p);
+  return make_int4(v.x, v.y, v.z, v.w);
+}
+
 // k_grid_interp_mfma: 32 TOAs x 16 kInterpRW realizations per wave, kInterpWPC persistent workgroups per CU
 // (compile-time; tools/interp_variants.sh builds the alternatives it measures into build/diag)
 #ifndef FPTA_INTERP_RW
@@ -137,6 +150,34 @@ __global__ __launch_bounds__(256, 3) void k_grid_dft_mfma(GridSegs gsegs, const 
       }
 }
 
+// ----------------------------------------------------------------------------- k_coef_merge
+// Coalesced grid signal: the anchor's coefficient columns += every other member's (same modes k = m + 1, same w0,
+// same chromatic weight per TOA), summed in member order. Thread = 2 adjacent realizations of one column.
+__global__ __launch_bounds__(256) void k_coef_merge(CoefMerge m, int32_t K, int32_t R_pad,
+                                                    double* __restrict__ coef) {
+  const int r = (blockIdx.x * 256 + threadIdx.x) * 2;
+  if (r >= R_pad) return;
+  const int j = blockIdx.y;
+  const int64_t prow = (int64_t)blockIdx.z * K;
+  double* __restrict__ dst = coef + (prow + m.dst + j) * R_pad + r;
+  dbl2 acc = *(const dbl2*)dst;
+  for (int i = 0; i < m.n; ++i)
+    if (j < m.ncol[i]) acc += *(const dbl2*)(coef + (prow + m.src[i] + j) * R_pad + r);
+  *(dbl2*)dst = acc;
+}
+
+hipError_t launch_coef_merge(hipStream_t st, const CoefMerge& m, int32_t P, int32_t K, int32_t R_pad, double* coef) {
+  if (m.n <= 0 || m.n > kGridMaxSeg || R_pad % 2 != 0 || P <= 0 || P > 65535) return hipErrorInvalidValue;
+  int32_t jmax = 0;
+  for (int i = 0; i < m.n; ++i) {
+    if (m.src[i] < 0 || m.ncol[i] <= 0 || m.src[i] + m.ncol[i] > K || m.dst + m.ncol[i] > K) return hipErrorInvalidValue;
+    jmax = std::max(jmax, m.ncol[i]);
+  }
+  hipLaunchKernelGGL(k_coef_merge, dim3((unsigned)((R_pad / 2 + 255) / 256), (unsigned)jmax, (unsigned)P), dim3(256),
+                     0, st, m, K, R_pad, coef);
+  return hipGetLastError();
+}
+
 // White-noise normals of (TOA t, global realizations g, g + 1 of the pair containing g): the
 // realization-paired stream of oracle.white_normals_rpairs (same words as kernels.hip white_pair).
 __device__ __forceinline__ void mfma_white_pair(int64_t t, int64_t g, uint32_t k0, uint32_t k1, double& z0,
@@ -184,7 +225,7 @@ __device__ __forceinline__ void interp_white(const SynthArgs& a, const InterpTil
   const int lr = lane & 15, lg = lane >> 4;
   const int tt = 2 * lr;  // this lane's even TOA in the chunk; tt + 1 the odd one
   if (tt >= t.cnt) return;
-  const int64_t tg = a.offs[t.p] + t.y + tt;
+  const int64_t tg = ld_uniform(a.offs + t.p) + t.y + tt;
   {
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
@@ -301,7 +342,7 @@ __device__ __forceinline__ void interp_store_rows(const SynthArgs& a, double* __
   const int lr = lane & 15, lg = lane >> 4;
   const int tt = 2 * lr;  // this lane's even TOA in the chunk; tt + 1 the odd one
   if (tt >= t.cnt) return;
-  const int64_t tg = a.offs[t.p] + t.y + tt;
+  const int64_t tg = ld_uniform(a.offs + t.p) + t.y + tt;
 #if FPTA_INTERP_DIAG == 2  // diagnostic build only: no stores (one conditional store keeps every sum live)
   {
     double s = 0.0;
@@ -389,7 +430,11 @@ __global__ __launch_bounds__(256, FPTA_INTERP_WPC) void k_grid_interp_mfma(Synth
     const int32_t* __restrict__ rt = band.rows + (int64_t)t.c * band.vmax;
 #pragma unroll
     for (int i = 0; i < kGridVMax / 64; ++i) t.rr[i] = rt[min(64 * i + lane, 4 * t.nq - 1)];
-    t.G0 = band.g + t.r0 + 2 * lr;
+    // a realization block past R_pad (R_pad not a multiple of 64 RW): this wave computes on block 0's columns and
+    // stores nothing. Tiles of one wave alternate realization blocks, so this is decided per tile, never by exiting
+    // (an exit on the first tile's block dropped the wave's later valid tiles, and a later invalid tile read past
+    // its rows and wrote another chunk's partial checksums)
+    t.G0 = band.g + (t.r0 < R_pad ? t.r0 : 0) + 2 * lr;
     t.Wp = band.wd + ((int64_t)t.c * band.vmax + lg) * kGridTT + 2 * lr;
   };
   auto load = [&](const InterpTile<RW>& t, int qq, dbl2(&av)[NP], dbl2& bv) {
@@ -425,8 +470,7 @@ __global__ __launch_bounds__(256, FPTA_INTERP_WPC) void k_grid_interp_mfma(Synth
 #endif
   InterpTile<RW> cur;
   setup(tile, cur);
-  if (cur.r0 >= R_pad) return;  // this wave's realization block is padding for every tile of the launch
-  FPTA_DCHECK(cur.r0 + 16 * RW <= R_pad, "k_grid_interp_mfma realization block", cur.r0 + 16 * RW, R_pad + 1);
+  FPTA_DCHECK(R_pad % (16 * RW) == 0, "k_grid_interp_mfma realization padding", R_pad % (16 * RW), 1);
   dbl2 a0[NP], a1[NP], b0, b1;
   load(cur, 0, a0, b0);
   load(cur, min(1, cur.nq - 1), a1, b1);
@@ -456,8 +500,10 @@ __global__ __launch_bounds__(256, FPTA_INTERP_WPC) void k_grid_interp_mfma(Synth
     if constexpr (WHITE) {
       // the Philox rounds of the white epilogue and a second tile's operands do not fit in the register budget
       // together: this variant stores first, then starts the next tile
-      interp_white<RW>(a, cur, acc);
-      interp_store<PART, RW>(a, out, cur, acc);
+      if (cur.r0 < R_pad) {
+        interp_white<RW>(a, cur, acc);
+        interp_store<PART, RW>(a, out, cur, acc);
+      }
       tile += stride;
       if (tile >= end) break;
       setup(tile, cur);
@@ -474,10 +520,193 @@ __global__ __launch_bounds__(256, FPTA_INTERP_WPC) void k_grid_interp_mfma(Synth
         load(nxt, min(1, nxt.nq - 1), a1, b1);
       }
       __builtin_amdgcn_sched_barrier(0);
-      interp_store<PART, RW>(a, out, cur, acc);
+      if (cur.r0 < R_pad) interp_store<PART, RW>(a, out, cur, acc);
       if (!more) break;
       cur = nxt;
     }
+  }
+}
+
+// ----------------------------------------------------------------------------- k_grid_interp_ws
+// The interpolation with warp-specialised roles, so the residual stores never stall an operand load. In
+// k_grid_interp_mfma a wave's loads and stores retire through one in-order counter (vmcnt): every load issued after
+// a tile's 32 stores waits for them, and the MFMA and store streams serialise (0.42 ms without stores, 0.33 ms of
+// stores alone, 0.63 ms together on C2). Here a workgroup (one per CU) has 4 compute waves and 4 producer waves:
+//  * producer wave p loads, kWsLead steps ahead, the 4 grid rows of compute wave p's 128 realizations and weight
+//    row p of the step, with direct-to-LDS loads (five wave-instructions per step) into a ring of kWsSlots slots;
+//    it waits only for its own loads (vmcnt) and never stores;
+//  * compute wave w reads its operands from LDS (lgkmcnt), runs the same MFMA steps as k_grid_interp_mfma (even /
+//    odd TOA B-tiles, realization tile pairs) and stores the tile; it issues no global load, so it never waits for
+//    its stores;
+//  * one s_barrier per band step: before barrier S the producers' loads of step S + 1 have landed and the compute
+//    waves' reads of step S are done, so slot (S + kWsLead) mod kWsSlots (step S - 1's) can be refilled after it.
+// Every wave walks the same tiles and steps (a tile = one chunk x 512 realizations), so all issue the same number
+// of barriers; compute waves whose realizations lie past R_pad compute on clamped rows and store nothing. The
+// barrier is a plain s_barrier: __syncthreads() would add a workgroup fence, i.e. vmcnt(0) on the stores.
+constexpr int kWsLead = 7;
+constexpr int kWsSlots = kWsLead + 1;
+constexpr int kWsSlotGrid = 4 * 4 * 128;          // doubles: [band row j][compute wave][128 realizations]
+constexpr int kWsSlot = kWsSlotGrid + 4 * kGridTT;  // + [band row j][32 TOAs] weights: 17 KB per slot
+constexpr int kWsLoadsPerStep = 5;                // per producer: 4 grid rows + 1 weight row
+
+// s_waitcnt with only vmcnt <= N (lgkmcnt, expcnt not waited), and with only lgkmcnt(0)
+template <int N>
+__device__ __forceinline__ void ws_wait_vm() {
+  static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+__device__ __forceinline__ void ws_wait_lgkm0() { __builtin_amdgcn_s_waitcnt(15 | (3 << 14) | (7 << 4)); }
+__device__ __forceinline__ void ws_barrier() { asm volatile("s_barrier" ::: "memory"); }
+// vmcnt <= kWsLoadsPerStep * n, n = the steps whose loads may stay in flight (0 .. kWsLead - 1)
+__device__ __forceinline__ void ws_wait_steps(int n) {
+  if (n <= 0) ws_wait_vm<0>();
+  else if (n == 1) ws_wait_vm<kWsLoadsPerStep>();
+  else if (n == 2) ws_wait_vm<2 * kWsLoadsPerStep>();
+  else if (n == 3) ws_wait_vm<3 * kWsLoadsPerStep>();
+  else if (n == 4) ws_wait_vm<4 * kWsLoadsPerStep>();
+  else if (n == 5) ws_wait_vm<5 * kWsLoadsPerStep>();
+  else ws_wait_vm<6 * kWsLoadsPerStep>();
+  static_assert(kWsLead - 1 <= 6, "ws_wait_steps covers up to 6 steps in flight");
+}
+
+template <bool PART>
+__global__ __launch_bounds__(512, 1) void k_grid_interp_ws(SynthArgs a, GridBand band, int32_t n_tiles, int32_t R_pad,
+                                                           double* __restrict__ out) {
+  constexpr int RW = 8, NP = RW / 2;
+  static_assert(kGridTT == 32, "two 16-TOA B-tiles per chunk");
+  __shared__ __attribute__((aligned(16))) double ring[kWsSlots * kWsSlot];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int lr = lane & 15, lg = lane >> 4;
+  const int per = (n_tiles + 7) >> 3;
+  const int x = blockIdx.x & 7;
+  const int stride = gridDim.x >> 3;
+  const int end = min(n_tiles, (x + 1) * per);
+  const int first = x * per + (int)(blockIdx.x >> 3);
+  const int n_rb = (R_pad + 511) / 512;
+  const bool producer = wave >= 4;
+  const int w = wave & 3;  // compute wave w, or the producer serving it
+  if (first >= end) return;  // no tile: every wave of the workgroup leaves (no barrier issued)
+
+  if (producer) {
+    // cursor of the step the producer loads next: tile, step q of nq, chunk, realization base. Everything it
+    // reads besides the operands is wave-uniform (scalar loads), so its vmcnt counts the ring loads alone.
+    int tile = first, q = 0, nq = 0, c = 0, r0 = 0;
+    auto setup = [&]() {
+      c = __builtin_amdgcn_readfirstlane(tile / n_rb);
+      const int rb = __builtin_amdgcn_readfirstlane(tile - c * n_rb);
+      r0 = rb * 512 + w * 128;
+      if (r0 >= R_pad) r0 = 0;  // a compute wave past R_pad: valid rows, its sums are never stored
+      nq = __builtin_amdgcn_readfirstlane(ld_uniform4(band.chunks + c).w) >> 2;
+    };
+    int issued = 0;  // steps whose loads are issued
+    bool valid = true;
+    setup();
+    auto issue = [&]() {
+      double* slot = ring + (issued % kWsSlots) * kWsSlot;
+#if FPTA_INTERP_DIAG == 6  // diagnostic build only: the producers load nothing (stale operands, same barriers)
+      if (issued >= 0) {
+        ++issued;
+        if (++q == nq) {
+          q = 0;
+          tile += stride;
+          valid = tile < end;
+          if (valid) setup();
+        }
+        return;
+      }
+#endif
+      const int4 r4 = ld_uniform4(band.rows + (int64_t)c * band.vmax + 4 * q);  // the step's 4 rows
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int row = __builtin_amdgcn_readfirstlane(j == 0 ? r4.x : (j == 1 ? r4.y : (j == 2 ? r4.z : r4.w)));
+        FPTA_DCHECK(row >= 0 && row < band.grid_rows, "k_grid_interp_ws grid row", row, band.grid_rows);
+        __builtin_amdgcn_global_load_lds((const void*)(band.g + (int64_t)row * R_pad + r0 + 2 * lane),
+                                         (__attribute__((address_space(3))) void*)(slot + (j * 4 + w) * 128), 16, 0,
+                                         0);
+      }
+      // weight row w of the step: 32 doubles = 64 dwords, one per lane
+      __builtin_amdgcn_global_load_lds(
+          (const void*)((const uint32_t*)(band.wd + ((int64_t)c * band.vmax + 4 * q + w) * kGridTT) + lane),
+          (__attribute__((address_space(3))) void*)(slot + kWsSlotGrid + w * kGridTT), 4, 0, 0);
+      ++issued;
+      if (++q == nq) {
+        q = 0;
+        tile += stride;
+        valid = tile < end;
+        if (valid) setup();
+      }
+    };
+    for (int i = 0; i < kWsLead && valid; ++i) issue();
+    ws_wait_steps(issued - 1);  // step 0 has landed
+    ws_barrier();
+    // iteration S: refill the slot of step S - 1 with step S + kWsLead, make sure step S + 1 has landed
+    for (int S = 0;; ++S) {
+      if (valid) issue();
+      ws_wait_steps(issued - (S + 2));
+      // the barrier count must equal the compute waves': one per step of the workgroup's tiles
+      if (S + 1 >= issued && !valid) {
+        ws_barrier();
+        break;
+      }
+      ws_barrier();
+    }
+    return;
+  }
+
+  // compute wave
+  d4 acc[2][RW];
+#pragma unroll
+  for (int e = 0; e < 2; ++e)
+#pragma unroll
+    for (int i = 0; i < RW; ++i) acc[e][i] = d4{0.0, 0.0, 0.0, 0.0};
+  auto read = [&](int S, dbl2(&av)[NP], dbl2& bv) {
+    const double* slot = ring + (S % kWsSlots) * kWsSlot;
+#pragma unroll
+    for (int m = 0; m < NP; ++m) av[m] = *(const dbl2*)(slot + (lg * 4 + w) * 128 + 32 * m + 2 * lr);
+    bv = *(const dbl2*)(slot + kWsSlotGrid + lg * kGridTT + 2 * lr);
+  };
+  auto mfma = [&](const dbl2(&av)[NP], const dbl2& bv) {
+#pragma unroll
+    for (int m = 0; m < NP; ++m) {
+      acc[0][2 * m] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m].x, bv.x, acc[0][2 * m], 0, 0, 0);
+      acc[0][2 * m + 1] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m].y, bv.x, acc[0][2 * m + 1], 0, 0, 0);
+      acc[1][2 * m] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m].x, bv.y, acc[1][2 * m], 0, 0, 0);
+      acc[1][2 * m + 1] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m].y, bv.y, acc[1][2 * m + 1], 0, 0, 0);
+    }
+  };
+  dbl2 a0[NP], a1[NP], b0, b1;
+  ws_barrier();  // step 0 has landed
+  read(0, a0, b0);
+  ws_wait_lgkm0();
+  int S = 0;
+  for (int tile = first; tile < end; tile += stride) {
+    InterpTile<RW> t;
+    t.c = __builtin_amdgcn_readfirstlane(tile / n_rb);
+    const int rb = __builtin_amdgcn_readfirstlane(tile - t.c * n_rb);
+    t.r0 = rb * 512 + w * 128;
+    const int4 ci = ld_uniform4(band.chunks + t.c);
+    t.p = __builtin_amdgcn_readfirstlane(ci.x);
+    t.y = __builtin_amdgcn_readfirstlane(ci.y);
+    t.cnt = __builtin_amdgcn_readfirstlane(ci.z);
+    t.nq = __builtin_amdgcn_readfirstlane(ci.w) >> 2;
+    // step S's operands in (a0, b0); step S + 1's are read from LDS after barrier S, while step S's MFMAs run
+    for (int q = 0; q < t.nq; ++q, ++S) {
+      ws_barrier();  // step S + 1 has landed; step S - 1's slot may now be refilled
+      read(S + 1, a1, b1);
+#if FPTA_INTERP_DIAG != 4  // diagnostic build 4: no MFMA steps (the epilogue stores zeros)
+      mfma(a0, b0);
+#endif
+      ws_wait_lgkm0();
+#pragma unroll
+      for (int m = 0; m < NP; ++m) a0[m] = a1[m];
+      b0 = b1;
+    }
+    if (t.r0 < R_pad) interp_store<PART, RW>(a, out, t, acc);
+#pragma unroll
+    for (int e = 0; e < 2; ++e)
+#pragma unroll
+      for (int i = 0; i < RW; ++i) acc[e][i] = d4{0.0, 0.0, 0.0, 0.0};
   }
 }
 
@@ -608,6 +837,27 @@ hipError_t launch_grid_interp_lds(hipStream_t st, const SynthArgs& a, const Grid
   auto kernel = a.part ? k_grid_interp_lds<false, true> : k_grid_interp_lds<false, false>;
   hipLaunchKernelGGL(kernel, dim3((unsigned)grid), dim3(256), lds_bytes, st, a, band, lds, (int32_t)tiles, R_pad,
                      a.out);
+  return hipGetLastError();
+}
+
+hipError_t launch_grid_interp_ws(hipStream_t st, const SynthArgs& a, const GridBand& band, int32_t R_pad) {
+  if (band.n_chunks <= 0 || band.vmax < 4 || band.vmax % 4 != 0 || band.vmax > kGridVMax || R_pad % 128 != 0 ||
+      a.w_on || a.accumulate)
+    return hipErrorInvalidValue;
+  const int32_t n_rb = (R_pad + 511) / 512;
+  const int64_t tiles = (int64_t)band.n_chunks * n_rb;
+  if (tiles > 0x7FFFFFFF) return hipErrorInvalidValue;
+  static int n_cu = 0;
+  if (!n_cu) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0)
+      n_cu = 256;
+  }
+  // persistent: one workgroup per CU (the ring takes 136 KB of the 160 KB LDS)
+  const int64_t grid = std::min<int64_t>((tiles + 7) / 8 * 8, ((int64_t)n_cu + 7) / 8 * 8);
+  auto kernel = a.part ? k_grid_interp_ws<true> : k_grid_interp_ws<false>;
+  hipLaunchKernelGGL(kernel, dim3((unsigned)grid), dim3(512), 0, st, a, band, (int32_t)tiles, R_pad, a.out);
   return hipGetLastError();
 }
 

@@ -207,8 +207,9 @@ int fpta_batch_info(fpta_ctx* ctx, int64_t* info);
  * realization, out[5] direct-contraction FMAs per realization, out[6] grid values per realization,
  * out[7] interpolation-weight bytes, out[8] the FPTA_OPT_GRID_MFMA mask in force, out[9] the a-priori
  * relative aliasing bound exp(-pi w sqrt(1 - 1/sigma)) of the width/oversampling options in force (auto
- * selection takes the gridded path only when it is <= 2e-12), out[10] width w, out[11] oversampling sigma.
- * out: host double[12]. */
+ * selection takes the gridded path only when it is <= 2e-12), out[10] width w, out[11] oversampling sigma,
+ * out[12] grid signals of the plan (signals after FPTA_OPT_GRID_COALESCE), out[13] layout signals, out[14]
+ * mean band rows per chunk (all grid signals, padded to 4). out: host double[16]. */
 int fpta_batch_grid_info(fpta_ctx* ctx, double* out);
 /* Why the last batch did not take the gridded path (signal count, non-harmonic grid, error bound, cost,
  * n_real below the threshold, ...); "" when it did. Owned by the context, valid until the next batch. */
@@ -269,6 +270,15 @@ int fpta_multi_synth(fpta_multi* m, uint64_t seed, int64_t real0, int64_t n_real
                                      (k_grid_interp_lds) where every group fits and no white noise is fused;
                                      0 (default, faster on MI355X) the register-tiled k_grid_interp_mfma.
                                      Results are identical. */
+#define FPTA_OPT_GRID_COALESCE 14 /* gridded path: 1 (default) sums, in coefficient space, the signals of a pulsar
+                                     that share the base frequency w0 and the chromatic weight on every TOA (e.g.
+                                     red noise and a common GWB on the pulsar's own span, or DM noise at a single
+                                     radio frequency): they then share one grid and one interpolation band. Exact
+                                     algebra (the sum is linear); results agree with 0 to rounding. */
+#define FPTA_OPT_INTERP_WS 15     /* gridded interpolation: 1 (default) the warp-specialised k_grid_interp_ws
+                                     (producer waves stage the operands in an LDS ring, compute waves only store,
+                                     so stores never delay an operand load) for blocks without fused white noise;
+                                     0 the register-pipelined k_grid_interp_mfma. Results are identical. */
 int fpta_set_option(fpta_ctx* ctx, int32_t key, int64_t value);
 /* Current value of option `key` (same keys as fpta_set_option). */
 int fpta_get_option(fpta_ctx* ctx, int32_t key, int64_t* value);

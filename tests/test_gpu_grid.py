@@ -308,3 +308,152 @@ def test_lds_interpolation_is_bitwise_identical(ctx, capi, shipped, fuse):
         np.testing.assert_array_equal(res[0][1], res[1][1])
     finally:
         ctx.set_options(shipped)
+
+
+def _shared_span_layout(ctx, rng, P=12, n=(300, 700), nu_const=True, with_masked=False):
+    """Pulsars on one common span T (as make_fake_array with equal Tobs): red noise, DM (idx 2) and a common
+    GWB all sit on f_k = k / T. At a single radio frequency (nu == freqf) DM's chromatic weight is 1, so the
+    three share w0 and the weight per TOA and coalesce into one grid signal; with several radio frequencies
+    only RN and the GWB do. A masked signal (backend noise) never joins an unmasked one."""
+    counts = rng.integers(n[0], n[1], size=P)
+    offs = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
+    t0, t1 = 4.4e9, 4.4e9 + 3.15e8
+    toas = np.concatenate([np.concatenate([[t0], np.sort(rng.uniform(t0, t1, k - 2)), [t1]]) for k in counts])
+    nu = np.full(offs[-1], 1400.0) if nu_const else rng.choice([800.0, 1400.0, 2500.0], size=offs[-1])
+    T = t1 - t0
+    ctx.batch_set_toas(offs, toas, nu)
+    segs = []
+    for nm, idx in ((30, 0.0), (100, 2.0)):
+        f = np.tile(np.arange(1, nm + 1) / T, (P, 1))
+        a = np.sqrt(O.powerlaw(f, rng.uniform(-14.5, -13.5, (P, 1)), 3.0) / T)
+        ctx.batch_add_signal(0, f, a, idx=idx)
+        segs.append(O.Segment(0, 2 * np.pi * f, a, idx))
+    fc = np.arange(1, 31) / T
+    ac = np.sqrt(O.powerlaw(fc, -14.0, 13 / 3) / T)
+    v = rng.normal(size=(P, 3))
+    L = O.mvn_factor(O.orf_hd(v / np.linalg.norm(v, axis=1)[:, None]))
+    ctx.batch_add_signal(1, fc, ac, L=L)
+    segs.append(O.Segment(1, 2 * np.pi * fc, ac, 0.0, L=L))
+    if with_masked:
+        mask = (np.arange(offs[-1]) % 3 == 0).astype(np.uint8)
+        f = np.tile(np.arange(1, 21) / T, (P, 1))
+        a = np.sqrt(O.powerlaw(f, -13.8, 2.0) / T)
+        ctx.batch_add_signal(0, f, a, idx=0.0, mask=mask)
+        segs.append(O.Segment(0, 2 * np.pi * f, a, 0.0, mask=mask.astype(bool)))
+    return offs, toas, nu, segs
+
+
+@pytest.mark.parametrize("nu_const,with_masked,n_grid", [(True, False, 1), (False, False, 2), (True, True, 2)])
+def test_coalesced_grid_signals(ctx, capi, shipped, nu_const, with_masked, n_grid):
+    """FPTA_OPT_GRID_COALESCE: signals sharing w0 and the chromatic weight share one grid; the block matches the
+    oracle at the gridded tolerance and the un-coalesced plan to rounding, coefficient downloads still return
+    every signal's own draws (taken before the merge), and the side stream gives bit-identical blocks."""
+    rng = np.random.default_rng(53 + n_grid + 7 * with_masked)
+    offs, toas, nu, segs = _shared_span_layout(ctx, rng, nu_const=nu_const, with_masked=with_masked)
+    try:
+        ctx.set_option(capi.OPT_SYNTH_PATH, 4)
+        got, co = ctx.batch_synth(11, 5, 150, coeffs=True)
+        gi = ctx.batch_grid_info()
+        assert gi["grid_signals"] == n_grid and gi["signals"] == len(segs), gi
+        want = O.batch_synth(offs, toas, nu, segs, 11, 5, 150)
+        assert rel_err(got, want) <= GRID_TOL
+        assert_parity(got, want, TOL)
+        ctx.set_option(capi.OPT_OVERLAP, 0)
+        np.testing.assert_array_equal(ctx.batch_synth(11, 5, 150), got)
+        ctx.set_option(capi.OPT_OVERLAP, 1)
+        ctx.set_option(capi.OPT_GRID_COALESCE, 0)
+        sep, co_sep = ctx.batch_synth(11, 5, 150, coeffs=True)
+        assert ctx.batch_grid_info()["grid_signals"] == len(segs)
+        np.testing.assert_array_equal(co, co_sep)
+        assert rel_err(got, sep) <= GRID_TOL
+    finally:
+        ctx.set_options(shipped)
+
+
+@pytest.mark.parametrize("fuse", [0, 1])
+@pytest.mark.parametrize("layout", ["coalesced", "single"])
+def test_pipelined_batches_are_bitwise_identical(ctx, capi, shipped, fuse, layout):
+    """Pipelined gridded batches (FPTA_OPT_OVERLAP 1): a streamed shard draws, merges and transforms block b + 1 on
+    the side stream into the other grid buffer while block b interpolates; the per-realization checksums of 5
+    back-to-back blocks (no host round trip) equal the single-stream ones bit for bit, with and without fused
+    checksums, for a coalesced multi-signal layout and a one-signal (C3-like) layout."""
+    rng = np.random.default_rng(61)
+    if layout == "coalesced":
+        _shared_span_layout(ctx, rng, nu_const=False)
+    else:
+        offs, toas, nu = random_layout(rng, 20, (100, 400))
+        ctx.batch_set_toas(offs, toas, nu)
+        f, a, L, _ = common_signal(rng, offs, toas, 30)
+        ctx.batch_add_signal(1, f, a, L=L)
+    try:
+        ctx.set_option(capi.OPT_SYNTH_PATH, 4)
+        ctx.set_option(capi.OPT_FUSE_CHECKSUMS, fuse)
+        res = {}
+        for ov in (0, 1):
+            ctx.set_option(capi.OPT_OVERLAP, ov)
+            res[ov] = ctx.batch_synth_checksums(21, 3, 5 * 256 - 17, batch=256)
+        np.testing.assert_array_equal(res[0], res[1])
+    finally:
+        ctx.set_options(shipped)
+
+
+@pytest.mark.parametrize("fuse", [0, 1])
+@pytest.mark.parametrize("R", [333, 1024, 1100])
+def test_warp_specialised_interpolation_is_bitwise_identical(ctx, capi, shipped, fuse, R):
+    """FPTA_OPT_INTERP_WS: the warp-specialised interpolation (producer waves fill an LDS ring, compute waves run the
+    same MFMA steps and only store) returns the register-pipelined kernel's block and checksums bit for bit, on a
+    ragged multi-signal layout with unsorted TOAs, for realization counts that leave compute waves idle (R_pad not a
+    multiple of 512)."""
+    rng = np.random.default_rng(43)
+    offs, toas, nu = random_layout(rng, 23, (31, 260))
+    perm = rng.permutation(offs[1] - offs[0])
+    toas[offs[0]:offs[1]] = toas[offs[0]:offs[1]][perm]
+    ctx.batch_set_toas(offs, toas, nu)
+    f, a = per_psr_signal(rng, offs, toas, 30)
+    ctx.batch_add_signal(0, f, a, idx=0.0)
+    f, a = per_psr_signal(rng, offs, toas, 100)
+    ctx.batch_add_signal(0, f, a, idx=2.0)
+    f, a, L, _ = common_signal(rng, offs, toas, 30)
+    ctx.batch_add_signal(1, f, a, L=L)
+    try:
+        ctx.set_option(capi.OPT_SYNTH_PATH, 4)
+        ctx.set_option(capi.OPT_FUSE_CHECKSUMS, fuse)
+        res = {}
+        for ws in (0, 1):
+            ctx.set_option(capi.OPT_INTERP_WS, ws)
+            res[ws] = (ctx.batch_synth(5, 300, R), ctx.batch_checksums())
+        np.testing.assert_array_equal(res[0][0], res[1][0])
+        np.testing.assert_array_equal(res[0][1], res[1][1])
+    finally:
+        ctx.set_options(shipped)
+
+
+@pytest.mark.parametrize("ws", [0, 1])
+@pytest.mark.parametrize("R", [1100, 1696])
+def test_partial_realization_blocks_write_every_sample(ctx, capi, shipped, ws, R):
+    """Regression: R_pad not a multiple of 512 (a C3 shard's last batch of 1696) gives persistent interpolation
+    waves tiles of a realization block past R_pad between valid ones. Every sample must be written (the block is
+    poisoned with NaN first) and the fused partial checksums must match a full pass over the block; the register
+    kernel once exited on its first tile's block (dropping later valid tiles) and let later invalid tiles write
+    another chunk's partials."""
+    rng = np.random.default_rng(47)
+    offs, toas, nu = random_layout(rng, 40, (300, 900))
+    ctx.batch_set_toas(offs, toas, nu)
+    f, a, L, _ = common_signal(rng, offs, toas, 30)
+    ctx.batch_add_signal(1, f, a, L=L)
+    segs = [O.Segment(1, 2 * np.pi * f, a, 0.0, L=L)]
+    try:
+        ctx.set_option(capi.OPT_SYNTH_PATH, 4)
+        ctx.set_option(capi.OPT_INTERP_WS, ws)
+        ctx.set_option(capi.OPT_FUSE_CHECKSUMS, 1)
+        ctx.batch_synth(9, 0, R, to_host=False)
+        ctx.debug_fill_out(np.nan)
+        got = ctx.batch_synth(9, 64, R)
+        sums = ctx.batch_checksums()
+        assert np.all(np.isfinite(got))
+        want = O.batch_synth(offs, toas, nu, segs, 9, 64, R)
+        assert rel_err(got, want) <= GRID_TOL
+        np.testing.assert_allclose(sums[:, 0], got.sum(axis=1), rtol=1e-10, atol=1e-12 * np.abs(got).max())
+        np.testing.assert_allclose(sums[:, 1], (got * got).sum(axis=1), rtol=1e-10)
+    finally:
+        ctx.set_options(shipped)

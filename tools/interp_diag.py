@@ -19,6 +19,7 @@ def main():
     ap.add_argument("--grid-mfma", type=int, default=-1)
     ap.add_argument("--label", default="")
     ap.add_argument("--width", type=int, default=0)
+    ap.add_argument("--ws", type=int, default=-1, help="FPTA_OPT_INTERP_WS (-1: library default)")
     args = ap.parse_args()
     import bench
     from fakepta_amd import _capi
@@ -30,6 +31,8 @@ def main():
     ctx.set_option(_capi.OPT_OVERLAP, 0)  # the kernels alone (no co-running draws of the next batch)
     if args.grid_mfma >= 0:
         ctx.set_option(_capi.OPT_GRID_MFMA, args.grid_mfma)
+    if args.ws >= 0:
+        ctx.set_option(_capi.OPT_INTERP_WS, args.ws)
     if args.width:
         ctx.set_option(_capi.OPT_GRID_WIDTH, args.width)
     for i in range(3):

@@ -2,12 +2,12 @@
 # Build (build) or time (run) compile-time variants of k_grid_interp_mfma: realization tiles per wave (RW),
 # persistent workgroups per CU (WPC), diagnostic cuts (DIAG 1: grid loads from one L1-resident row; 2: no
 # stores; 3: non-temporal stores; 4: no band loop, the store stream alone; 5: every other workgroup starts
-# ~7 us late). VARIANTS entries are RW:WPC:DIAG. Throwaway libraries in build/diag, loaded by tools/interp_diag.py
+# ~7 us late; 6: k_grid_interp_ws producers load nothing). WS selects FPTA_OPT_INTERP_WS values to time. VARIANTS entries are RW:WPC:DIAG. Throwaway libraries in build/diag, loaded by tools/interp_diag.py
 # through FAKEPTA_AMD_LIB; never the product or the bench. Results: profiles/r02_interp_diag*.txt (a single
 # operand set at 3 workgroups per CU measured 0.70 ms against 0.66 for the shipped 2-deep pipeline at 2).
 S=fakepta_amd/csrc
 D=build/diag
-VARIANTS="8:2:0 8:2:5"
+VARIANTS=${VARIANTS:-"8:2:0 8:2:2 8:2:4 8:2:6"}
 if [ "$1" = build ]; then
   mkdir -p $D
   for v in $VARIANTS; do
@@ -22,5 +22,7 @@ fi
 set -o pipefail
 for v in $VARIANTS; do
   IFS=: read rw wpc dg <<< "$v"
-  FAKEPTA_AMD_LIB=$D/lib_rw${rw}_wpc${wpc}_d${dg}.so timeout -k 5 120 python tools/interp_diag.py --label "rw$rw-wpc$wpc-d$dg" || exit 1
+  for ws in ${WS:-0 1}; do
+    FAKEPTA_AMD_LIB=$D/lib_rw${rw}_wpc${wpc}_d${dg}.so timeout -k 5 120 python tools/interp_diag.py --ws $ws --label "rw$rw-wpc$wpc-d$dg-ws$ws" || exit 1
+  done
 done
