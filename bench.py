@@ -35,7 +35,7 @@ FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 matrix (= vector) peak, AMD datasheet (M
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 SYNTH_KERNELS = {3: ("k_synth_valu_seeded<2,16>", "fp64-valu"), 2: ("k_synth_mfma<4,2>", "fp64-mfma"),
                  1: ("k_synth_direct", "fp64-valu")}
-GRID_INTERP = ("k_grid_interp_mfma<false, false, 8>", "fp64-mfma")
+GRID_INTERP = {0: ("k_grid_interp_mfma<false, false, 8>", "fp64-mfma"), 1: ("k_grid_interp_ws<false>", "fp64-mfma")}
 # layout tag of the gridded plan a PMC traffic record must carry to describe the shipped interpolation kernel
 # (32-TOA chunks, every signal's band back to back); untagged records describe round-1 kernels of the same name
 GRID_LAYOUT = "band32"
@@ -59,6 +59,8 @@ def parse():
     ap.add_argument("--path", type=int, default=0, help="synthesis path: 0 auto, 1 direct, 2 MFMA, 3 VALU, 4 gridded")
     ap.add_argument("--grid-mfma", type=int, default=-1,
                     help="gridded path kernels on MFMA: bit 0 DFT, bit 1 interpolation (-1: library default)")
+    ap.add_argument("--interp-ws", type=int, default=-1,
+                    help="gridded interpolation kernel: 1 warp-specialised, 0 register-pipelined (-1: library default)")
     ap.add_argument("--exact-launches", type=int, default=5,
                     help="launches of the exact fused kernel (path 3) timed after the run for roofline_exact")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL on ROCm) or gloo (CPU rehearsal)")
@@ -249,6 +251,8 @@ def main():
         ctx.set_option(_capi.OPT_SYNTH_PATH, args.path)
     if args.grid_mfma >= 0:
         ctx.set_option(_capi.OPT_GRID_MFMA, args.grid_mfma)
+    if args.interp_ws >= 0:
+        ctx.set_option(_capi.OPT_INTERP_WS, args.interp_ws)
 
     if args.config == "c2":
         R = args.real
@@ -301,7 +305,7 @@ def main():
     n_launch_real = R if args.config == "c2" else n_job / max(1, -(-shard_bounds(n_job, 0, world)[1] // R))
     out_bytes = 8.0 * info["n_toa"] * n_launch_real
     if path == 4:
-        kernel, pipe = GRID_INTERP
+        kernel, pipe = GRID_INTERP[ctx.get_option(_capi.OPT_INTERP_WS)]
         traffic, traffic_src = pmc_traffic(kernel, info, R, args.traffic, GRID_LAYOUT)
         achieved = out_bytes / synth_avg_s / 1e9
         R_pad = -(-int(n_launch_real) // 128) * 128

@@ -343,7 +343,7 @@ __device__ __forceinline__ void interp_store_rows(const SynthArgs& a, double* __
   const int tt = 2 * lr;  // this lane's even TOA in the chunk; tt + 1 the odd one
   if (tt >= t.cnt) return;
   const int64_t tg = ld_uniform(a.offs + t.p) + t.y + tt;
-#if FPTA_INTERP_DIAG == 2  // diagnostic build only: no stores (one conditional store keeps every sum live)
+#if FPTA_INTERP_DIAG == 2 || FPTA_INTERP_DIAG == 7  // diagnostic builds only: no stores (one conditional store keeps every sum live)
   {
     double s = 0.0;
 #pragma unroll
@@ -442,7 +442,7 @@ __global__ __launch_bounds__(256, FPTA_INTERP_WPC) void k_grid_interp_mfma(Synth
     const int src = blk == 0 ? t.rr[0] : (blk == 1 ? t.rr[1] : (blk == 2 ? t.rr[2] : t.rr[3]));
     const int row = __builtin_amdgcn_ds_bpermute(((4 * qq + lg) & 63) << 2, src);
     FPTA_DCHECK(row >= 0 && row < band.grid_rows, "k_grid_interp_mfma grid row", row, band.grid_rows);
-#if FPTA_INTERP_DIAG == 1  // diagnostic build only (tools/interp_variants.sh): every step reads one L1-resident row
+#if FPTA_INTERP_DIAG == 1 || FPTA_INTERP_DIAG == 7  // diagnostic builds only (tools/interp_variants.sh): every step reads one L1-resident row
     const double* __restrict__ gr = t.G0 + (int64_t)(row & 3) * R_pad;
 #else
     const double* __restrict__ gr = t.G0 + (int64_t)row * R_pad;
@@ -453,6 +453,16 @@ __global__ __launch_bounds__(256, FPTA_INTERP_WPC) void k_grid_interp_mfma(Synth
   };
   d4 acc[2][RW];  // [TOA parity][realization tile]
   auto mfma = [&](const dbl2(&av)[NP], const dbl2& bv) {
+#if FPTA_INTERP_DIAG == 8  // diagnostic build only: accumulators pinned to AGPRs (MFMA by inline asm)
+#pragma unroll
+    for (int m = 0; m < NP; ++m) {
+      asm volatile("v_mfma_f64_16x16x4_f64 %0, %1, %2, %0" : "+a"(acc[0][2 * m]) : "v"(av[m].x), "v"(bv.x));
+      asm volatile("v_mfma_f64_16x16x4_f64 %0, %1, %2, %0" : "+a"(acc[0][2 * m + 1]) : "v"(av[m].y), "v"(bv.x));
+      asm volatile("v_mfma_f64_16x16x4_f64 %0, %1, %2, %0" : "+a"(acc[1][2 * m]) : "v"(av[m].x), "v"(bv.y));
+      asm volatile("v_mfma_f64_16x16x4_f64 %0, %1, %2, %0" : "+a"(acc[1][2 * m + 1]) : "v"(av[m].y), "v"(bv.y));
+    }
+    return;
+#endif
 #pragma unroll
     for (int m = 0; m < NP; ++m) {
       acc[0][2 * m] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m].x, bv.x, acc[0][2 * m], 0, 0, 0);
@@ -467,6 +477,9 @@ __global__ __launch_bounds__(256, FPTA_INTERP_WPC) void k_grid_interp_mfma(Synth
 #if FPTA_INTERP_DIAG == 5  // diagnostic build only: every other workgroup starts half a tile late (phase stagger)
   if ((blockIdx.x >> 3) & 1)
     for (int i = 0; i < 2; ++i) __builtin_amdgcn_s_sleep(127);
+#endif
+#if FPTA_INTERP_DIAG == 9  // diagnostic build only: the 8 waves of a CU start 0..7 units of ~3.4 us apart
+  for (int i = 0; i < wave + 4 * ((blockIdx.x >> 3) & 1); ++i) __builtin_amdgcn_s_sleep(127);
 #endif
   InterpTile<RW> cur;
   setup(tile, cur);
@@ -543,7 +556,10 @@ __global__ __launch_bounds__(256, FPTA_INTERP_WPC) void k_grid_interp_mfma(Synth
 // Every wave walks the same tiles and steps (a tile = one chunk x 512 realizations), so all issue the same number
 // of barriers; compute waves whose realizations lie past R_pad compute on clamped rows and store nothing. The
 // barrier is a plain s_barrier: __syncthreads() would add a workgroup fence, i.e. vmcnt(0) on the stores.
-constexpr int kWsLead = 7;
+#ifndef FPTA_WS_LEAD
+#define FPTA_WS_LEAD 3
+#endif
+constexpr int kWsLead = FPTA_WS_LEAD;  // 3: a 4-slot ring (68 KB) leaves a CU room for co-running DFT / draw waves
 constexpr int kWsSlots = kWsLead + 1;
 constexpr int kWsSlotGrid = 4 * 4 * 128;          // doubles: [band row j][compute wave][128 realizations]
 constexpr int kWsSlot = kWsSlotGrid + 4 * kGridTT;  // + [band row j][32 TOAs] weights: 17 KB per slot
