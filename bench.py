@@ -37,8 +37,8 @@ SYNTH_KERNELS = {3: ("k_synth_valu_seeded<2,16>", "fp64-valu"), 2: ("k_synth_mfm
                  1: ("k_synth_direct", "fp64-valu")}
 GRID_INTERP = {0: ("k_grid_interp_mfma<false, false, 8>", "fp64-mfma"), 1: ("k_grid_interp_ws<false>", "fp64-mfma")}
 # layout tag of the gridded plan a PMC traffic record must carry to describe the shipped interpolation kernel
-# (32-TOA chunks, every signal's band back to back); untagged records describe round-1 kernels of the same name
-GRID_LAYOUT = "band32"
+# (32-TOA chunks, every grid signal's band back to back, coalesced signals); older tags describe earlier plans
+GRID_LAYOUT = "band32c"
 GRID_DFT = {True: "k_grid_dft_mfma<2,4>", False: "k_grid_dft<8>"}
 
 
@@ -61,6 +61,8 @@ def parse():
                     help="gridded path kernels on MFMA: bit 0 DFT, bit 1 interpolation (-1: library default)")
     ap.add_argument("--interp-ws", type=int, default=-1,
                     help="gridded interpolation kernel: 1 warp-specialised, 0 register-pipelined (-1: library default)")
+    ap.add_argument("--overlap", type=int, default=-1,
+                    help="FPTA_OPT_OVERLAP: 1 pipelined blocks (side stream), 0 one stream (-1: library default)")
     ap.add_argument("--exact-launches", type=int, default=5,
                     help="launches of the exact fused kernel (path 3) timed after the run for roofline_exact")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL on ROCm) or gloo (CPU rehearsal)")
@@ -228,6 +230,26 @@ def exact_roofline(ctx, capi, sim, seed, R, launches):
             "frac": achieved / FP64_PEAK_TFLOPS, "write_GBps": 8.0 * info["n_toa"] * R / t / 1e9}
 
 
+def isolated_grid(ctx, capi, sim, seed, R, launches):
+    """The gridded kernels on the same batch with one stream (FPTA_OPT_OVERLAP 0), after the timed run: in the
+    pipelined timed region the interpolation shares the CUs with the next block's draws and DFT, so its HIP-event
+    time there includes that co-running work. Returns (interpolation, DFT) average launch seconds."""
+    old = ctx.get_option(capi.OPT_OVERLAP)
+    ctx.set_option(capi.OPT_OVERLAP, 0)
+    ctx.set_option(capi.OPT_PROFILE, 1)
+    try:
+        sim.synth(R, seed=seed, real0=0, to_host=False)
+        ctx.synchronize()
+        ctx.reset_stats()
+        for i in range(launches):
+            sim.synth(R, seed=seed, real0=(i + 1) * R, to_host=False)
+        ctx.synchronize()
+        return kernel_avg_s(ctx, capi.K_SYNTH), kernel_avg_s(ctx, capi.K_GRID)
+    finally:
+        ctx.set_option(capi.OPT_OVERLAP, old)
+        ctx.set_option(capi.OPT_PROFILE, 0)
+
+
 def main():
     args = parse()
     refuse_debug_environment()
@@ -253,6 +275,8 @@ def main():
         ctx.set_option(_capi.OPT_GRID_MFMA, args.grid_mfma)
     if args.interp_ws >= 0:
         ctx.set_option(_capi.OPT_INTERP_WS, args.interp_ws)
+    if args.overlap >= 0:
+        ctx.set_option(_capi.OPT_OVERLAP, args.overlap)
 
     if args.config == "c2":
         R = args.real
@@ -336,6 +360,12 @@ def main():
                     "traffic_source": traffic_src, "flops_per_launch": flops, "avg_launch_ms": synth_avg_s * 1e3,
                     "write_GBps": out_bytes / synth_avg_s / 1e9}
 
+    if path == 4 and args.config == "c2" and args.exact_launches > 0:
+        t_int, t_dft = isolated_grid(ctx, _capi, sim, args.seed, R, args.exact_launches)
+        roofline["isolated"] = {"note": "same batch, one stream (no co-running draws / DFT), after the timed run",
+                                "avg_launch_ms": t_int * 1e3, "achieved": out_bytes / t_int / 1e9,
+                                "frac": out_bytes / t_int / 1e9 / HBM_PEAK_GBS, "dft_avg_launch_ms": t_dft * 1e3,
+                                "dft_TFLOPs": 2.0 * gi["fma_dft"] * (-(-R // 128) * 128) / t_dft / 1e12}
     roofline_exact = None
     if args.config == "c2" and args.exact_launches > 0:
         roofline_exact = exact_roofline(ctx, _capi, sim, args.seed, R, args.exact_launches)

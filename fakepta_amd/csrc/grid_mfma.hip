@@ -42,7 +42,11 @@ __device__ __forceinline__ int4 ld_uniform4(const void* p) {
 #ifndef FPTA_INTERP_DIAG
 #define FPTA_INTERP_DIAG 0  // 0 in every product build
 #endif
+#ifndef FPTA_INTERP_DEPTH
+#define FPTA_INTERP_DEPTH 2
+#endif
 constexpr int kInterpRW = FPTA_INTERP_RW;
+constexpr int kInterpDepth = FPTA_INTERP_DEPTH;  // k_grid_interp_mfma: steps of operand prefetch (2 or 3)
 constexpr int kInterpWPC = FPTA_INTERP_WPC;
 
 // ----------------------------------------------------------------------------- k_grid_dft_mfma
@@ -484,30 +488,49 @@ __global__ __launch_bounds__(256, FPTA_INTERP_WPC) void k_grid_interp_mfma(Synth
   InterpTile<RW> cur;
   setup(tile, cur);
   FPTA_DCHECK(R_pad % (16 * RW) == 0, "k_grid_interp_mfma realization padding", R_pad % (16 * RW), 1);
+  // operand sets: step q's operands are loaded kInterpDepth steps ahead (FPTA_INTERP_DEPTH 2 or 3). After a tile's
+  // epilogue the first load that waits (vmcnt) for its 32 stores is that of step kInterpDepth of the next tile.
   dbl2 a0[NP], a1[NP], b0, b1;
-  load(cur, 0, a0, b0);
-  load(cur, min(1, cur.nq - 1), a1, b1);
+#if FPTA_INTERP_DEPTH == 3
+  dbl2 a2[NP], b2;
+#endif
+  auto prefetch = [&](const InterpTile<RW>& t) {
+    load(t, 0, a0, b0);
+    load(t, min(1, t.nq - 1), a1, b1);
+#if FPTA_INTERP_DEPTH == 3
+    load(t, min(2, t.nq - 1), a2, b2);
+#endif
+  };
+  prefetch(cur);
   while (true) {
 #pragma unroll
     for (int e = 0; e < 2; ++e)
 #pragma unroll
       for (int i = 0; i < RW; ++i) acc[e][i] = d4{0.0, 0.0, 0.0, 0.0};
-    // steps q (in a0) and q + 1 (in a1) are loaded; each set is refilled two steps ahead right after its MFMAs
+    // each operand set is refilled kInterpDepth steps ahead right after its MFMAs
 #if FPTA_INTERP_DIAG == 4  // diagnostic build only: no band loop (the epilogue stores zeros): the store stream alone
-    for (int q = cur.nq; q < cur.nq; q += 2) {
+    for (int q = cur.nq; q < cur.nq; q += kInterpDepth) {
 #else
-    for (int q = 0; q < cur.nq; q += 2) {
+    for (int q = 0; q < cur.nq; q += kInterpDepth) {
 #endif
       __builtin_amdgcn_sched_barrier(0);
       mfma(a0, b0);
       __builtin_amdgcn_sched_barrier(0);
-      if (q + 2 < cur.nq) load(cur, q + 2, a0, b0);
+      if (q + kInterpDepth < cur.nq) load(cur, q + kInterpDepth, a0, b0);
       __builtin_amdgcn_sched_barrier(0);
       if (q + 1 < cur.nq) {
         mfma(a1, b1);
         __builtin_amdgcn_sched_barrier(0);
-        if (q + 3 < cur.nq) load(cur, q + 3, a1, b1);
+        if (q + 1 + kInterpDepth < cur.nq) load(cur, q + 1 + kInterpDepth, a1, b1);
       }
+#if FPTA_INTERP_DEPTH == 3
+      __builtin_amdgcn_sched_barrier(0);
+      if (q + 2 < cur.nq) {
+        mfma(a2, b2);
+        __builtin_amdgcn_sched_barrier(0);
+        if (q + 2 + kInterpDepth < cur.nq) load(cur, q + 2 + kInterpDepth, a2, b2);
+      }
+#endif
     }
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (WHITE) {
@@ -520,17 +543,15 @@ __global__ __launch_bounds__(256, FPTA_INTERP_WPC) void k_grid_interp_mfma(Synth
       tile += stride;
       if (tile >= end) break;
       setup(tile, cur);
-      load(cur, 0, a0, b0);
-      load(cur, min(1, cur.nq - 1), a1, b1);
+      prefetch(cur);
     } else {
-      // next tile: its first two steps are in flight before this tile's stores enter the vmcnt queue
+      // next tile: its first steps are in flight before this tile's stores enter the vmcnt queue
       tile += stride;
       const bool more = tile < end;
       InterpTile<RW> nxt = cur;
       if (more) {
         setup(tile, nxt);
-        load(nxt, 0, a0, b0);
-        load(nxt, min(1, nxt.nq - 1), a1, b1);
+        prefetch(nxt);
       }
       __builtin_amdgcn_sched_barrier(0);
       if (cur.r0 < R_pad) interp_store<PART, RW>(a, out, cur, acc);

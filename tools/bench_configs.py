@@ -103,12 +103,14 @@ def c4():
     offs = (np.arange(P + 1) * n_p).astype(np.int64)
     toas = (np.linspace(0, T, n_p)[None, :] + rng.uniform(0, 86400, (P, 1))).ravel()
     nu = np.abs(1400.0 + rng.normal(0, 10, P * n_p))
-    from fakepta.correlated_noises import orf_factor
+    from fakepta_amd.batch import batch_factor
     class _P:  # noqa: E306
         def __init__(self, p):
             self.pos = p
     from fakepta.correlated_noises import hd
-    L = orf_factor(hd([_P(x) for x in fib(P)]))
+    # the batch path's factor (fakepta_amd.batch.batch_factor, as BatchSimulator): Cholesky of the positive-definite
+    # HD ORF, so k_mix_mfma stops each pulsar tile's q loop at its last pulsar (half the FLOPs of the SVD factor)
+    L = batch_factor(hd([_P(x) for x in fib(P)]))
     f = np.arange(1, N + 1) / np.ptp(toas)
     amp = np.sqrt(O.powerlaw(f, -15.0, 13 / 3) * O.delta_f(f))
     ctx.batch_set_toas(offs, toas, nu)
@@ -118,7 +120,9 @@ def c4():
     return dict(config="c4", K=2 * N, n_toa=P * n_p, realizations=R, ms_per_step=dt / 5 * 1e3,
                 samples_per_s=P * n_p * R * 5 / dt, kernels_ms_per_step=kt, path=ctx.batch_grid_info()["last_path"],
                 synth_direct_equiv_tflops=flops / ((kt["synth"] + kt["grid"]) / 1e3) / 1e12,
-                mix_tflops=2.0 * P * P * 2 * N * R / (kt["mix"] / 1e3) / 1e12 if kt["mix"] else None)
+                mix_factor="cholesky" if np.all(np.triu(L, 1) == 0) else "svd",
+                mix_tflops=(P * (P + 1) if np.all(np.triu(L, 1) == 0) else 2.0 * P * P) * 2 * N * R / (kt["mix"] / 1e3) / 1e12
+                if kt["mix"] else None)
 
 
 def c5():

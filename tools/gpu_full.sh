@@ -18,7 +18,7 @@ for p in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 120 rocprofv3 --pmc $p --output-format csv -d ${o}_traffic/pass$i -o run -- python bench.py --steps 5 --warmup 2 --cpu-sample 0 --exact-launches 0 > ${o}_traffic_$p.log 2>&1 || { tail -20 ${o}_traffic_$p.log; exit 1; }
   i=$((i+1))
 done
-python tools/collect_traffic.py ${o}_traffic ${o}_grid_traffic.json 320 200000 1024 k_grid_interp_mfma band32 || exit 1
+python tools/collect_traffic.py ${o}_traffic ${o}_grid_traffic.json 320 200000 1024 k_grid_interp_ws band32c || exit 1
 timeout -k 10 300 python -u bench.py --traffic ${o}_grid_traffic.json > ${o}_bench.log 2>&1 || { tail -20 ${o}_bench.log; exit 1; }
 cat ${o}_bench.log
 timeout -k 10 300 python -u bench.py --config c3 --cpu-sample 0 > ${o}_bench_c3.log 2>&1 || { tail -20 ${o}_bench_c3.log; exit 1; }
