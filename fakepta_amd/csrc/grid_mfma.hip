@@ -358,6 +358,28 @@ __device__ __forceinline__ void interp_store_rows(const SynthArgs& a, double* __
     return;
   }
 #endif
+  // fast path (full chunk, every realization of the tile stored, no accumulate, 16-byte aligned rows): straight-line
+  // 16-byte stores from a wave-uniform row base plus one 32-bit lane offset, no per-store tests. The general path
+  // below spends ~28 instructions and several branches per store, which held the SIMD's issue while the partner
+  // wave's MFMAs needed it.
+  {
+    const int64_t t0 = tg - tt;  // wave-uniform first sample of the chunk
+    const bool fast = t.cnt == kGridTT && !a.accumulate && t.r0 + 16 * RW <= a.n_real &&
+                      ((((uintptr_t)(out + t0)) | ((uintptr_t)a.ldo << 3)) & 15) == 0 &&
+                      a.ldo < ((int64_t)1 << 26);  // lane offsets (< 6 ldo + 32 doubles) fit 32 bits
+    if (__builtin_amdgcn_readfirstlane(fast ? 1 : 0)) {
+      const uint32_t vo = (uint32_t)(((int64_t)2 * lg * a.ldo + tt) * 8);
+      const char* base = (const char*)(out + t0 + (int64_t)t.r0 * a.ldo);
+#pragma unroll
+      for (int i = 0; i < RW; ++i)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int k = 32 * (i >> 1) + 8 * g + (i & 1);  // row of (tile i, register g) past r0 + 2 lg
+          *(dbl2*)((char*)base + (int64_t)k * a.ldo * 8 + vo) = dbl2{acc[0][i][g], acc[1][i][g]};
+        }
+      return;
+    }
+  }
   // one 16-byte store per (lane, realization) when both TOAs exist and the row offset r * ldo + tg keeps 16-byte
   // alignment (ldo and tg even), else the pair is stored as two 8-byte stores
   double* __restrict__ ocol = out + tg;

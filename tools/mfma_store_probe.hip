@@ -9,6 +9,9 @@
 //           L2-resident table, two steps ahead: the interpolation's operand stream)
 //   mode 6: as mode 5 with the operands read from LDS (ds_read_b128) instead
 //   mode 7: as mode 5 without stores
+//   mode 8: as mode 5 with the interpolation's store addresses: out[r][t] with a row pitch of 200,000 doubles, a
+//           wave's 128 realization rows (r0 + 32 m + 2 (lg + 4 g) + h) x the 32 TOAs of its chunk, chunks walked
+//           as the persistent tiles are
 // Prints per mode the time and the MFMA / store rates. hipcc --offload-arch=gfx950 -O3 tools/mfma_store_probe.hip
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -25,9 +28,9 @@ __global__ __launch_bounds__(512, 1) void probe(double* __restrict__ out, long l
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const bool compute = MODE == 0 || MODE == 3 || MODE >= 5 || ((MODE == 2 || MODE == 4) && wave < 4);
-  const bool store = MODE == 1 || MODE == 3 || MODE == 5 || MODE == 6 || (MODE == 2 && wave >= 4) ||
+  const bool store = MODE == 1 || MODE == 3 || MODE == 5 || MODE == 6 || MODE == 8 || (MODE == 2 && wave >= 4) ||
                      (MODE == 4 && wave < 4);
-  constexpr bool LOADS = MODE >= 5;
+  constexpr bool LOADS = MODE >= 5;  // modes 5-8
   if (MODE == 6) {
     for (int i = threadIdx.x; i < 8192; i += 512) lds[i] = table[i];
     __syncthreads();
@@ -74,6 +77,19 @@ __global__ __launch_bounds__(512, 1) void probe(double* __restrict__ out, long l
       }
     }
     if (store) {
+      if (MODE == 8) {
+        // tile t of this wave: chunk (blockIdx.x + gridDim.x * t) mod 6250, realization block (wave & 3) x 128 of
+        // 1024 (waves 4-7 the same blocks on the next chunk), 200,000 TOAs per row
+        const long long chunk = ((long long)blockIdx.x * 2 + (wave >> 2) + (long long)gridDim.x * 2 * t) % 6250;
+        const int r0 = (wave & 3) * 128, lr = lane & 15, lg = lane >> 4;
+#pragma unroll
+        for (int s = 0; s < kStorePerTile; ++s) {
+          const int i = s >> 2, g = s & 3;
+          const int r = r0 + 32 * (i >> 1) + 2 * (lg + 4 * g) + (i & 1);
+          const double v = acc[s & 15][s >> 4];
+          *(dbl2*)(out + (long long)r * 200000 + chunk * 32 + 2 * lr) = dbl2{v, v + 1.0};
+        }
+      } else
 #pragma unroll
       for (int s = 0; s < kStorePerTile; ++s) {
         // 4 rows of 256 B per instruction (the interpolation's store shape), rows spread over the buffer
@@ -134,6 +150,7 @@ int main() {
   run(probe<5>, "mode 5 + operand loads (global)", 8, 8);
   run(probe<6>, "mode 6 + operand loads (LDS)", 8, 8);
   run(probe<7>, "mode 7 operand loads, no stores", 8, 0);
+  run(probe<8>, "mode 8 mode 5, interpolation addresses", 8, 8);
   if (hipDeviceSynchronize() != hipSuccess) return 2;
   return 0;
 }
