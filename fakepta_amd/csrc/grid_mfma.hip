@@ -62,20 +62,28 @@ constexpr int kInterpWPC = FPTA_INTERP_WPC;
 // one 16-byte value per lane (256-byte runs per grid row). Wave tile 16 MJ rows x 16 MR realizations. The table
 // is zero-padded to ntab (multiple of 8) modes and lde (multiple of 16 MJ) rows; padded coefficient modes
 // re-read the signal's last mode (finite) against zero table rows.
+// Grid (1-D, XCD-grouped): a coefficient tile T = (pulsar, 64 MR-realization block) has nz row blocks over all
+// signals, which read the same coefficients; workgroup b runs on XCD b % 8 and the nz row blocks of one tile are
+// consecutive workgroups of one XCD, so the tile is read from HBM once and re-read from that XCD's L2 (a 3-D grid
+// with the row block slowest re-read every coefficient tile from HBM per row block: 0.83 GB per C2 launch).
 template <int MJ, int MR>
 __global__ __launch_bounds__(256, 3) void k_grid_dft_mfma(GridSegs gsegs, const double* __restrict__ coef,
-                                                          int32_t K, int32_t R_pad) {
+                                                          int32_t K, int32_t R_pad, int32_t n_xb, int32_t P,
+                                                          int32_t nz) {
   static_assert(MJ % 2 == 0 && MR % 2 == 0, "operands come in tile pairs");
   constexpr int PJ = MJ / 2, PR = MR / 2;
-  int bz = blockIdx.z, s = 0;
+  const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
+  const int tile = (slot / nz) * 8 + xcd;
+  if (tile >= n_xb * P) return;
+  const int bx = tile % n_xb, p = tile / n_xb;
+  int bz = slot - (slot / nz) * nz, s = 0;
   while (s + 1 < gsegs.n && bz >= gsegs.s[s].nblk) bz -= gsegs.s[s++].nblk;
   const GridSegDev& gs = gsegs.s[s];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const int lr = lane & 15, lg = lane >> 4;
-  const int r0 = (blockIdx.x * 4 + wave) * 16 * MR;
+  const int r0 = (bx * 4 + wave) * 16 * MR;
   if (r0 >= R_pad) return;
-  const int p = blockIdx.y;
   const int j0 = bz * 16 * MJ;
   const double* __restrict__ cp = coef + ((int64_t)p * K + gs.col0 + 2 * lg) * R_pad + r0 + 2 * lr;
   const double* __restrict__ ec = gs.ecos + (int64_t)lg * gs.lde + j0 + 2 * lr;
@@ -932,10 +940,12 @@ hipError_t launch_grid_dft_mfma(hipStream_t st, GridSegs gsegs, int32_t P, const
     if (g.lde < g.nblk * 16 * kDftMJ || g.ntab < ((g.nm + 7) & ~7)) return hipErrorInvalidValue;
     gz += g.nblk;
   }
-  if (gz > 65535) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((k_grid_dft_mfma<kDftMJ, kDftMR>),
-                     dim3((unsigned)((R_pad + 64 * kDftMR - 1) / (64 * kDftMR)), (unsigned)P, (unsigned)gz), dim3(256),
-                     0, st, gsegs, coef, K, R_pad);
+  const int64_t n_xb = (R_pad + 64 * kDftMR - 1) / (64 * kDftMR);
+  const int64_t n_tiles = n_xb * P;
+  const int64_t blocks = (n_tiles + 7) / 8 * 8 * gz;  // 8 tiles (one per XCD) x gz row blocks per group of slots
+  if (gz > 65535 || blocks > 0x7FFFFFFF) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((k_grid_dft_mfma<kDftMJ, kDftMR>), dim3((unsigned)blocks), dim3(256), 0, st, gsegs, coef, K,
+                     R_pad, (int32_t)n_xb, P, (int32_t)gz);
   return hipGetLastError();
 }
 

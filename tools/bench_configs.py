@@ -116,13 +116,19 @@ def c4():
     ctx.batch_set_toas(offs, toas, nu)
     ctx.batch_add_signal(1, f, amp, idx=0.0, L=L)
     dt, kt = timed(ctx, _capi, lambda s: ctx.batch_synth(7, s * R, R, to_host=False), 5, warmup=1)
+    # kernel times with one stream (pipelined blocks share the CUs, so their HIP-event times overlap)
+    ctx.set_option(_capi.OPT_OVERLAP, 0)
+    _, kt1 = timed(ctx, _capi, lambda s: ctx.batch_synth(7, (s + 10) * R, R, to_host=False), 3, warmup=1)
+    ctx.set_option(_capi.OPT_OVERLAP, 1)
+    kt = dict(kt, isolated=kt1)
     flops = 2.0 * 2 * N * P * n_p * R
     return dict(config="c4", K=2 * N, n_toa=P * n_p, realizations=R, ms_per_step=dt / 5 * 1e3,
                 samples_per_s=P * n_p * R * 5 / dt, kernels_ms_per_step=kt, path=ctx.batch_grid_info()["last_path"],
-                synth_direct_equiv_tflops=flops / ((kt["synth"] + kt["grid"]) / 1e3) / 1e12,
+                synth_direct_equiv_tflops=flops / ((kt1["synth"] + kt1["grid"]) / 1e3) / 1e12,
                 mix_factor="cholesky" if np.all(np.triu(L, 1) == 0) else "svd",
-                mix_tflops=(P * (P + 1) if np.all(np.triu(L, 1) == 0) else 2.0 * P * P) * 2 * N * R / (kt["mix"] / 1e3) / 1e12
-                if kt["mix"] else None)
+                mix_ms_isolated=kt1["mix"],
+                mix_tflops=(P * (P + 1) if np.all(np.triu(L, 1) == 0) else 2.0 * P * P) * 2 * N * R / (kt1["mix"] / 1e3) / 1e12
+                if kt1["mix"] else None)
 
 
 def c5():
