@@ -329,7 +329,10 @@ def main():
     n_launch_real = R if args.config == "c2" else n_job / max(1, -(-shard_bounds(n_job, 0, world)[1] // R))
     out_bytes = 8.0 * info["n_toa"] * n_launch_real
     if path == 4:
-        kernel, pipe = GRID_INTERP[ctx.get_option(_capi.OPT_INTERP_WS)]
+        # the warp-specialised kernel serves plain blocks; fused-checksum blocks (c3) take the register kernel
+        kernel, pipe = GRID_INTERP[ctx.get_option(_capi.OPT_INTERP_WS) if args.config == "c2" else 0]
+        if args.config != "c2":
+            kernel = kernel.replace("false, false", "false, true")
         traffic, traffic_src = pmc_traffic(kernel, info, R, args.traffic, GRID_LAYOUT)
         achieved = out_bytes / synth_avg_s / 1e9
         R_pad = -(-int(n_launch_real) // 128) * 128

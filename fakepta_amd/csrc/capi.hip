@@ -1063,7 +1063,9 @@ int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad, bool pipe = fa
   KTimer kt(c, FPTA_K_SYNTH);
   GridBand band{G.chunks.as<int4>(), G.rows.as<int32_t>(), G.wd.as<double>(), gbase, G.n_chunks, G.vmax,
                 G.grid_rows};
-  if (c->interp_ws && !c->interp_lds && !a.w_on && !a.accumulate) {
+  // the warp-specialised kernel for plain blocks; with fused partial checksums its reduce-scatter temporaries take
+  // its VGPRs to 230 and the register kernel is faster (C3: 47.9 vs 52.5 ms per job, profiles/r02k_ab_c2c3_ws.txt)
+  if (c->interp_ws && !c->interp_lds && !a.w_on && !a.accumulate && !a.part) {
     HIPCHK(c, launch_grid_interp_ws(c->stream, a, band, R_pad), "k_grid_interp_ws launch");
   } else if (c->interp_lds && G.lds_ok && !a.w_on) {
     GridLds lds{G.groups.as<int4>(), G.urows.as<int32_t>(), G.lrows.as<int32_t>(), G.n_groups, G.lds_rows};

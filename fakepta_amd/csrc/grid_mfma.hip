@@ -383,7 +383,10 @@ __device__ __forceinline__ void interp_store_rows(const SynthArgs& a, double* __
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const int k = 32 * (i >> 1) + 8 * g + (i & 1);  // row of (tile i, register g) past r0 + 2 lg
-          *(dbl2*)((char*)base + (int64_t)k * a.ldo * 8 + vo) = dbl2{acc[0][i][g], acc[1][i][g]};
+          // non-temporal: the block is never re-read by this kernel, and L2-allocating 1.6 GB of stores would evict
+          // the grid rows the next chunks re-read (they then queue behind the write stream: tools/mfma_store_probe)
+          __builtin_nontemporal_store(dbl2{acc[0][i][g], acc[1][i][g]},
+                                      (dbl2*)((char*)base + (int64_t)k * a.ldo * 8 + vo));
         }
       return;
     }
@@ -923,8 +926,8 @@ hipError_t launch_grid_interp_ws(hipStream_t st, const SynthArgs& a, const GridB
   }
   // persistent: one workgroup per CU (the ring takes 136 KB of the 160 KB LDS)
   const int64_t grid = std::min<int64_t>((tiles + 7) / 8 * 8, ((int64_t)n_cu + 7) / 8 * 8);
-  auto kernel = a.part ? k_grid_interp_ws<true> : k_grid_interp_ws<false>;
-  hipLaunchKernelGGL(kernel, dim3((unsigned)grid), dim3(512), 0, st, a, band, (int32_t)tiles, R_pad, a.out);
+  if (a.part) return hipErrorInvalidValue;  // fused partial checksums take k_grid_interp_mfma (faster there)
+  hipLaunchKernelGGL(k_grid_interp_ws<false>, dim3((unsigned)grid), dim3(512), 0, st, a, band, (int32_t)tiles, R_pad, a.out);
   return hipGetLastError();
 }
 

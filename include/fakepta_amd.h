@@ -277,7 +277,8 @@ int fpta_multi_synth(fpta_multi* m, uint64_t seed, int64_t real0, int64_t n_real
                                      algebra (the sum is linear); results agree with 0 to rounding. */
 #define FPTA_OPT_INTERP_WS 15     /* gridded interpolation: 1 (default) the warp-specialised k_grid_interp_ws
                                      (producer waves stage the operands in an LDS ring, compute waves only store,
-                                     so stores never delay an operand load) for blocks without fused white noise;
+                                     so stores never delay an operand load) for blocks without fused white noise
+                                     or fused partial checksums;
                                      0 the register-pipelined k_grid_interp_mfma. Results are identical. */
 int fpta_set_option(fpta_ctx* ctx, int32_t key, int64_t value);
 /* Current value of option `key` (same keys as fpta_set_option). */

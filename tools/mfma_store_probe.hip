@@ -9,6 +9,9 @@
 //           L2-resident table, two steps ahead: the interpolation's operand stream)
 //   mode 6: as mode 5 with the operands read from LDS (ds_read_b128) instead
 //   mode 7: as mode 5 without stores
+//   mode 9: as mode 8 with the operands read from a 256 MiB table (rows re-read ~5 times, as the grid rows are)
+//   mode 10: as mode 9 without stores
+//   modes 11-14: mode 9 with the stores' cache policy bits: nt / sc1 / sc0 sc1 / nt sc0 sc1
 //   mode 8: as mode 5 with the interpolation's store addresses: out[r][t] with a row pitch of 200,000 doubles, a
 //           wave's 128 realization rows (r0 + 32 m + 2 (lg + 4 g) + h) x the 32 TOAs of its chunk, chunks walked
 //           as the persistent tiles are
@@ -23,14 +26,16 @@ constexpr int kMfmaPerTile = 160, kStorePerTile = 32;
 
 template <int MODE>
 __global__ __launch_bounds__(512, 1) void probe(double* __restrict__ out, long long n_rows, int tiles, double seed,
-                                                 double* __restrict__ sink, const double* __restrict__ table) {
+                                                 double* __restrict__ sink, const double* __restrict__ table,
+                                                 const double* __restrict__ big) {
   __shared__ double lds[8192];  // 64 KB operand image (mode 6)
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const bool compute = MODE == 0 || MODE == 3 || MODE >= 5 || ((MODE == 2 || MODE == 4) && wave < 4);
-  const bool store = MODE == 1 || MODE == 3 || MODE == 5 || MODE == 6 || MODE == 8 || (MODE == 2 && wave >= 4) ||
+  const bool store = MODE == 1 || MODE == 3 || MODE == 5 || MODE == 6 || MODE == 8 || MODE == 9 || MODE >= 11 ||
+                     (MODE == 2 && wave >= 4) ||
                      (MODE == 4 && wave < 4);
-  constexpr bool LOADS = MODE >= 5;  // modes 5-8
+  constexpr bool LOADS = MODE >= 5;  // modes 5-10
   if (MODE == 6) {
     for (int i = threadIdx.x; i < 8192; i += 512) lds[i] = table[i];
     __syncthreads();
@@ -48,8 +53,15 @@ __global__ __launch_bounds__(512, 1) void probe(double* __restrict__ out, long l
 #pragma unroll
     for (int j = 0; j < 5; ++j) {
       const int off = ((base + j) & 63) * 128 + 2 * lane;
-      if (MODE == 6) o[j] = *(const dbl2*)(lds + off);
-      else o[j] = *(const dbl2*)(table + off);
+      if (MODE == 6) {
+        o[j] = *(const dbl2*)(lds + off);
+      } else if (MODE >= 9) {  // 9 .. 14
+        // 1 KB rows of a 256 MiB table: a tile walks ~37 rows of a 2.4 MB window that moves 1/5 of itself per tile
+        const long long row = ((long long)blockIdx.x * 997 + (long long)t * 480 + (wave & 3) * 7 + k * 4 + j) % 262144;
+        o[j] = *(const dbl2*)(big + row * 128 + 2 * lane);
+      } else {
+        o[j] = *(const dbl2*)(table + off);
+      }
     }
   };
   dbl2 o0[5], o1[5];
@@ -77,7 +89,7 @@ __global__ __launch_bounds__(512, 1) void probe(double* __restrict__ out, long l
       }
     }
     if (store) {
-      if (MODE == 8) {
+      if (MODE == 8 || MODE == 9 || MODE >= 11) {
         // tile t of this wave: chunk (blockIdx.x + gridDim.x * t) mod 6250, realization block (wave & 3) x 128 of
         // 1024 (waves 4-7 the same blocks on the next chunk), 200,000 TOAs per row
         const long long chunk = ((long long)blockIdx.x * 2 + (wave >> 2) + (long long)gridDim.x * 2 * t) % 6250;
@@ -87,7 +99,13 @@ __global__ __launch_bounds__(512, 1) void probe(double* __restrict__ out, long l
           const int i = s >> 2, g = s & 3;
           const int r = r0 + 32 * (i >> 1) + 2 * (lg + 4 * g) + (i & 1);
           const double v = acc[s & 15][s >> 4];
-          *(dbl2*)(out + (long long)r * 200000 + chunk * 32 + 2 * lr) = dbl2{v, v + 1.0};
+          dbl2* dst = (dbl2*)(out + (long long)r * 200000 + chunk * 32 + 2 * lr);
+          const dbl2 val = dbl2{v, v + 1.0};
+          if (MODE == 11) asm volatile("global_store_dwordx4 %0, %1, off nt" ::"v"(dst), "v"(val) : "memory");
+          else if (MODE == 12) asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(dst), "v"(val) : "memory");
+          else if (MODE == 13) asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(dst), "v"(val) : "memory");
+          else if (MODE == 14) asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1 nt" ::"v"(dst), "v"(val) : "memory");
+          else *dst = val;
         }
       } else
 #pragma unroll
@@ -109,7 +127,8 @@ __global__ __launch_bounds__(512, 1) void probe(double* __restrict__ out, long l
 int main() {
   const long long bytes = 2LL << 30;
   const long long n_rows = bytes / 256;  // 256-B rows
-  double *out, *sink, *table;
+  double *out, *sink, *table, *big;
+  if (hipMalloc(&big, 256LL << 20) != hipSuccess || hipMemset(big, 0x3f, 256LL << 20) != hipSuccess) return 1;
   if (hipMalloc(&out, bytes) != hipSuccess || hipMalloc(&sink, 64) != hipSuccess ||
       hipMalloc(&table, 8192 * sizeof(double)) != hipSuccess)
     return 1;
@@ -131,7 +150,7 @@ int main() {
   auto run = [&](auto kernel, const char* name, int compute_waves, int store_waves) {
     for (int rep = 0; rep < 3; ++rep) {
       hipEventRecord(e0, 0);
-      hipLaunchKernelGGL(kernel, dim3(n_cu), dim3(512), 0, 0, out, n_rows, tiles, 1.0 + rep, sink, table);
+      hipLaunchKernelGGL(kernel, dim3(n_cu), dim3(512), 0, 0, out, n_rows, tiles, 1.0 + rep, sink, table, big);
       hipEventRecord(e1, 0);
       hipEventSynchronize(e1);
       float ms = 0;
@@ -151,6 +170,13 @@ int main() {
   run(probe<6>, "mode 6 + operand loads (LDS)", 8, 8);
   run(probe<7>, "mode 7 operand loads, no stores", 8, 0);
   run(probe<8>, "mode 8 mode 5, interpolation addresses", 8, 8);
+  run(probe<9>, "mode 9 mode 8, 256 MiB operand table", 8, 8);
+  run(probe<10>, "mode 10 mode 9 without stores", 8, 0);
+  run(probe<11>, "mode 11 mode 9, nt stores", 8, 8);
+  run(probe<12>, "mode 12 mode 9, sc1 stores", 8, 8);
+  run(probe<13>, "mode 13 mode 9, sc0 sc1 stores", 8, 8);
+  run(probe<14>, "mode 14 mode 9, sc0 sc1 nt stores", 8, 8);
+  run(probe<1>, "mode 1 store only (8 waves)", 0, 8);
   if (hipDeviceSynchronize() != hipSuccess) return 2;
   return 0;
 }
