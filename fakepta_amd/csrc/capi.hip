@@ -730,20 +730,50 @@ int grid_build(fpta_ctx* c, Layout& L) {
     G.why = "gridded path: needs 1.." + std::to_string(kGridMaxSeg) + " grid signals (after coalescing)";
     return FPTA_OK;
   }
-  const int32_t w = G.w;
-  // shape parameter of the exponential-of-semicircle kernel for oversampling sigma (2.31 w at sigma = 2)
-  const double beta = 0.98 * M_PI * w * (1.0 - 0.5 / G.sigma), hw = 0.5 * w;
   const int64_t N = L.n_toa;
   // per (segment, TOA): first interpolation row J (unwrapped) and offset d = u - J, u = theta / h
   std::vector<std::vector<int64_t>> J(n_seg, std::vector<int64_t>(N));
   std::vector<std::vector<double>> D(n_seg, std::vector<double>(N));
-  std::vector<int32_t> nf(n_seg);
+  std::vector<int32_t> nf(n_seg), ws(n_seg);
+  std::vector<double> betas(n_seg);
+  // Per grid signal: the options' (w, sigma) give nf0 = sigma (2 N + 1) grid points; the DFT computes whole blocks
+  // of kGridDftRows rows of the half range, so nf1 = 2 (rows of those blocks - 1) points cost it nothing more. The
+  // larger effective oversampling sigma1 = nf1 / (2 N + 1) reaches the options' a-priori bound with a narrower kernel
+  // w1; the signal takes (nf1, w1) when its interpolation band (w + the cells a 32-TOA chunk spans) is estimated
+  // narrower. C2: red noise + GWB (30 modes) nf 92 -> 126, w 15 -> 13; DM (100 modes) keeps 302 / 15.
+  const double bound_target = G.err_bound;
+  G.err_bound = 0.0;
   for (int32_t s = 0; s < n_seg; ++s) {
     const Seg* sg = L.segs[G.anchor[s]];
     const SegDesc& d = sg->d;
     int32_t n = (int32_t)std::ceil(G.sigma * (2.0 * d.nm + 1.0));
     n += n & 1;
-    nf[s] = std::max(n, 2 * w + 2);
+    int32_t n0 = std::max(n, 2 * G.w + 2), w0 = G.w;
+    // grid cells per TOA per grid point: mean over pulsars of w0 dt / (2 pi), dt the mean TOA spacing
+    double rho = 0.0;
+    for (int32_t p = 0; p < L.P; ++p) {
+      const int64_t a0 = L.h_offs[p], a1 = L.h_offs[p + 1];
+      double tmin = L.h_toas[a0], tmax = L.h_toas[a0];
+      for (int64_t t = a0; t < a1; ++t) {
+        tmin = std::min(tmin, L.h_toas[t]);
+        tmax = std::max(tmax, L.h_toas[t]);
+      }
+      if (a1 - a0 > 1) rho += sg->h_w0[d.kind == 0 ? p : 0] * (tmax - tmin) / (double)(a1 - a0 - 1) / (2.0 * M_PI);
+    }
+    rho /= L.P;
+    const int32_t blocks = (n0 / 2 + kGridDftRows) / kGridDftRows;  // ceil((half + 1) / rows per block)
+    const int32_t n1 = 2 * (blocks * kGridDftRows - 1);
+    const double sig1 = n1 / (2.0 * d.nm + 1.0);
+    int32_t w1 = G.w;
+    while (w1 > 4 && std::exp(-M_PI * (w1 - 1) * std::sqrt(1.0 - 1.0 / sig1)) <= bound_target) --w1;
+    const bool fill = n1 > n0 && 2 * w1 + 2 <= n1 && w1 + kGridTT * n1 * rho < w0 + kGridTT * n0 * rho - 0.25;
+    nf[s] = fill ? n1 : n0;
+    ws[s] = fill ? w1 : w0;
+    const double sig = nf[s] / (2.0 * d.nm + 1.0);
+    // shape parameter of the exponential-of-semicircle kernel for oversampling sigma (2.31 w at sigma = 2)
+    betas[s] = 0.98 * M_PI * ws[s] * (1.0 - 0.5 / sig);
+    G.err_bound = std::max(G.err_bound, std::exp(-M_PI * ws[s] * std::sqrt(1.0 - 1.0 / sig)));
+    const double hw = 0.5 * ws[s];
     const double h = 2.0 * M_PI / nf[s];
     for (int32_t p = 0; p < L.P; ++p) {
       const double w0 = sg->h_w0[d.kind == 0 ? p : 0];
@@ -778,7 +808,7 @@ int grid_build(fpta_ctx* c, Layout& L) {
       while (t < t_lim) {
         bool fits = true;
         for (int32_t s = 0; s < n_seg && fits; ++s)
-          fits = std::max(hi[s], J[s][t]) - std::min(lo[s], J[s][t]) + w + 1 <= kGridRowCap;
+          fits = std::max(hi[s], J[s][t]) - std::min(lo[s], J[s][t]) + ws[s] + 1 <= kGridRowCap;
         if (!fits) break;
         for (int32_t s = 0; s < n_seg; ++s) {
           lo[s] = std::min(lo[s], J[s][t]);
@@ -794,7 +824,7 @@ int grid_build(fpta_ctx* c, Layout& L) {
       }
       for (int32_t s = 0; s < n_seg; ++s) {
         band_lo[s].push_back(lo[s]);
-        band_n[s].push_back((int32_t)(hi[s] - lo[s]) + w);
+        band_n[s].push_back((int32_t)(hi[s] - lo[s]) + ws[s]);
         for (int64_t u = t0; u < t; ++u) J[s][u] -= lo[s];  // row of the TOA's first weight in its band
       }
     }
@@ -940,7 +970,7 @@ int grid_build(fpta_ctx* c, Layout& L) {
     gs->ntab = (d.nm + 7) / 8 * 8;         // whole pairs of 4-mode MFMA k-steps (zero rows)
     gs->rowoff = rowoff[s];
     // q_k = (2 pi / nf) / phi_hat(k), phi_hat(k) = alpha int_{-1}^{1} phi(z) cos(k alpha z) dz, alpha = pi w / nf
-    const double alpha = M_PI * w / nf[s];
+    const double alpha = M_PI * ws[s] / nf[s], beta = betas[s];
     std::vector<double> ec((size_t)gs->ntab * gs->lde, 0.0), es((size_t)gs->ntab * gs->lde, 0.0);
     for (int32_t m = 0; m < d.nm; ++m) {
       const int64_t k = m + 1;
@@ -965,7 +995,7 @@ int grid_build(fpta_ctx* c, Layout& L) {
       return rc;
     HIPCHK(c,
            launch_grid_weights(c->stream, d, N, L.nu.as<double>(), d_chunk_of.as<int32_t>(), d_tt_of.as<int32_t>(),
-                               d_row.as<int32_t>(), d_d.as<double>(), w, beta, vmax, G.wd.as<double>()),
+                               d_row.as<int32_t>(), d_d.as<double>(), ws[s], beta, vmax, G.wd.as<double>()),
            "k_grid_weights launch");
     HIPCHK(c, hipStreamSynchronize(c->stream), "grid weights sync");  // d_row / d_d are reused
     G.fma_dft += (double)L.P * (gs->half + 1) * 2.0 * d.nm;
