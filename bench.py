@@ -369,6 +369,17 @@ def main():
                                 "avg_launch_ms": t_int * 1e3, "achieved": out_bytes / t_int / 1e9,
                                 "frac": out_bytes / t_int / 1e9 / HBM_PEAK_GBS, "dft_avg_launch_ms": t_dft * 1e3,
                                 "dft_TFLOPs": 2.0 * gi["fma_dft"] * (-(-R // 128) * 128) / t_dft / 1e12}
+    pcie = None
+    if args.config == "c2" and args.exact_launches > 0:
+        # PCIe-inclusive rate (never `value`): every step's block copied to a host numpy array
+        sim.synth(R, seed=args.seed, real0=0, to_host=True)
+        t0 = time.perf_counter()
+        for i in range(2):
+            sim.synth(R, seed=args.seed, real0=(i + 1) * R, to_host=True)
+        dt_h = (time.perf_counter() - t0) / 2
+        pcie = {"note": "block copied to pageable host memory every step (not the metric)",
+                "ms_per_step": dt_h * 1e3, "samples_per_s": info["n_toa"] * R / dt_h,
+                "host_GBps": 8.0 * info["n_toa"] * R / dt_h / 1e9}
     roofline_exact = None
     if args.config == "c2" and args.exact_launches > 0:
         roofline_exact = exact_roofline(ctx, _capi, sim, args.seed, R, args.exact_launches)
@@ -393,6 +404,7 @@ def main():
             "path_reason": gi["path_reason"] or None,
             "roofline": roofline,
             "roofline_exact": roofline_exact,
+            "pcie_inclusive": pcie,
             "kernels_ms_per_step": {k: (v[1] / max(v[0], 1)) * (v[0] / max(args.steps, 1)) for k, v in kstats.items()},
             "checksum": float(np.sum(sums[:, 1])),
             "n_checksums": int(len(sums)),

@@ -990,8 +990,10 @@ hipError_t launch_grid_interp_mfma(hipStream_t st, const SynthArgs& a, const Gri
 // Grid: every pulsar tile of a column block runs on one XCD (block b: XCD b % 8), so the block's Z columns
 // (P x 256 doubles) are read from HBM once and served to the other pulsar tiles from that XCD's L2. A lower-
 // triangular factor (Cholesky of a positive-definite ORF) stops the q loop at the tile's last pulsar.
-template <int NU, int NB>
-__global__ __launch_bounds__(256, 2) void k_mix_mfma(const double* __restrict__ LT, int32_t lt_ld,
+// OCC waves per SIMD: the small-array instance (<2, 1, 3>, 168 VGPRs) fits beside the warp-specialised interpolation
+// of the previous block (2 x 168), so pipelined blocks' mixing co-runs with it instead of waiting for it.
+template <int NU, int NB, int OCC>
+__global__ __launch_bounds__(256, OCC) void k_mix_mfma(const double* __restrict__ LT, int32_t lt_ld,
                                                      const double* __restrict__ amp, int32_t P, int64_t M,
                                                      int32_t R_pad, int32_t lower, int32_t n_pt, int32_t n_cb,
                                                      const double* __restrict__ zbuf, double* __restrict__ coef,
@@ -1065,12 +1067,11 @@ __global__ __launch_bounds__(256, 2) void k_mix_mfma(const double* __restrict__ 
       }
 }
 
-constexpr int kMixNU = 2, kMixNB = 2;  // k_mix_mfma wave tile: 64 pulsars x 64 columns
-
-hipError_t launch_mix_mfma(hipStream_t st, const SegDesc& sd, int32_t P, int32_t R_pad, const double* zbuf,
-                           double* coef, int32_t K, double* x_out) {
+template <int NU, int NB, int OCC>
+hipError_t launch_mix_mfma_t(hipStream_t st, const SegDesc& sd, int32_t P, int32_t R_pad, const double* zbuf,
+                             double* coef, int32_t K, double* x_out) {
   const int64_t M = (int64_t)2 * sd.nm * R_pad;  // a multiple of 256: R_pad is a multiple of 128
-  constexpr int kCols = 4 * 32 * kMixNB, kRows = 32 * kMixNU;
+  constexpr int kCols = 4 * 32 * NB, kRows = 32 * NU;
   if (P <= 0 || !sd.LT || M % kCols != 0) return hipErrorInvalidValue;
   const int64_t n_cb = M / kCols;
   const int32_t n_pt = (P + kRows - 1) / kRows;
@@ -1078,9 +1079,19 @@ hipError_t launch_mix_mfma(hipStream_t st, const SegDesc& sd, int32_t P, int32_t
   if (sd.lt_ld < n_pt * kRows || sd.lt_rows < (P + 7) / 8 * 8 + 4) return hipErrorInvalidValue;
   const int64_t blocks = (n_cb + 7) / 8 * 8 * n_pt;
   if (blocks > 0x7FFFFFFF || n_cb > 0x7FFFFFFF) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((k_mix_mfma<kMixNU, kMixNB>), dim3((unsigned)blocks), dim3(256), 0, st, sd.LT, sd.lt_ld, sd.amp,
-                     P, M, R_pad, sd.l_lower, n_pt, (int32_t)n_cb, zbuf, coef, K, sd.col0, x_out);
+  hipLaunchKernelGGL((k_mix_mfma<NU, NB, OCC>), dim3((unsigned)blocks), dim3(256), 0, st, sd.LT, sd.lt_ld, sd.amp, P,
+                     M, R_pad, sd.l_lower, n_pt, (int32_t)n_cb, zbuf, coef, K, sd.col0, x_out);
   return hipGetLastError();
+}
+
+// Wave tile 64 pulsars x 64 columns at 2 waves per SIMD for large arrays (C4: the mix is a kernel of its own);
+// 64 x 32 at 3 waves per SIMD for small ones, whose mixing co-runs with the previous block's interpolation.
+constexpr int kMixLargeP = 256;
+
+hipError_t launch_mix_mfma(hipStream_t st, const SegDesc& sd, int32_t P, int32_t R_pad, const double* zbuf,
+                           double* coef, int32_t K, double* x_out) {
+  return P >= kMixLargeP ? launch_mix_mfma_t<2, 2, 2>(st, sd, P, R_pad, zbuf, coef, K, x_out)
+                         : launch_mix_mfma_t<2, 1, 3>(st, sd, P, R_pad, zbuf, coef, K, x_out);
 }
 
 // ----------------------------------------------------------------------------- partial checksums
