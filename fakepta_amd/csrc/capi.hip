@@ -966,7 +966,7 @@ int grid_build(fpta_ctx* c, Layout& L) {
     G.segs.push_back(gs);
     gs->nf = nf[s];
     gs->half = nf[s] / 2;
-    gs->lde = (gs->half + 32) / 32 * 32;  // row tiles of k_grid_dft_mfma (32) and k_grid_dft (kGridMI)
+    gs->lde = (gs->half + kGridDftRows) / kGridDftRows * kGridDftRows;  // row blocks of k_grid_dft_mfma and k_grid_dft
     gs->ntab = (d.nm + 7) / 8 * 8;         // whole pairs of 4-mode MFMA k-steps (zero rows)
     gs->rowoff = rowoff[s];
     // q_k = (2 pi / nf) / phi_hat(k), phi_hat(k) = alpha int_{-1}^{1} phi(z) cos(k alpha z) dz, alpha = pi w / nf

@@ -82,7 +82,12 @@ static_assert(sizeof(kSeededVariants) == sizeof(kValuVariants), "one variant ind
 constexpr int kGridVMax = 256;  // band rows per chunk, all signals (k_grid_interp_mfma keeps them in 4 VGPRs)
 constexpr int kGridTT = 32;  // TOAs per interpolation chunk (k_grid_interp_mfma: even / odd TOAs = two MFMA B-tiles)
 constexpr int kGridMI = 8;   // grid rows per wave in k_grid_dft
-constexpr int kGridDftRows = 32;  // grid rows of the half range per k_grid_dft_mfma row block (16 x its MJ)
+#ifndef FPTA_DFT_MJ
+#define FPTA_DFT_MJ 2
+#endif
+constexpr int kDftMJ = FPTA_DFT_MJ;      // k_grid_dft_mfma wave tile: 16 MJ grid rows x 16 kDftMR realizations
+constexpr int kDftMR = 8 / FPTA_DFT_MJ;  // (the accumulators stay at 2 MJ MR = 16 tiles)
+constexpr int kGridDftRows = 16 * kDftMJ;  // grid rows of the half range per k_grid_dft_mfma row block
 struct GridSegDev {
   const double* ecos;  // [nm][lde] q_k cos(2 pi k j / nf), k = m + 1 (zero-padded columns)
   const double* esin;  // [nm][lde] q_k sin(2 pi k j / nf)

@@ -931,7 +931,6 @@ hipError_t launch_grid_interp_ws(hipStream_t st, const SynthArgs& a, const GridB
   return hipGetLastError();
 }
 
-constexpr int kDftMJ = 2, kDftMR = 4;  // k_grid_dft_mfma wave tile: 32 grid rows x 64 realizations
 static_assert(16 * kDftMJ == kGridDftRows, "grid_build sizes grids to whole DFT row blocks");
 
 hipError_t launch_grid_dft_mfma(hipStream_t st, GridSegs gsegs, int32_t P, const double* coef, int32_t K,
