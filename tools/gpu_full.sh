@@ -21,7 +21,13 @@ done
 python tools/collect_traffic.py ${o}_traffic ${o}_grid_traffic.json 320 200000 1024 k_grid_interp_ws band32c || exit 1
 timeout -k 10 300 python -u bench.py --traffic ${o}_grid_traffic.json > ${o}_bench.log 2>&1 || { tail -20 ${o}_bench.log; exit 1; }
 cat ${o}_bench.log
-timeout -k 10 300 python -u bench.py --config c3 --cpu-sample 0 > ${o}_bench_c3.log 2>&1 || { tail -20 ${o}_bench_c3.log; exit 1; }
+i=0
+for p in FETCH_SIZE WRITE_SIZE; do
+  timeout -s KILL 200 rocprofv3 --pmc $p --output-format csv -d ${o}_traffic_c3/pass$i -o run -- python bench.py --config c3 --steps 1 --warmup 1 --cpu-sample 0 > ${o}_traffic_c3_$p.log 2>&1 || { tail -20 ${o}_traffic_c3_$p.log; exit 1; }
+  i=$((i+1))
+done
+python tools/collect_traffic.py ${o}_traffic_c3 ${o}_grid_traffic_c3.json 60 200000 4096 k_grid_interp_mfma band32c || exit 1
+timeout -k 10 300 python -u bench.py --config c3 --cpu-sample 0 --traffic ${o}_grid_traffic_c3.json > ${o}_bench_c3.log 2>&1 || { tail -20 ${o}_bench_c3.log; exit 1; }
 cat ${o}_bench_c3.log
 timeout -k 10 300 python -u bench.py --path 3 --cpu-sample 0 > ${o}_bench_exact.log 2>&1 || { tail -20 ${o}_bench_exact.log; exit 1; }
 timeout -k 10 300 python -u tools/bench_configs.py c1 c3 c4 c5 > ${o}_configs.jsonl 2>&1 || { tail -20 ${o}_configs.jsonl; exit 1; }
