@@ -525,14 +525,30 @@ int run_coefficients(fpta_ctx* c, Layout& L, uint64_t seed, int64_t real0, int32
   merge = merge && G.built && G.ok && G.merges;
   // the download of per-signal coefficients must precede every merge: then all events wait for the end
   const bool defer = merge && coef_host;
+  // A common (kind-1) member of a coalesced grid signal adds into the anchor's columns inside its own k_mix_mfma
+  // (no k_coef_merge pass over it) when the anchor is drawn before it and every member before it (index order,
+  // anchor excluded) does the same: the sums then run in k_coef_merge's order, bit for bit. Not when the
+  // per-signal coefficients are downloaded (they are taken before any merge) or mixed draws are returned.
+  const bool mfma_mix = P >= kMixTiledMinP && R_pad % 128 == 0 && c->mix_mfma;
+  std::vector<int32_t> fuse_into(L.segs.size(), -1);
+  if (merge && !defer && mfma_mix && !x_out)
+    for (size_t g = 0; g < G.members.size(); ++g) {
+      bool prefix = true;
+      for (int32_t i : G.members[g]) {
+        if (i == G.anchor[g]) continue;
+        prefix = prefix && L.segs[i]->d.kind == 1 && G.anchor[g] < i;
+        if (prefix) fuse_into[i] = L.segs[G.anchor[g]]->d.col0;
+      }
+    }
   auto merge_group = [&](size_t g) -> int {
     CoefMerge m{};
     m.dst = L.segs[G.anchor[g]]->d.col0;
     for (int32_t i : G.members[g])
-      if (i != G.anchor[g]) {
+      if (i != G.anchor[g] && fuse_into[i] < 0) {
         m.src[m.n] = L.segs[i]->d.col0;
         m.ncol[m.n++] = 2 * L.segs[i]->d.nm;
       }
+    if (m.n == 0) return FPTA_OK;  // every member was added inside its mix
     KTimer kt(c, FPTA_K_GEN, st);
     HIPCHK(c, launch_coef_merge(st, m, P, L.K, R_pad, c->coef.as<double>()), "k_coef_merge launch");
     return FPTA_OK;
@@ -548,8 +564,9 @@ int run_coefficients(fpta_ctx* c, Layout& L, uint64_t seed, int64_t real0, int32
     }
     if (d.kind == 1) {
       KTimer kt(c, FPTA_K_MIX, st);
-      if (P >= kMixTiledMinP && R_pad % 128 == 0 && c->mix_mfma)
-        HIPCHK(c, launch_mix_mfma(st, d, P, R_pad, c->zbuf.as<double>(), c->coef.as<double>(), L.K, x_out),
+      if (mfma_mix)
+        HIPCHK(c,
+               launch_mix_mfma(st, d, P, R_pad, c->zbuf.as<double>(), c->coef.as<double>(), L.K, x_out, fuse_into[i]),
                "k_mix_mfma launch");
       else if (P >= kMixTiledMinP && R_pad % 128 == 0)
         HIPCHK(c, launch_mix_tiled(st, d, P, R_pad, c->zbuf.as<double>(), c->coef.as<double>(), L.K, x_out),

@@ -160,9 +160,10 @@ hipError_t launch_gen(hipStream_t st, const SegDesc& sd, int32_t seg_id, int32_t
                       int32_t zin_nseg, int32_t zin_nm, double* coef, int32_t K, double* zbuf);
 hipError_t launch_mix(hipStream_t st, const SegDesc& sd, int32_t P, int32_t R_pad, const double* zbuf,
                       double* coef, int32_t K, double* x_out);
-// the same product on v_mfma_f64_16x16x4_f64 (grid_mfma.hip), the large-array path
+// the same product on v_mfma_f64_16x16x4_f64 (grid_mfma.hip), the large-array path. acc_col0 >= 0: add the mixed
+// coefficients into columns acc_col0 .. (a coalesced grid signal's anchor) instead of writing the signal's own
 hipError_t launch_mix_mfma(hipStream_t st, const SegDesc& sd, int32_t P, int32_t R_pad, const double* zbuf,
-                           double* coef, int32_t K, double* x_out);
+                           double* coef, int32_t K, double* x_out, int32_t acc_col0 = -1);
 hipError_t launch_mix_tiled(hipStream_t st, const SegDesc& sd, int32_t P, int32_t R_pad, const double* zbuf,
                             double* coef, int32_t K, double* x_out);
 hipError_t launch_epoch_normals(hipStream_t st, int64_t n_blocks, int32_t n_real, int64_t real0, uint32_t k0,

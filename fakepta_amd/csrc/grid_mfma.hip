@@ -989,6 +989,14 @@ hipError_t launch_grid_interp_mfma(hipStream_t st, const SynthArgs& a, const Gri
 // Grid: every pulsar tile of a column block runs on one XCD (block b: XCD b % 8), so the block's Z columns
 // (P x 256 doubles) are read from HBM once and served to the other pulsar tiles from that XCD's L2. A lower-
 // triangular factor (Cholesky of a positive-definite ORF) stops the q loop at the tile's last pulsar.
+// o + (a v0, a v1) with the products rounded before the add (-ffp-contract=fast ignores contract pragmas), as
+// k_coef_merge adds the stored coefficients a v: a block is bit-identical whichever of the two sums it
+__device__ __forceinline__ dbl2 add_rounded_product(dbl2 o, double a, double v0, double v1) {
+  double t0 = a * v0, t1 = a * v1;
+  asm volatile("" : "+v"(t0), "+v"(t1));  // an opaque value: the add cannot fuse with the multiply
+  return dbl2{o.x + t0, o.y + t1};
+}
+
 // OCC waves per SIMD: the small-array instance (<2, 1, 3>, 168 VGPRs) fits beside the warp-specialised interpolation
 // of the previous block (2 x 168), so pipelined blocks' mixing co-runs with it instead of waiting for it.
 template <int NU, int NB, int OCC>
@@ -996,7 +1004,8 @@ __global__ __launch_bounds__(256, OCC) void k_mix_mfma(const double* __restrict_
                                                      const double* __restrict__ amp, int32_t P, int64_t M,
                                                      int32_t R_pad, int32_t lower, int32_t n_pt, int32_t n_cb,
                                                      const double* __restrict__ zbuf, double* __restrict__ coef,
-                                                     int32_t K, int32_t col0, double* __restrict__ x_out) {
+                                                     int32_t K, int32_t col0, double* __restrict__ x_out,
+                                                     int32_t add_into) {
   const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
   const int cb = (slot / n_pt) * 8 + xcd;
   const int pt = slot - (slot / n_pt) * n_pt;
@@ -1060,7 +1069,13 @@ __global__ __launch_bounds__(256, OCC) void k_mix_mfma(const double* __restrict_
           const int r = (int)(m - (int64_t)jc * R_pad);
           const double a = amp[jc >> 1];
           const double v0 = acc[2 * u + e][2 * b][g], v1 = acc[2 * u + e][2 * b + 1][g];
-          *(dbl2*)(coef + ((int64_t)p * K + col0 + jc) * R_pad + r) = dbl2{a * v0, a * v1};
+          double* dst = coef + ((int64_t)p * K + col0 + jc) * R_pad + r;
+          if (add_into) {  // into a coalesced grid signal's anchor columns
+            const dbl2 o = *(const dbl2*)dst;
+            *(dbl2*)dst = add_rounded_product(o, a, v0, v1);
+          } else {
+            *(dbl2*)dst = dbl2{a * v0, a * v1};
+          }
           if (x_out) *(dbl2*)(x_out + (int64_t)p * M + m) = dbl2{v0, v1};
         }
       }
@@ -1068,7 +1083,7 @@ __global__ __launch_bounds__(256, OCC) void k_mix_mfma(const double* __restrict_
 
 template <int NU, int NB, int OCC>
 hipError_t launch_mix_mfma_t(hipStream_t st, const SegDesc& sd, int32_t P, int32_t R_pad, const double* zbuf,
-                             double* coef, int32_t K, double* x_out) {
+                             double* coef, int32_t K, double* x_out, int32_t acc_col0) {
   const int64_t M = (int64_t)2 * sd.nm * R_pad;  // a multiple of 256: R_pad is a multiple of 128
   constexpr int kCols = 4 * 32 * NB, kRows = 32 * NU;
   if (P <= 0 || !sd.LT || M % kCols != 0) return hipErrorInvalidValue;
@@ -1079,7 +1094,8 @@ hipError_t launch_mix_mfma_t(hipStream_t st, const SegDesc& sd, int32_t P, int32
   const int64_t blocks = (n_cb + 7) / 8 * 8 * n_pt;
   if (blocks > 0x7FFFFFFF || n_cb > 0x7FFFFFFF) return hipErrorInvalidValue;
   hipLaunchKernelGGL((k_mix_mfma<NU, NB, OCC>), dim3((unsigned)blocks), dim3(256), 0, st, sd.LT, sd.lt_ld, sd.amp, P,
-                     M, R_pad, sd.l_lower, n_pt, (int32_t)n_cb, zbuf, coef, K, sd.col0, x_out);
+                     M, R_pad, sd.l_lower, n_pt, (int32_t)n_cb, zbuf, coef, K, acc_col0 >= 0 ? acc_col0 : sd.col0,
+                     x_out, acc_col0 >= 0 ? 1 : 0);
   return hipGetLastError();
 }
 
@@ -1088,9 +1104,10 @@ hipError_t launch_mix_mfma_t(hipStream_t st, const SegDesc& sd, int32_t P, int32
 constexpr int kMixLargeP = 256;
 
 hipError_t launch_mix_mfma(hipStream_t st, const SegDesc& sd, int32_t P, int32_t R_pad, const double* zbuf,
-                           double* coef, int32_t K, double* x_out) {
-  return P >= kMixLargeP ? launch_mix_mfma_t<2, 2, 2>(st, sd, P, R_pad, zbuf, coef, K, x_out)
-                         : launch_mix_mfma_t<2, 1, 3>(st, sd, P, R_pad, zbuf, coef, K, x_out);
+                           double* coef, int32_t K, double* x_out, int32_t acc_col0) {
+  if (acc_col0 >= 0 && (x_out || acc_col0 + 2 * sd.nm > K)) return hipErrorInvalidValue;
+  return P >= kMixLargeP ? launch_mix_mfma_t<2, 2, 2>(st, sd, P, R_pad, zbuf, coef, K, x_out, acc_col0)
+                         : launch_mix_mfma_t<2, 1, 3>(st, sd, P, R_pad, zbuf, coef, K, x_out, acc_col0);
 }
 
 // ----------------------------------------------------------------------------- partial checksums
