@@ -209,6 +209,15 @@ struct fpta_ctx {
   bool gfree_set[2] = {false, false};
   int gbuf = 0;
   bool coef_last_side = false;
+  // FPTA_OPT_SIDE_SPLIT: grid signal split_g (per-pulsar members only) of the current pipelined block runs its draws
+  // and DFT on side2. At each block start side waits for side2's previous work (ev_s2done) and side2 for side's
+  // (ev_s2begin), so a layout change never lets one stream write columns the other still reads; ev_gready2: side2's
+  // DFT is done.
+  int side_split = 1;
+  hipStream_t side2 = nullptr;
+  hipEvent_t ev_s2begin = nullptr, ev_s2done = nullptr, ev_gready2 = nullptr;
+  bool s2done_set = false;
+  int32_t split_g = -1;
   bool coef_copy_pending = false;  // the block's coefficients are still to be downloaded after the synthesis
   DevBuf part, part_tmp; // partial checksums [n_chunks][R_pad][2] of the last block, reduction scratch
   bool part_ready = false;  // part holds the partials of the current block (c->out, out_R)
@@ -497,6 +506,7 @@ int run_coefficients(fpta_ctx* c, Layout& L, uint64_t seed, int64_t real0, int32
   if (!use_side) c->coef_free_set = false;  // coef is written on the ctx stream from here on
   const size_t coef_bytes = sizeof(double) * (size_t)P * std::max(L.K, 1) * R_pad;
   if (c->side && c->coef.cap < coef_bytes) HIPCHK(c, hipStreamSynchronize(c->side), "side sync");  // before a regrow
+  if (c->side2 && c->coef.cap < coef_bytes) HIPCHK(c, hipStreamSynchronize(c->side2), "side sync");
   if (use_side) {
     if (!c->side) HIPCHK(c, hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking), "side stream create");
     if (!c->ev_begin) HIPCHK(c, hipEventCreateWithFlags(&c->ev_begin, hipEventDisableTiming), "event create");
@@ -513,6 +523,9 @@ int run_coefficients(fpta_ctx* c, Layout& L, uint64_t seed, int64_t real0, int32
       HIPCHK(c, hipStreamWaitEvent(c->side, c->coef_free_set ? c->ev_coef_free : c->ev_begin, 0), "side wait");
     }
     c->coef_free_set = false;
+    // the previous split block's second side stream (its draws and DFT) comes first as well
+    if (c->s2done_set) HIPCHK(c, hipStreamWaitEvent(c->side, c->ev_gready2, 0), "side wait");
+    c->s2done_set = false;
     st = c->side;
   }
   HIPCHK(c, c->coef.ensure(coef_bytes), "coef alloc");
@@ -540,6 +553,33 @@ int run_coefficients(fpta_ctx* c, Layout& L, uint64_t seed, int64_t real0, int32
         if (prefix) fuse_into[i] = L.segs[G.anchor[g]]->d.col0;
       }
     }
+  // FPTA_OPT_SIDE_SPLIT: in a pipelined block, the grid signal with the largest DFT (half range x modes) whose
+  // members are all per-pulsar signals (no zbuf, no mixing) is drawn, merged and transformed on side2, beside the
+  // other signals' chain on side. Both streams start after everything before the block on side.
+  c->split_g = -1;
+  std::vector<int32_t> group_of(L.segs.size(), -1);
+  for (size_t g = 0; g < G.members.size(); ++g)
+    for (int32_t i : G.members[g]) group_of[i] = (int32_t)g;
+  if (pipe && use_side && c->side_split && G.built && G.ok && G.members.size() > 1 && !zin && !x_out && !coef_host) {
+    int64_t best = -1;
+    for (size_t g = 0; g < G.members.size(); ++g) {
+      bool per_pulsar = true;
+      for (int32_t i : G.members[g]) per_pulsar = per_pulsar && L.segs[i]->d.kind == 0;
+      const int64_t cost = (int64_t)G.segs[g]->half * L.segs[G.anchor[g]]->d.nm;
+      if (per_pulsar && cost > best) {
+        best = cost;
+        c->split_g = (int32_t)g;
+      }
+    }
+  }
+  if (c->split_g >= 0) {
+    if (!c->side2) HIPCHK(c, hipStreamCreateWithFlags(&c->side2, hipStreamNonBlocking), "side stream create");
+    for (hipEvent_t* e : {&c->ev_s2begin, &c->ev_gready2})
+      if (!*e) HIPCHK(c, hipEventCreateWithFlags(e, hipEventDisableTiming), "event create");
+    HIPCHK(c, hipEventRecord(c->ev_s2begin, c->side), "event record");
+    HIPCHK(c, hipStreamWaitEvent(c->side2, c->ev_s2begin, 0), "side wait");
+  }
+  auto stream_of = [&](int32_t g) { return g >= 0 && g == c->split_g ? c->side2 : st; };
   auto merge_group = [&](size_t g) -> int {
     CoefMerge m{};
     m.dst = L.segs[G.anchor[g]]->d.col0;
@@ -549,16 +589,18 @@ int run_coefficients(fpta_ctx* c, Layout& L, uint64_t seed, int64_t real0, int32
         m.ncol[m.n++] = 2 * L.segs[i]->d.nm;
       }
     if (m.n == 0) return FPTA_OK;  // every member was added inside its mix
-    KTimer kt(c, FPTA_K_GEN, st);
-    HIPCHK(c, launch_coef_merge(st, m, P, L.K, R_pad, c->coef.as<double>()), "k_coef_merge launch");
+    hipStream_t sg = stream_of((int32_t)g);
+    KTimer kt(c, FPTA_K_GEN, sg);
+    HIPCHK(c, launch_coef_merge(sg, m, P, L.K, R_pad, c->coef.as<double>()), "k_coef_merge launch");
     return FPTA_OK;
   };
   for (size_t i = 0; i < L.segs.size(); ++i) {
     const SegDesc& d = L.segs[i]->d;
+    hipStream_t si = stream_of(group_of[i]);  // side2 only for members of split_g (kind 0: no mixing below)
     {
-      KTimer kt(c, FPTA_K_GEN, st);
+      KTimer kt(c, FPTA_K_GEN, si);
       HIPCHK(c,
-             launch_gen(st, d, (int32_t)i, P, R, R_pad, real0, k0, k1, zin, (int32_t)L.segs.size(), zin_nm,
+             launch_gen(si, d, (int32_t)i, P, R, R_pad, real0, k0, k1, zin, (int32_t)L.segs.size(), zin_nm,
                         c->coef.as<double>(), L.K, c->zbuf.as<double>()),
              "k_gen launch");
     }
@@ -1033,6 +1075,7 @@ int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad, bool pipe = fa
   const size_t gbytes = sizeof(double) * (size_t)G.grid_rows * R_pad;
   if (G.g_rpad != R_pad || (pipe && G.g2.cap < gbytes)) {
     if (c->side) HIPCHK(c, hipStreamSynchronize(c->side), "side sync");  // no reader of a buffer being regrown
+    if (c->side2) HIPCHK(c, hipStreamSynchronize(c->side2), "side sync");
     HIPCHK(c, hipStreamSynchronize(c->stream), "grid regrow sync");
     HIPCHK(c, G.g.ensure(gbytes), "grid alloc");
     if (pipe) HIPCHK(c, G.g2.ensure(gbytes), "grid alloc");
@@ -1063,7 +1106,30 @@ int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad, bool pipe = fa
       g.ntab = gs->ntab;
     }
     const bool early_free = c->coef_side && !c->coef_copy_pending;
-    if (pipe) {
+    const int32_t split = pipe && c->split_g < gsegs.n ? c->split_g : -1;
+    c->split_g = -1;
+    if (pipe && split >= 0) {
+      // the split signal's DFT on side2 (after its draws there), the others' on side
+      GridSegs one{}, rest{};
+      for (int32_t s = 0; s < gsegs.n; ++s) {
+        GridSegs& dst = s == split ? one : rest;
+        dst.s[dst.n++] = gsegs.s[s];
+      }
+      {
+        if (c->gfree_set[gi]) HIPCHK(c, hipStreamWaitEvent(c->side2, c->ev_gfree[gi], 0), "grid buffer wait");
+        KTimer kt2(c, FPTA_K_GRID, c->side2);
+        HIPCHK(c,
+               (c->grid_mfma & 1) ? launch_grid_dft_mfma(c->side2, one, L.P, a.coef, a.K, R_pad)
+                                  : launch_grid_dft(c->side2, one, L.P, a.coef, a.K, R_pad),
+               "k_grid_dft launch");
+      }
+      HIPCHK(c, hipEventRecord(c->ev_gready2, c->side2), "event record");
+      c->s2done_set = true;
+      HIPCHK(c,
+             (c->grid_mfma & 1) ? launch_grid_dft_mfma(c->side, rest, L.P, a.coef, a.K, R_pad)
+                                : launch_grid_dft(c->side, rest, L.P, a.coef, a.K, R_pad),
+             "k_grid_dft launch");
+    } else if (pipe) {
       HIPCHK(c,
              (c->grid_mfma & 1) ? launch_grid_dft_mfma(c->side, gsegs, L.P, a.coef, a.K, R_pad)
                                 : launch_grid_dft(c->side, gsegs, L.P, a.coef, a.K, R_pad),
@@ -1107,6 +1173,7 @@ int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad, bool pipe = fa
     a.part = c->part.as<double>();
   }
   if (pipe) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_gready, 0), "grid ready wait");
+  if (pipe && c->s2done_set) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_gready2, 0), "grid ready wait");
   KTimer kt(c, FPTA_K_SYNTH);
   GridBand band{G.chunks.as<int4>(), G.rows.as<int32_t>(), G.wd.as<double>(), gbase, G.n_chunks, G.vmax,
                 G.grid_rows};
@@ -1453,6 +1520,12 @@ int fpta_destroy(fpta_ctx* c) {
     (void)hipStreamSynchronize(c->side);
     (void)hipStreamDestroy(c->side);
   }
+  if (c->side2) {
+    (void)hipStreamSynchronize(c->side2);
+    (void)hipStreamDestroy(c->side2);
+  }
+  for (hipEvent_t e : {c->ev_s2begin, c->ev_s2done, c->ev_gready2})
+    if (e) (void)hipEventDestroy(e);
   if (c->ev_begin) (void)hipEventDestroy(c->ev_begin);
   if (c->ev_coef_free) (void)hipEventDestroy(c->ev_coef_free);
   for (hipEvent_t e : {c->ev_gready, c->ev_gfree[0], c->ev_gfree[1]})
@@ -1506,6 +1579,9 @@ int fpta_set_option(fpta_ctx* c, int32_t key, int64_t value) {
     case FPTA_OPT_INTERP_WS:
       c->interp_ws = value ? 1 : 0;
       return FPTA_OK;
+    case FPTA_OPT_SIDE_SPLIT:
+      c->side_split = value ? 1 : 0;
+      return FPTA_OK;
     case FPTA_OPT_VALU_VARIANT:
       if (value < 0 || value >= kNumValuVariants) return fail(c, FPTA_EINVAL, "unknown VALU variant");
       c->valu_variant = (int)value;
@@ -1542,6 +1618,7 @@ int fpta_get_option(fpta_ctx* c, int32_t key, int64_t* value) {
     case FPTA_OPT_INTERP_LDS: *value = c->interp_lds; return FPTA_OK;
     case FPTA_OPT_GRID_COALESCE: *value = c->grid_coalesce; return FPTA_OK;
     case FPTA_OPT_INTERP_WS: *value = c->interp_ws; return FPTA_OK;
+    case FPTA_OPT_SIDE_SPLIT: *value = c->side_split; return FPTA_OK;
   }
   return fail(c, FPTA_EINVAL, "get_option: unknown key");
 }

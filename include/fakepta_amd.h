@@ -280,6 +280,10 @@ int fpta_multi_synth(fpta_multi* m, uint64_t seed, int64_t real0, int64_t n_real
                                      so stores never delay an operand load) for blocks without fused white noise
                                      or fused partial checksums;
                                      0 the register-pipelined k_grid_interp_mfma. Results are identical. */
+#define FPTA_OPT_SIDE_SPLIT 16    /* pipelined gridded blocks (FPTA_OPT_OVERLAP): 1 (default) the grid signal with
+                                     the largest DFT, when it has no common (ORF-mixed) member, is drawn and
+                                     transformed on a second side stream, beside the other signals' draws, mixing
+                                     and DFT; 0 one side stream for all. Results are identical. */
 int fpta_set_option(fpta_ctx* ctx, int32_t key, int64_t value);
 /* Current value of option `key` (same keys as fpta_set_option). */
 int fpta_get_option(fpta_ctx* ctx, int32_t key, int64_t* value);
