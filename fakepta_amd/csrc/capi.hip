@@ -573,7 +573,11 @@ int run_coefficients(fpta_ctx* c, Layout& L, uint64_t seed, int64_t real0, int32
     }
   }
   if (c->split_g >= 0) {
-    if (!c->side2) HIPCHK(c, hipStreamCreateWithFlags(&c->side2, hipStreamNonBlocking), "side stream create");
+    if (!c->side2) {  // at the highest priority: its chain (the largest DFT) is the longer one (profiles/r02n_*)
+      int lo = 0, hi = 0;
+      HIPCHK(c, hipDeviceGetStreamPriorityRange(&lo, &hi), "stream priority range");
+      HIPCHK(c, hipStreamCreateWithPriority(&c->side2, hipStreamNonBlocking, hi), "side stream create");
+    }
     for (hipEvent_t* e : {&c->ev_s2begin, &c->ev_gready2})
       if (!*e) HIPCHK(c, hipEventCreateWithFlags(e, hipEventDisableTiming), "event create");
     HIPCHK(c, hipEventRecord(c->ev_s2begin, c->side), "event record");
