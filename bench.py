@@ -186,7 +186,8 @@ def cpu_baseline(sim, psrs, n_sample, seed):
 def pmc_traffic(kernel, info, R, path_arg, layout=None):
     """HBM bytes per launch from the matching profiles/*traffic.json PMC record (same kernel, shape and, for the
     gridded path, plan layout)."""
-    candidates = ([path_arg] if path_arg else sorted(glob.glob(os.path.join(ROOT, "profiles", "*traffic.json"))))
+    # newest round first (profiles/rNN<letter>_*: a later tag sorts after an earlier one)
+    candidates = ([path_arg] if path_arg else sorted(glob.glob(os.path.join(ROOT, "profiles", "*traffic.json")), reverse=True))
     for cand in candidates:
         try:
             with open(cand) as fh:
