@@ -400,6 +400,31 @@ def test_pipelined_batches_are_bitwise_identical(ctx, capi, shipped, fuse, layou
         ctx.set_options(shipped)
 
 
+def test_pipelined_layout_switches_are_bitwise_identical(ctx, capi, shipped):
+    """Pipelined blocks across layout changes on one context: a 70-pulsar layout (DM on the second side stream, the
+    GWB mix adding into red noise), a 12-pulsar one with other coefficient columns, then a 70-pulsar one again. Each
+    run of blocks returns the single-stream checksums bit for bit: the two side streams join at every block start,
+    so no stream writes coefficient columns or a grid buffer the other, or an earlier layout's block, still reads."""
+    def run(ov, split):
+        ctx.set_option(capi.OPT_OVERLAP, ov)
+        ctx.set_option(capi.OPT_SIDE_SPLIT, split)
+        out = []
+        for v, P in enumerate((70, 12, 70)):
+            ctx.batch_clear()
+            _shared_span_layout(ctx, np.random.default_rng(71 + v), P=P, n=(120, 300), nu_const=False)
+            ctx.set_option(capi.OPT_SYNTH_PATH, 4)
+            out.append(ctx.batch_synth_checksums(5, 3, 3 * 256 - 5, batch=256))
+        return out
+    try:
+        ref = run(0, 1)
+        for ov, split in ((1, 1), (1, 0)):
+            for a, b in zip(ref, run(ov, split)):
+                np.testing.assert_array_equal(a, b)
+    finally:
+        ctx.batch_clear()
+        ctx.set_options(shipped)
+
+
 @pytest.mark.parametrize("fuse", [0, 1])
 @pytest.mark.parametrize("R", [333, 1024, 1100])
 def test_warp_specialised_interpolation_is_bitwise_identical(ctx, capi, shipped, fuse, R):
