@@ -39,7 +39,7 @@ GRID_INTERP = {0: ("k_grid_interp_mfma<false, false, 8>", "fp64-mfma"), 1: ("k_g
 # layout tag of the gridded plan a PMC traffic record must carry to describe the shipped interpolation kernel
 # (32-TOA chunks, every grid signal's band back to back, coalesced signals); older tags describe earlier plans
 GRID_LAYOUT = "band32c"
-GRID_DFT = {True: "k_grid_dft_mfma<2,4>", False: "k_grid_dft<8>"}
+GRID_DFT = {True: "k_grid_dft_mfma<2,2>", False: "k_grid_dft<8>"}
 
 
 def parse():

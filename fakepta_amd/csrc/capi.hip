@@ -64,7 +64,9 @@ struct Seg {
 struct GridSeg {
   int32_t nf = 0, half = 0, lde = 0, ntab = 0;
   int64_t rowoff = 0;
-  DevBuf ecos, esin;
+  DevBuf ecos, esin;  // half-range tables (k_grid_dft)
+  int32_t ldq = 0, ntq = 0;
+  DevBuf tq;          // quarter-range tables by mode parity (k_grid_dft_mfma)
 };
 
 // Gridded-synthesis plan of a layout (built once per layout, reused by every batch).
@@ -799,19 +801,18 @@ int grid_build(fpta_ctx* c, Layout& L) {
   std::vector<std::vector<double>> D(n_seg, std::vector<double>(N));
   std::vector<int32_t> nf(n_seg), ws(n_seg);
   std::vector<double> betas(n_seg);
-  // Per grid signal: the options' (w, sigma) give nf0 = sigma (2 N + 1) grid points; the DFT computes whole blocks
-  // of kGridDftRows rows of the half range, so nf1 = 2 (rows of those blocks - 1) points cost it nothing more. The
-  // larger effective oversampling sigma1 = nf1 / (2 N + 1) reaches the options' a-priori bound with a narrower kernel
-  // w1; the signal takes (nf1, w1) when its interpolation band (w + the cells a 32-TOA chunk spans) is estimated
-  // narrower. C2: red noise + GWB (30 modes) nf 92 -> 126, w 15 -> 13; DM (100 modes) keeps 302 / 15.
+  // Per grid signal: the options' (w, sigma) give nf0 = sigma (2 N + 1) grid points, a multiple of 4 (the MFMA DFT
+  // runs on the quarter range); it computes whole blocks of kGridDftRows rows of the quarter range, so nf1 = 4 (rows
+  // of those blocks - 1) points cost it nothing more. The larger effective oversampling sigma1 = nf1 / (2 N + 1)
+  // reaches the options' a-priori bound with a narrower kernel w1; the signal takes (nf1, w1) when its interpolation
+  // band (w + the cells a 32-TOA chunk spans) is estimated narrower.
   const double bound_target = G.err_bound;
   G.err_bound = 0.0;
   for (int32_t s = 0; s < n_seg; ++s) {
     const Seg* sg = L.segs[G.anchor[s]];
     const SegDesc& d = sg->d;
     int32_t n = (int32_t)std::ceil(G.sigma * (2.0 * d.nm + 1.0));
-    n += n & 1;
-    int32_t n0 = std::max(n, 2 * G.w + 2), w0 = G.w;
+    int32_t n0 = (std::max(n, 2 * G.w + 2) + 3) / 4 * 4, w0 = G.w;
     // grid cells per TOA per grid point: mean over pulsars of w0 dt / (2 pi), dt the mean TOA spacing
     double rho = 0.0;
     for (int32_t p = 0; p < L.P; ++p) {
@@ -824,8 +825,8 @@ int grid_build(fpta_ctx* c, Layout& L) {
       if (a1 - a0 > 1) rho += sg->h_w0[d.kind == 0 ? p : 0] * (tmax - tmin) / (double)(a1 - a0 - 1) / (2.0 * M_PI);
     }
     rho /= L.P;
-    const int32_t blocks = (n0 / 2 + kGridDftRows) / kGridDftRows;  // ceil((half + 1) / rows per block)
-    const int32_t n1 = 2 * (blocks * kGridDftRows - 1);
+    const int32_t blocks = (n0 / 4 + kGridDftRows) / kGridDftRows;  // ceil((nf / 4 + 1) / rows per block)
+    const int32_t n1 = 4 * (blocks * kGridDftRows - 1);
     const double sig1 = n1 / (2.0 * d.nm + 1.0);
     int32_t w1 = G.w;
     while (w1 > 4 && std::exp(-M_PI * (w1 - 1) * std::sqrt(1.0 - 1.0 / sig1)) <= bound_target) --w1;
@@ -1050,6 +1051,18 @@ int grid_build(fpta_ctx* c, Layout& L) {
     if ((rc = upload(c, gs->ecos, ec.data(), sizeof(double) * ec.size(), "grid ecos")) ||
         (rc = upload(c, gs->esin, es.data(), sizeof(double) * es.size(), "grid esin")))
       return rc;
+    // quarter-range tables by parity: [0] cos / [1] sin of odd k = 2 t + 1 (m = 2 t), [2] / [3] of even k = 2 t + 2
+    gs->ldq = (nf[s] / 4 + kGridDftRows) / kGridDftRows * kGridDftRows;
+    gs->ntq = ((d.nm + 1) / 2 + 7) / 8 * 8;
+    std::vector<double> tq((size_t)4 * gs->ntq * gs->ldq, 0.0);
+    for (int32_t m = 0; m < d.nm; ++m) {
+      const int32_t par = m & 1, t = m >> 1;
+      for (int32_t j = 0; j <= nf[s] / 4; ++j) {
+        tq[((size_t)(2 * par) * gs->ntq + t) * gs->ldq + j] = ec[(size_t)m * gs->lde + j];
+        tq[((size_t)(2 * par + 1) * gs->ntq + t) * gs->ldq + j] = es[(size_t)m * gs->lde + j];
+      }
+    }
+    if ((rc = upload(c, gs->tq, tq.data(), sizeof(double) * tq.size(), "grid quarter tables"))) return rc;
     // weight rows of signal s: its band's virtual offset in the chunk + the TOA's first row in the band
     std::vector<int32_t> row(N);
     for (int64_t t = 0; t < N; ++t) row[t] = (int32_t)J[s][t] + voff[(size_t)s * n_chunks + chunk_of[t]];
@@ -1061,7 +1074,8 @@ int grid_build(fpta_ctx* c, Layout& L) {
                                d_row.as<int32_t>(), d_d.as<double>(), ws[s], beta, vmax, G.wd.as<double>()),
            "k_grid_weights launch");
     HIPCHK(c, hipStreamSynchronize(c->stream), "grid weights sync");  // d_row / d_d are reused
-    G.fma_dft += (double)L.P * (gs->half + 1) * 2.0 * d.nm;
+    // multiply-adds per realization: quarter range by parity on MFMA, half range on VALU
+    G.fma_dft += (double)L.P * ((c->grid_mfma & 1) ? (gs->nf / 4 + 1) * 2.0 * d.nm : (gs->half + 1) * 2.0 * d.nm);
     G.grid_vals += (double)L.P * gs->nf;
     G.fma_grid = G.fma_dft + G.fma_interp;
   }
@@ -1108,6 +1122,9 @@ int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad, bool pipe = fa
       g.nm = d.nm;
       g.col0 = d.col0;
       g.ntab = gs->ntab;
+      g.tq = gs->tq.as<double>();
+      g.ldq = gs->ldq;
+      g.ntq = gs->ntq;
     }
     const bool early_free = c->coef_side && !c->coef_copy_pending;
     const int32_t split = pipe && c->split_g < gsegs.n ? c->split_g : -1;

@@ -86,8 +86,8 @@ constexpr int kGridMI = 8;   // grid rows per wave in k_grid_dft
 #define FPTA_DFT_MJ 2
 #endif
 constexpr int kDftMJ = FPTA_DFT_MJ;      // k_grid_dft_mfma wave tile: 16 MJ grid rows x 16 kDftMR realizations
-constexpr int kDftMR = 8 / FPTA_DFT_MJ;  // (the accumulators stay at 2 MJ MR = 16 tiles)
-constexpr int kGridDftRows = 16 * kDftMJ;  // grid rows of the half range per k_grid_dft_mfma row block
+constexpr int kDftMR = 4 / FPTA_DFT_MJ;  // (the accumulators stay at 4 MJ MR = 16 tiles: two parities, cos and sin)
+constexpr int kGridDftRows = 16 * kDftMJ;  // grid rows per k_grid_dft_mfma row block (quarter range) and k_grid_dft (half)
 struct GridSegDev {
   const double* ecos;  // [nm][lde] q_k cos(2 pi k j / nf), k = m + 1 (zero-padded columns)
   const double* esin;  // [nm][lde] q_k sin(2 pi k j / nf)
@@ -95,6 +95,9 @@ struct GridSegDev {
   int32_t nf, half, lde, nm, col0;
   int32_t ntab;        // mode rows of ecos/esin (nm zero-padded to a multiple of 8)
   int32_t nblk;        // k_grid_dft row blocks of this signal (set by launch_grid_dft*)
+  const double* tq;    // k_grid_dft_mfma: [4][ntq][ldq] q_k cos / sin(2 pi k j / nf), j <= nf / 4, for the modes of
+                       // odd k (m = 2 t) and of even k (m = 2 t + 1), t < ntq (zero-padded)
+  int32_t ldq, ntq;
 };
 constexpr int kGridMaxSeg = 16;  // signals per layout on the gridded path (passed by value as kernel arguments)
 struct GridSegs {

@@ -50,57 +50,28 @@ constexpr int kInterpDepth = FPTA_INTERP_DEPTH;  // k_grid_interp_mfma: steps of
 constexpr int kInterpWPC = FPTA_INTERP_WPC;
 
 // ----------------------------------------------------------------------------- k_grid_dft_mfma
-// Per pulsar two GEMMs sharing the output tile (4 modes per MFMA):
-//   Cj[j][r] = sum_k ecos[k][j] c_k[r],  Sj[j][r] = sum_k esin[k][j] s_k[r],
-//   g_j = Cj + Sj, g_{nf - j} = Cj - Sj (cos even, sin odd in j).
-// A = table (grid row, mode), B = coefficients (mode, realization). Both operands come in tile pairs from one
-// 16-byte load per lane: lane (lr, lg) loads table rows 2 lr, 2 lr + 1 (.x row tile 2u, .y row tile 2u + 1) and
-// realizations 2 lr, 2 lr + 1 (.x realization tile 2m, .y tile 2m + 1), so a 4-mode step issues MJ + MR loads
-// for 2 MJ MR MFMAs (the one-double-per-lane version issued one load per MFMA and was address-unit bound).
-// D of (row tile 2u + h, realization tile 2m + e): lane (lr, lg) register g holds grid row
-// j0 + 32 u + 2 (lg + 4 g) + h, realization r0 + 32 m + 2 lr + e, so the two realization tiles of a pair store
-// one 16-byte value per lane (256-byte runs per grid row). Wave tile 16 MJ rows x 16 MR realizations. The table
-// is zero-padded to ntab (multiple of 8) modes and lde (multiple of 16 MJ) rows; padded coefficient modes
-// re-read the signal's last mode (finite) against zero table rows.
+// Quarter-range real DFT (one radix-2 step, then GEMMs): with nf = 4 Q and theta = 2 pi k j / nf, the modes of odd k
+// (m = k - 1 even) and of even k (m odd) give per grid row j in [0, Q]
+//   Oc_j = sum_{k odd} q_k c_k cos theta,  Os_j = sum_{k odd} q_k s_k sin theta,  Ec_j, Es_j likewise for k even,
+// and, as even-k terms repeat with period nf / 2 and odd-k terms change sign (cos even, sin odd in j),
+//   g_j = E + O,  g_{nf/2 + j} = E - O,  g_{nf/2 - j} = (Ec - Es) - (Oc - Os),  g_{nf - j} = (Ec - Es) + (Oc - Os)
+// (E = Ec + Es, O = Oc + Os): nf nm / 2 multiply-adds per (pulsar, realization), half the half-range DFT's.
+// A = table (grid row, mode of one parity), B = coefficients (mode, realization), four GEMMs sharing the output tile.
+// Both operands come in tile pairs from one 16-byte load per lane: lane (lr, lg) loads table rows 2 lr, 2 lr + 1
+// (.x row tile 2u, .y row tile 2u + 1) and realizations 2 lr, 2 lr + 1 (.x realization tile 2m, .y tile 2m + 1), so
+// a 4-mode step issues MJ + MR loads for 2 MJ MR MFMAs. D of (row tile 2u + h, realization tile 2m + e): lane
+// (lr, lg) register g holds grid row j0 + 32 u + 2 (lg + 4 g) + h, realization r0 + 32 m + 2 lr + e, so the two
+// realization tiles of a pair store one 16-byte value per lane (256-byte runs per grid row). Wave tile 16 MJ rows x
+// 16 MR realizations. Tables tq[4][ntq][ldq] (odd-k cos, odd-k sin, even-k cos, even-k sin) are zero-padded to ntq
+// (multiple of 8) modes per parity and ldq (multiple of 16 MJ) rows; padded modes re-read the parity's last mode
+// (finite) against zero table rows.
 // Grid (1-D, XCD-grouped): a coefficient tile T = (pulsar, 64 MR-realization block) has nz row blocks over all
 // signals, which read the same coefficients; workgroup b runs on XCD b % 8 and the nz row blocks of one tile are
-// consecutive workgroups of one XCD, so the tile is read from HBM once and re-read from that XCD's L2 (a 3-D grid
-// with the row block slowest re-read every coefficient tile from HBM per row block: 0.83 GB per C2 launch).
-template <int MJ, int MR>
-__global__ __launch_bounds__(256, 3) void k_grid_dft_mfma(GridSegs gsegs, const double* __restrict__ coef,
-                                                          int32_t K, int32_t R_pad, int32_t n_xb, int32_t P,
-                                                          int32_t nz) {
-  static_assert(MJ % 2 == 0 && MR % 2 == 0, "operands come in tile pairs");
-  constexpr int PJ = MJ / 2, PR = MR / 2;
-  const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
-  const int tile = (slot / nz) * 8 + xcd;
-  if (tile >= n_xb * P) return;
-  const int bx = tile % n_xb, p = tile / n_xb;
-  int bz = slot - (slot / nz) * nz, s = 0;
-  while (s + 1 < gsegs.n && bz >= gsegs.s[s].nblk) bz -= gsegs.s[s++].nblk;
-  const GridSegDev& gs = gsegs.s[s];
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  const int lr = lane & 15, lg = lane >> 4;
-  const int r0 = (bx * 4 + wave) * 16 * MR;
-  if (r0 >= R_pad) return;
-  const int j0 = bz * 16 * MJ;
-  const double* __restrict__ cp = coef + ((int64_t)p * K + gs.col0 + 2 * lg) * R_pad + r0 + 2 * lr;
-  const double* __restrict__ ec = gs.ecos + (int64_t)lg * gs.lde + j0 + 2 * lr;
-  const double* __restrict__ es = gs.esin + (int64_t)lg * gs.lde + j0 + 2 * lr;
-  d4 C[MJ][MR], S[MJ][MR];
-#pragma unroll
-  for (int u = 0; u < MJ; ++u)
-#pragma unroll
-    for (int i = 0; i < MR; ++i) {
-      C[u][i] = d4{0.0, 0.0, 0.0, 0.0};
-      S[u][i] = d4{0.0, 0.0, 0.0, 0.0};
-    }
-  const int nq = ((gs.nm + 7) >> 3) << 1;  // even: the table has ntab >= nm rounded up to 8 modes (zero rows)
-  // operands of k-step q; the coefficient row is clamped to the signal's last mode (a valid, finite value
-  // that meets a zero table row), so every load is unconditional and the next step's loads stay in
-  // flight across the current step's MFMAs. Two operand sets alternate (unrolled by 2: no register
-  // copies, which would wait on the prefetch).
+// consecutive workgroups of one XCD, so the tile is read from HBM once and re-read from that XCD's L2.
+template <int PJ, int PR>
+__device__ __forceinline__ void dft_parity(d4 (&C)[2 * PJ][2 * PR], d4 (&S)[2 * PJ][2 * PR],
+                                           const double* __restrict__ cb, const double* __restrict__ tc,
+                                           const double* __restrict__ ts, int n, int par, int ldq, int R_pad, int lg) {
   struct Ops {
     dbl2 bc[PR], bs[PR], ac[PJ], as[PJ];
   };
@@ -121,21 +92,25 @@ __global__ __launch_bounds__(256, 3) void k_grid_dft_mfma(GridSegs gsegs, const 
             __builtin_amdgcn_mfma_f64_16x16x4f64(o.as[u].y, o.bs[i].y, S[2 * u + 1][2 * i + 1], 0, 0, 0);
       }
   };
+  // operands of k-step q: modes of this parity t = 4 q + lg (m = 2 t + par), clamped to the parity's last mode (a
+  // valid, finite value that meets a zero table row), so every load is unconditional and the next step's loads stay
+  // in flight across the current step's MFMAs; two operand sets alternate (no register copies)
   auto load = [&](int qq, Ops& o) {
-    const int m = min(4 * qq + lg, gs.nm - 1) - lg;  // mode of lane group 0 (clamped)
-    const double* __restrict__ cq = cp + (int64_t)(2 * m) * R_pad;
-    const int64_t eo = (int64_t)(4 * qq) * gs.lde;
+    const int m = 2 * min(4 * qq + lg, n - 1) + par;
+    const double* __restrict__ cq = cb + (int64_t)(2 * m) * R_pad;
 #pragma unroll
     for (int i = 0; i < PR; ++i) {
       o.bc[i] = *(const dbl2*)(cq + 32 * i);
       o.bs[i] = *(const dbl2*)(cq + R_pad + 32 * i);
     }
+    const int64_t eo = (int64_t)(4 * qq) * ldq;
 #pragma unroll
     for (int u = 0; u < PJ; ++u) {
-      o.ac[u] = *(const dbl2*)(ec + eo + 32 * u);
-      o.as[u] = *(const dbl2*)(es + eo + 32 * u);
+      o.ac[u] = *(const dbl2*)(tc + eo + 32 * u);
+      o.as[u] = *(const dbl2*)(ts + eo + 32 * u);
     }
   };
+  const int nq = ((n + 7) >> 3) << 1;  // even: the tables hold ntq >= n rounded up to 8 modes (zero rows)
   Ops o0, o1;
   load(0, o0);
   for (int q = 0; q < nq; q += 2) {
@@ -144,6 +119,45 @@ __global__ __launch_bounds__(256, 3) void k_grid_dft_mfma(GridSegs gsegs, const 
     load(min(q + 2, nq - 1), o0);
     mfma(o1);
   }
+}
+
+template <int MJ, int MR>
+__global__ __launch_bounds__(256, 3) void k_grid_dft_mfma(GridSegs gsegs, const double* __restrict__ coef,
+                                                          int32_t K, int32_t R_pad, int32_t n_xb, int32_t P,
+                                                          int32_t nz) {
+  static_assert(MJ % 2 == 0 && MR % 2 == 0, "operands come in tile pairs");
+  constexpr int PJ = MJ / 2, PR = MR / 2;
+  const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
+  const int tile = (slot / nz) * 8 + xcd;
+  if (tile >= n_xb * P) return;
+  const int bx = tile % n_xb, p = tile / n_xb;
+  int bz = slot - (slot / nz) * nz, s = 0;
+  while (s + 1 < gsegs.n && bz >= gsegs.s[s].nblk) bz -= gsegs.s[s++].nblk;
+  const GridSegDev& gs = gsegs.s[s];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int lr = lane & 15, lg = lane >> 4;
+  const int r0 = (bx * 4 + wave) * 16 * MR;
+  if (r0 >= R_pad) return;
+  const int j0 = bz * 16 * MJ;
+  const double* __restrict__ cb = coef + ((int64_t)p * K + gs.col0) * R_pad + r0 + 2 * lr;
+  // [0] odd k (m even), [1] even k (m odd): cos and sin accumulators
+  d4 C[2][MJ][MR], S[2][MJ][MR];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int u = 0; u < MJ; ++u)
+#pragma unroll
+      for (int i = 0; i < MR; ++i) {
+        C[a][u][i] = d4{0.0, 0.0, 0.0, 0.0};
+        S[a][u][i] = d4{0.0, 0.0, 0.0, 0.0};
+      }
+  const int64_t tstride = (int64_t)gs.ntq * gs.ldq;
+  const double* __restrict__ t0 = gs.tq + (int64_t)lg * gs.ldq + j0 + 2 * lr;
+  const int n_odd = (gs.nm + 1) >> 1, n_even = gs.nm >> 1;
+  dft_parity<PJ, PR>(C[0], S[0], cb, t0, t0 + tstride, n_odd, 0, gs.ldq, R_pad, lg);
+  if (n_even > 0) dft_parity<PJ, PR>(C[1], S[1], cb, t0 + 2 * tstride, t0 + 3 * tstride, n_even, 1, gs.ldq, R_pad, lg);
+  const int Q = gs.nf >> 2, H = gs.nf >> 1;
   double* __restrict__ gp = gs.g + (int64_t)p * gs.nf * R_pad + r0 + 2 * lr;
 #pragma unroll
   for (int u = 0; u < PJ; ++u)
@@ -152,12 +166,25 @@ __global__ __launch_bounds__(256, 3) void k_grid_dft_mfma(GridSegs gsegs, const 
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int j = j0 + 32 * u + 2 * (lg + 4 * g) + h;
+        if (j > Q) continue;
 #pragma unroll
         for (int i = 0; i < PR; ++i) {
-          const double c0 = C[2 * u + h][2 * i][g], s0 = S[2 * u + h][2 * i][g];
-          const double c1 = C[2 * u + h][2 * i + 1][g], s1 = S[2 * u + h][2 * i + 1][g];
-          if (j <= gs.half) *(dbl2*)(gp + (int64_t)j * R_pad + 32 * i) = dbl2{c0 + s0, c1 + s1};
-          if (j > 0 && 2 * j < gs.nf) *(dbl2*)(gp + (int64_t)(gs.nf - j) * R_pad + 32 * i) = dbl2{c0 - s0, c1 - s1};
+          double pe[2], me[2], po[2], mo[2];
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const double oc = C[0][2 * u + h][2 * i + e][g], os = S[0][2 * u + h][2 * i + e][g];
+            const double ec = C[1][2 * u + h][2 * i + e][g], es = S[1][2 * u + h][2 * i + e][g];
+            pe[e] = ec + es;
+            me[e] = ec - es;
+            po[e] = oc + os;
+            mo[e] = oc - os;
+          }
+          *(dbl2*)(gp + (int64_t)j * R_pad + 32 * i) = dbl2{pe[0] + po[0], pe[1] + po[1]};
+          *(dbl2*)(gp + (int64_t)(H + j) * R_pad + 32 * i) = dbl2{pe[0] - po[0], pe[1] - po[1]};
+          if (j > 0 && j < Q) {
+            *(dbl2*)(gp + (int64_t)(H - j) * R_pad + 32 * i) = dbl2{me[0] - mo[0], me[1] - mo[1]};
+            *(dbl2*)(gp + (int64_t)(gs.nf - j) * R_pad + 32 * i) = dbl2{me[0] + mo[0], me[1] + mo[1]};
+          }
         }
       }
 }
@@ -939,8 +966,9 @@ hipError_t launch_grid_dft_mfma(hipStream_t st, GridSegs gsegs, int32_t P, const
   int64_t gz = 0;
   for (int s = 0; s < gsegs.n; ++s) {
     GridSegDev& g = gsegs.s[s];
-    g.nblk = (g.half + 16 * kDftMJ) / (16 * kDftMJ);  // ceil((half + 1) / (16 MJ))
-    if (g.lde < g.nblk * 16 * kDftMJ || g.ntab < ((g.nm + 7) & ~7)) return hipErrorInvalidValue;
+    if (g.nf % 4 != 0 || !g.tq) return hipErrorInvalidValue;  // quarter-range tables
+    g.nblk = (g.nf / 4 + 16 * kDftMJ) / (16 * kDftMJ);  // ceil((nf / 4 + 1) / (16 MJ))
+    if (g.ldq < g.nblk * 16 * kDftMJ || g.ntq < ((((g.nm + 1) >> 1) + 7) & ~7)) return hipErrorInvalidValue;
     gz += g.nblk;
   }
   const int64_t n_xb = (R_pad + 64 * kDftMR - 1) / (64 * kDftMR);
