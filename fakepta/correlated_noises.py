@@ -154,7 +154,10 @@ def add_common_correlated_noise(psrs, orf='hd', spectrum='powerlaw', name='gw', 
             p.update_noisedict(signal_name, kwargs)
     else:
         raise ValueError(f'unknown spectrum {spectrum!r}')
-    n_modes = len(f_psd)
+    # the reference sizes `fourier` / `nbin` by `components` and loops range(components) over the first modes of
+    # f_psd, storing the full f and psd (correlated_noises.py:140-160); with fewer frequencies than components it
+    # injects every mode, draws one more (sin, cos) pair and fails on coeffs[2 * len(f_psd)] (:157)
+    n_modes = min(int(components), len(f_psd))
     # replace-on-reinject (correlated_noises.py:133-134), all pulsars in one GPU launch
     if any(signal_name in p.signal_model for p in psrs):
         old = reconstruct_array(psrs, [signal_name])
@@ -162,8 +165,9 @@ def add_common_correlated_noise(psrs, orf='hd', spectrum='powerlaw', name='gw', 
             p.residuals -= r
     for p in psrs:
         p.signal_model[signal_name] = {'orf': orf, 'spectrum': spectrum, 'hmap': h_map, 'f': f_psd, 'psd': psd,
-                                       'fourier': np.zeros((2, n_modes)), 'nbin': n_modes, 'idx': idx}
-    amp0 = np.sqrt(np.repeat(psd, 2))[0::2]           # coeffs[2i] of correlated_noises.py:147
+                                       'fourier': np.zeros((2, components)), 'nbin': components, 'idx': idx}
+    amp0 = np.sqrt(np.repeat(psd, 2))[0::2][:n_modes]  # coeffs[2i] of correlated_noises.py:147
+    sq_df = df[:n_modes] ** 0.5
     L = orf_factor(orf_matrix(psrs, orf, h_map))
     P = len(psrs)
     # multivariate_normal(mean=0, cov=orf) draws standard_normal(P) per call: sin first, then cos
@@ -173,14 +177,19 @@ def add_common_correlated_noise(psrs, orf='hd', spectrum='powerlaw', name='gw', 
         z[i, 1] = np.random.standard_normal(P)
     offs = np.concatenate([[0], np.cumsum([len(p.toas) for p in psrs])]).astype(np.int64)
     res = np.concatenate([p.residuals for p in psrs])
-    x = _capi.get_context().common_accumulate(offs, np.concatenate([p.toas for p in psrs]),
-                                              np.concatenate([p.freqs for p in psrs]), f_psd, df ** 0.5 * amp0,
-                                              float(idx), float(freqf), L, z, res)
+    if n_modes:
+        x = _capi.get_context().common_accumulate(offs, np.concatenate([p.toas for p in psrs]),
+                                                  np.concatenate([p.freqs for p in psrs]), f_psd[:n_modes],
+                                                  sq_df * amp0, float(idx), float(freqf), L, z, res)
     for n, p in enumerate(psrs):
         p.residuals[:] = res[offs[n]:offs[n + 1]]
-        p.signal_model[signal_name]['fourier'][0] = x[:, 0, n] * amp0 / df ** 0.5
-        p.signal_model[signal_name]['fourier'][1] = x[:, 1, n] * amp0 / df ** 0.5
-
+        if n_modes:
+            p.signal_model[signal_name]['fourier'][0, :n_modes] = x[:, 0, n] * amp0 / sq_df
+            p.signal_model[signal_name]['fourier'][1, :n_modes] = x[:, 1, n] * amp0 / sq_df
+    if components > n_modes:
+        np.random.standard_normal(P)
+        np.random.standard_normal(P)
+        raise IndexError(f'index {2 * len(f_psd)} is out of bounds for axis 0 with size {2 * len(f_psd)}')
 
 def add_roemer_delay(psrs, planet, d_mass=0., d_Om=0., d_omega=0., d_inc=0., d_a=0., d_e=0., d_l0=0.):
     """Ephemeris-error Roemer delay (correlated_noises.py:163-172). Deterministic, not part of the

@@ -44,6 +44,16 @@ def _df(f):
     return np.diff(np.append(0.0, f))
 
 
+def _stored_modes(sm):
+    """(f, df, fourier) of a stored GP truncated to the modes reconstruct_signal's zip(c.T, f, df) visits
+    (fake_pta.py:539-545): a common signal injected with components < len(f_psd) stores every frequency but
+    only `components` coefficient pairs (correlated_noises.py:140-143)."""
+    f = np.asarray(sm['f'], dtype=float)
+    c = np.asarray(sm['fourier'], dtype=float)
+    n = min(len(f), c.shape[1])
+    return f[:n], _df(f)[:n], c[:, :n]
+
+
 class Pulsar:
     """ENTERPRISE-compatible fake pulsar (fakepta/fake_pta.py:24-567)."""
 
@@ -447,14 +457,14 @@ class Pulsar:
                     sig += det.cw_delay(self.toas, self.pos, self.pdist, **entry)
             if signal in _GP_SIGNALS or 'common' in signal:
                 sm = self.signal_model[signal]
-                df = _df(sm['f'])
-                segs.append((sm['f'], df * sm['fourier'][0], df * sm['fourier'][1], float(sm['idx']), float(freqf)))
+                f, df, c = _stored_modes(sm)
+                segs.append((f, df * c[0], df * c[1], float(sm['idx']), float(freqf)))
                 masks.append(None)
             if 'system_noise' in signal:
                 sm = self.signal_model[signal]
                 backend = signal.split('system_noise_')[1]
-                df = _df(sm['f'])
-                segs.append((sm['f'], df * sm['fourier'][0], df * sm['fourier'][1], 0.0, float(freqf)))
+                f, df, c = _stored_modes(sm)
+                segs.append((f, df * c[0], df * c[1], 0.0, float(freqf)))
                 masks.append(self.backend_flags == backend)
         if segs:
             _capi.get_context().gp_accumulate(self.toas, self.freqs, segs, sig,
@@ -490,24 +500,24 @@ def reconstruct_array(psrs, signals=None, freqf=1400):
         if not (gp or sysn):
             continue
         have = [p.signal_model[signal] if signal in p.signal_model else None for p in psrs]
-        nm = max((len(sm['f']) for sm in have if sm is not None), default=0)
+        have = [None if sm is None else (sm, *_stored_modes(sm)) for sm in have]
+        nm = max((len(h[1]) for h in have if h is not None), default=0)
         if nm == 0:
             continue
         f = np.zeros((P, nm))
         cc = np.zeros((P, nm))
         cs = np.zeros((P, nm))
         idx = None
-        for i, sm in enumerate(have):
-            if sm is None:
+        for i, h in enumerate(have):
+            if h is None:
                 f[i] = np.arange(1, nm + 1) / max(psrs[i].Tspan, 1.0)
                 continue
-            fi = np.asarray(sm['f'], float)
-            df = _df(fi)
+            sm, fi, df, c = h
             f[i, :len(fi)] = fi
             if len(fi) < nm:  # zero-amplitude continuation of the grid
                 f[i, len(fi):] = fi[-1] + fi[0] * np.arange(1, nm - len(fi) + 1)
-            cc[i, :len(fi)] = df * sm['fourier'][0]
-            cs[i, :len(fi)] = df * sm['fourier'][1]
+            cc[i, :len(fi)] = df * c[0]
+            cs[i, :len(fi)] = df * c[1]
             idx = float(sm['idx']) if idx is None else idx
             if float(sm['idx']) != idx:
                 raise ValueError(f'signal {signal!r} has different chromatic indices across pulsars')

@@ -55,6 +55,7 @@ _SIGS = [
     ("fpta_batch_correlations", _c_int, [_ctx_p, _i32, _vp]),
     ("fpta_batch_info", _c_int, [_ctx_p, _vp]),
     ("fpta_batch_grid_info", _c_int, [_ctx_p, _vp]),
+    ("fpta_batch_grid_info_n", _c_int, [_ctx_p, _vp, _i32]),
     ("fpta_set_option", _c_int, [_ctx_p, _i32, _i64]),
     ("fpta_kernel_stats", _c_int, [_ctx_p, _i32, ctypes.POINTER(_i64), ctypes.POINTER(_dbl)]),
     ("fpta_reset_stats", _c_int, [_ctx_p]),
@@ -294,9 +295,9 @@ class Context:
 
     def batch_grid_info(self):
         """Gridded-path plan figures, the path of the last batch and why it was not the gridded path
-        (fpta_batch_grid_info, fpta_batch_path_reason)."""
+        (fpta_batch_grid_info_n, fpta_batch_path_reason)."""
         g = np.zeros(16, dtype=np.float64)
-        self._check(_lib.fpta_batch_grid_info(self._h, _ptr(g)), "fpta_batch_grid_info")
+        self._check(_lib.fpta_batch_grid_info_n(self._h, _ptr(g), len(g)), "fpta_batch_grid_info_n")
         keys = ("last_path", "ok", "n_chunks", "fma_dft", "fma_interp", "fma_direct", "grid_vals", "weight_bytes",
                 "grid_mfma", "err_bound", "width", "sigma", "grid_signals", "signals", "band_rows_per_chunk")
         d = dict(zip(keys, g.tolist()))
@@ -406,14 +407,23 @@ class Context:
 
 
 class _Borrowed(Context):
-    """A device context owned by a MultiContext (not destroyed by this wrapper)."""
+    """A device context owned by a MultiContext (not destroyed by this wrapper). It keeps its parent alive and is
+    invalidated when the parent closes, so a call on it never reaches a context fpta_multi_destroy has freed."""
 
-    def __init__(self, handle, device):
+    def __init__(self, handle, device, parent):
         self._h = handle
         self.device = device
+        self._parent = parent
 
     def close(self):
         self._h = None
+
+    def __getattribute__(self, name):
+        if name not in ("_h", "_parent", "device", "close", "__class__", "__dict__") and not name.startswith("__"):
+            parent = object.__getattribute__(self, "_parent")
+            if object.__getattribute__(self, "_h") is None or getattr(parent, "_h", None) is None:
+                raise FptaError("context of a closed MultiContext")
+        return object.__getattribute__(self, name)
 
 
 class MultiContext:
@@ -436,6 +446,8 @@ class MultiContext:
 
     def close(self):
         if getattr(self, "_h", None):
+            for b in getattr(self, "_borrowed", ()):
+                b.close()
             _lib.fpta_multi_destroy(self._h)
             self._h = None
 
@@ -449,7 +461,11 @@ class MultiContext:
         return int(_lib.fpta_multi_size(self._h))
 
     def context(self, i):
-        return _Borrowed(_lib.fpta_multi_context(self._h, int(i)), self.devices[i])
+        if not getattr(self, "_h", None):
+            raise FptaError("MultiContext is closed")
+        b = _Borrowed(_lib.fpta_multi_context(self._h, int(i)), self.devices[i], self)
+        self.__dict__.setdefault("_borrowed", []).append(b)
+        return b
 
     def set_toas(self, offs, toas, nu):
         offs = np.ascontiguousarray(offs, dtype=np.int64)

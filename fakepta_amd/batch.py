@@ -24,6 +24,13 @@ def _df(f):
     return np.diff(np.append(0.0, f))
 
 
+def _n_modes(sm):
+    """Modes a stored signal carries: its coefficient pairs, at most len(f) (reconstruct_signal's zip,
+    fake_pta.py:543; a common signal stores `components` pairs on a longer f_psd, correlated_noises.py:140-143)."""
+    n = len(sm["f"])
+    return min(n, np.shape(sm["fourier"])[1]) if "fourier" in sm else n
+
+
 def batch_factor(orf_mat):
     """Square root of the ORF for batched draws: the lower Cholesky factor when the ORF is
     positive definite (HD, curn: triangular mixing on device, half the FLOPs), otherwise the SVD
@@ -72,21 +79,25 @@ class BatchSimulator:
             raise KeyError(f"no pulsar carries signal {name!r}")
         sm0 = have[0].signal_model[name]
         if "common" in name:
+            n = _n_modes(sm0)
             f = np.asarray(sm0["f"], float)
-            amp = np.sqrt(np.asarray(sm0["psd"], float) * _df(f))
+            amp = np.sqrt(np.asarray(sm0["psd"], float) * _df(f))[:n]
+            f = f[:n]
             L = batch_factor(orf_matrix(self.psrs, sm0["orf"], sm0.get("hmap")))
             self.add_signal(name, 1, f, amp, idx=float(sm0["idx"]), L=L)
             return
-        nm = max(len(p.signal_model[name]["f"]) for p in have)
+        nm = max(_n_modes(p.signal_model[name]) for p in have)
         f = np.zeros((P, nm))
         amp = np.zeros((P, nm))
         mask = None
         for i, p in enumerate(self.psrs):
             if name in p.signal_model:
                 sm = p.signal_model[name]
+                n = _n_modes(sm)
                 fi = np.asarray(sm["f"], float)
-                f[i, :len(fi)] = fi
-                amp[i, :len(fi)] = np.sqrt(np.asarray(sm["psd"], float) * _df(fi))
+                amp[i, :n] = np.sqrt(np.asarray(sm["psd"], float) * _df(fi))[:n]
+                fi = fi[:n]
+                f[i, :n] = fi
                 if len(fi) < nm:  # continue the grid with zero-amplitude modes
                     step = fi[0] if len(fi) else 1.0
                     f[i, len(fi):] = fi[-1] + step * np.arange(1, nm - len(fi) + 1)
@@ -274,13 +285,18 @@ def simulate_sharded(sim, n_real, seed=0, real0=0, batch=4096, comm=None, on_bat
     lo, hi = shard_bounds(n_real, comm.rank, G)
     sums = np.empty((hi - lo, 2))
     # checksums from the gridded interpolation's partial sums (FPTA_OPT_FUSE_CHECKSUMS): no second pass over
-    # each resident block; the context's own setting is restored afterwards
+    # each resident block;
+    # each rank's context's own settings are restored afterwards. The synthesis path is chosen once for the job
+    # (FPTA_OPT_MFMA_MIN_REAL 1): a tail batch below the default threshold would otherwise take the direct path, and
+    # its realizations would depend on the batch split and the number of ranks
     ctx = getattr(sim, "ctx", None)
-    fuse = None
+    fuse = min_real = None
     if ctx is not None:
         from fakepta_amd import _capi
         fuse = ctx.get_option(_capi.OPT_FUSE_CHECKSUMS)
+        min_real = ctx.get_option(_capi.OPT_MFMA_MIN_REAL)
         ctx.set_option(_capi.OPT_FUSE_CHECKSUMS, 1)
+        ctx.set_option(_capi.OPT_MFMA_MIN_REAL, 1)
     try:
         if ctx is not None and on_batch is None and hi > lo:
             # no per-batch consumer: the whole shard streams inside the library, batches back to back
@@ -294,5 +310,6 @@ def simulate_sharded(sim, n_real, seed=0, real0=0, batch=4096, comm=None, on_bat
     finally:
         if fuse is not None:
             ctx.set_option(_capi.OPT_FUSE_CHECKSUMS, fuse)
+            ctx.set_option(_capi.OPT_MFMA_MIN_REAL, min_real)
     sizes = [shard_bounds(n_real, g, G)[1] - shard_bounds(n_real, g, G)[0] for g in range(G)]
     return comm.gather_to_root(sums, sizes)

@@ -226,14 +226,14 @@ struct fpta_ctx {
   int32_t part_chunks = 0, part_rpad = 0;
   int last_path = 0;     // synthesis path of the last batch (1 direct, 2 MFMA, 3 VALU, 4 gridded)
   std::string path_reason;  // why the last batch did not take the gridded path (empty if it did)
-  // gridded path defaults: w = 16 at sigma = 1.5. Flat-spectrum worst case at real-MJD epochs 1.4e-12 (100 modes)
-  // and 3.6e-12 (257 modes) relative (the numpy model of oracle.grid_synth and the GPU agree); the earlier
-  // w = 14 reached 3.2e-11 there (profiles/r02_gputest1.log). sigma = 1.5 keeps the grid (DFT) a quarter
-  // smaller than sigma = 2 (tools/sweep_grid.py --params, profiles/r01_sweep_wsig.txt)
+  // gridded path defaults: w = 15 at sigma = 1.5 (a-priori bound 1.5e-12). The measured flat-spectrum worst case at
+  // real-MJD epochs is <= ~6e-12 relative (tests/test_gpu_grid.py at the shipped defaults; the numpy model of
+  // oracle.grid_synth and the GPU agree); w = 14 (bound 9.4e-12) is refused by the auto path. sigma = 1.5 keeps the
+  // grid (DFT) a quarter smaller than sigma = 2 (tools/sweep_grid.py --params, profiles/r01_sweep_wsig.txt)
   int grid_w = 15;       // gridded path: kernel width in grid cells
   int grid_sigma100 = 150;  // gridded path: oversampling x 100
-  int grid_mfma = 1;     // gridded path: bit 0 k_grid_dft_mfma (else k_grid_dft); the interpolation is always
-                         // k_grid_interp_mfma
+  int grid_mfma = 1;     // gridded path: bit 0 k_grid_dft_mfma (else k_grid_dft); the interpolation is always on
+                         // MFMA (k_grid_interp_ws / k_grid_interp_mfma)
   // profiling
   struct Pending {
     int which;
@@ -591,6 +591,7 @@ int run_coefficients(fpta_ctx* c, Layout& L, uint64_t seed, int64_t real0, int32
     m.dst = L.segs[G.anchor[g]]->d.col0;
     for (int32_t i : G.members[g])
       if (i != G.anchor[g] && fuse_into[i] < 0) {
+        if (m.n >= kGridMaxSeg) return fail(c, FPTA_EINVAL, "coef merge: more than kGridMaxSeg members");
         m.src[m.n] = L.segs[i]->d.col0;
         m.ncol[m.n++] = 2 * L.segs[i]->d.nm;
       }
@@ -769,6 +770,8 @@ int grid_build(fpta_ctx* c, Layout& L) {
     for (int32_t i = 0; i < n_layout; ++i) {
       int32_t join = -1;
       for (size_t g = 0; c->grid_coalesce && g < G.members.size() && join < 0; ++g) {
+        // a grid signal merges at most kGridMaxSeg other members (CoefMerge::src): a full group starts a new one
+        if (G.members[g].size() > (size_t)kGridMaxSeg) continue;
         const int32_t f = G.members[g][0];
         bool same = true;
         for (int32_t p = 0; p < L.P && same; ++p) same = w0_of(i, p) == w0_of(f, p);
@@ -1578,8 +1581,9 @@ int fpta_set_option(fpta_ctx* c, int32_t key, int64_t value) {
       c->fuse_white = value ? 1 : 0;
       return FPTA_OK;
     case FPTA_OPT_GRID_MFMA:
-      if (value < 0 || value > 1) return fail(c, FPTA_EINVAL, "grid MFMA mask must be 0 or 1");
-      c->grid_mfma = (int)value;
+      // bit 1 (the interpolation kernel in round 1) is accepted and ignored: the interpolation is always on MFMA
+      if (value < 0 || value > 3) return fail(c, FPTA_EINVAL, "grid MFMA mask must be in 0..3");
+      c->grid_mfma = (int)(value & 1);
       return FPTA_OK;
     case FPTA_OPT_FUSE_CHECKSUMS:
       c->fuse_sums = value ? 1 : 0;
@@ -2137,10 +2141,11 @@ int fpta_batch_info(fpta_ctx* c, int64_t* info) {
   return FPTA_OK;
 }
 
-int fpta_batch_grid_info(fpta_ctx* c, double* out) {
-  if (!c || !out) return fail(c, FPTA_EINVAL, "grid_info: bad arguments");
+int fpta_batch_grid_info_n(fpta_ctx* c, double* dst, int32_t n_out) {
+  if (!c || !dst || n_out < 0) return fail(c, FPTA_EINVAL, "grid_info: bad arguments");
   const GridPlan& G = c->batch.grid;
   const bool ok = G.built && G.ok;
+  double out[FPTA_GRID_INFO_LEN];
   out[0] = c->last_path;
   out[1] = ok ? 1.0 : 0.0;
   out[2] = ok ? G.n_chunks : 0.0;
@@ -2157,7 +2162,14 @@ int fpta_batch_grid_info(fpta_ctx* c, double* out) {
   out[13] = (double)c->batch.segs.size();
   out[14] = ok ? G.mean_v : 0.0;
   out[15] = 0.0;
-  return FPTA_OK;
+  std::memcpy(dst, out, sizeof(double) * std::min<int32_t>(n_out, FPTA_GRID_INFO_LEN));
+  return FPTA_GRID_INFO_LEN;
+}
+
+// the round-1 contract: 9 values (a caller's double[9] stays in bounds)
+int fpta_batch_grid_info(fpta_ctx* c, double* out) {
+  const int rc = fpta_batch_grid_info_n(c, out, 9);
+  return rc < 0 ? rc : FPTA_OK;
 }
 
 const char* fpta_batch_path_reason(const fpta_ctx* c) { return c ? c->path_reason.c_str() : ""; }
@@ -2316,11 +2328,15 @@ static int stream_checksums(fpta_multi* m, uint64_t seed, int64_t real0, int64_t
     if (e == hipSuccess) e = hipHostMalloc((void**)&stage[g], sizeof(double) * 2 * n, hipHostMallocDefault);
     if (e != hipSuccess) rc = multi_fail(m, (int)g, hip_fail(c, e, "multi_synth staging"));
   }
-  // a checksums-only job: the gridded interpolation writes partial checksums (no second pass over each block)
-  std::vector<int> fuse(G);
+  // a checksums-only job: the gridded interpolation writes partial checksums (no second pass over each block).
+  // The path is chosen once for the job, not per batch: a tail batch below FPTA_OPT_MFMA_MIN_REAL would otherwise
+  // take the direct path and its realizations (and checksums) would depend on the batch split and device count
+  std::vector<int> fuse(G), min_real(G);
   for (int64_t g = 0; g < G; ++g) {
     fuse[g] = m->ctx[g]->fuse_sums;
     m->ctx[g]->fuse_sums = 1;
+    min_real[g] = m->ctx[g]->mfma_min_real;
+    m->ctx[g]->mfma_min_real = 1;
   }
   // round-robin: batch k of every device, then batch k + 1 (each device's stream orders its own work)
   for (int64_t k = 0; !rc; ++k) {
@@ -2346,7 +2362,10 @@ static int stream_checksums(fpta_multi* m, uint64_t seed, int64_t real0, int64_t
     if (!rc) std::memcpy(checksums_out + 2 * (beg[g] - 0), stage[g], sizeof(double) * 2 * (beg[g + 1] - beg[g]));
     (void)hipHostFree(stage[g]);
   }
-  for (int64_t g = 0; g < G; ++g) m->ctx[g]->fuse_sums = fuse[g];
+  for (int64_t g = 0; g < G; ++g) {
+    m->ctx[g]->fuse_sums = fuse[g];
+    m->ctx[g]->mfma_min_real = min_real[g];
+  }
   return rc;
 }
 

@@ -951,7 +951,7 @@ hipError_t launch_grid_interp_ws(hipStream_t st, const SynthArgs& a, const GridB
         hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0)
       n_cu = 256;
   }
-  // persistent: one workgroup per CU (the ring takes 136 KB of the 160 KB LDS)
+  // persistent: one workgroup per CU (the 4-slot ring takes 4 x 17 KB = 68 KB of the 160 KB LDS)
   const int64_t grid = std::min<int64_t>((tiles + 7) / 8 * 8, ((int64_t)n_cu + 7) / 8 * 8);
   if (a.part) return hipErrorInvalidValue;  // fused partial checksums take k_grid_interp_mfma (faster there)
   hipLaunchKernelGGL(k_grid_interp_ws<false>, dim3((unsigned)grid), dim3(512), 0, st, a, band, (int32_t)tiles, R_pad, a.out);

@@ -209,7 +209,11 @@ int fpta_batch_info(fpta_ctx* ctx, int64_t* info);
  * relative aliasing bound exp(-pi w sqrt(1 - 1/sigma)) of the width/oversampling options in force (auto
  * selection takes the gridded path only when it is <= 2e-12), out[10] width w, out[11] oversampling sigma,
  * out[12] grid signals of the plan (signals after FPTA_OPT_GRID_COALESCE), out[13] layout signals, out[14]
- * mean band rows per chunk (all grid signals, padded to 4). out: host double[16]. */
+ * mean band rows per chunk (all grid signals, padded to 4).
+ * fpta_batch_grid_info_n writes the first min(n_out, FPTA_GRID_INFO_LEN) values and returns FPTA_GRID_INFO_LEN
+ * (negative on error); fpta_batch_grid_info keeps the round-1 contract: out[0..8], host double[9]. */
+#define FPTA_GRID_INFO_LEN 16
+int fpta_batch_grid_info_n(fpta_ctx* ctx, double* out, int32_t n_out);
 int fpta_batch_grid_info(fpta_ctx* ctx, double* out);
 /* Why the last batch did not take the gridded path (signal count, non-harmonic grid, error bound, cost,
  * n_real below the threshold, ...); "" when it did. Owned by the context, valid until the next batch. */

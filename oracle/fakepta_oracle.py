@@ -197,17 +197,20 @@ def mvn_factor(cov):
     return (np.sqrt(s)[:, None] * vt).T
 
 
-def common_synth_loop(toas_list, freqs_list, f, psd, z, L, idx, freqf=1400.0):
-    """Loop-faithful restatement of fakepta/correlated_noises.py:146-160.
+def common_synth_loop(toas_list, freqs_list, f, psd, z, L, idx, freqf=1400.0, components=None):
+    """Loop-faithful restatement of fakepta/correlated_noises.py:140-160.
 
     z: [N, 2, P] standard normals in the reference's draw order (sin vector first, then cos).
-    Returns (residual list, fourier [P, 2, N])."""
+    components: modes looped (default len(f)); fourier is [P, 2, components] (:142) and the loop runs over the
+    first `components` entries of f, so components > len(f) raises IndexError as the reference does at :157.
+    Returns (residual list, fourier [P, 2, components])."""
     P = len(toas_list)
+    components = len(f) if components is None else int(components)
     df = delta_f(f)
     coeffs = np.sqrt(np.repeat(psd, 2))
     res = [np.zeros(len(t)) for t in toas_list]
-    fourier = np.zeros((P, 2, len(f)))
-    for i in range(len(f)):
+    fourier = np.zeros((P, 2, components))
+    for i in range(components):
         orf_corr_sin = L @ z[i, 0]
         orf_corr_cos = L @ z[i, 1]
         for n in range(P):

@@ -40,3 +40,31 @@ def common_signal(rng, offs, toas, n_modes, log10_A=-14.5, gamma=13 / 3, orf="hd
         pos = v / np.linalg.norm(v, axis=1)[:, None]
     L = O.mvn_factor(O.ORFS[orf](pos))
     return f, amp, L, pos
+
+
+class EnterpriseStandin:
+    """Stand-in for an enterprise.pulsar.Pulsar built from fixture G8's arrays (tools/gen_golden.py
+    g8_standin_arrays): exactly the attributes copy_array reads (reference fake_pta.py:687-712)."""
+
+    def __init__(self, a, i):
+        lo, hi = a["offs"][i], a["offs"][i + 1]
+        self.name = str(a["names"][i])
+        self.toas = a["toas"][lo:hi].copy()
+        self.freqs = a["freqs"][lo:hi].copy()
+        self.toaerrs = a["toaerrs"][lo:hi].copy()
+        self.backend_flags = a["backend_flags"][lo:hi].copy()
+        self.residuals = np.zeros(hi - lo)
+        self.theta, self.phi = float(a["theta"][i]), float(a["phi"][i])
+        self.Mmat = np.stack([np.ones(hi - lo), self.toas - self.toas[0]], 1)
+        self.fitpars = ["Offset", "F0"]
+        self.pdist = (1.0, 0.2)
+        self.planetssb = None
+        self.pos_t = None
+
+
+def g8_inputs(golden):
+    """(stand-in pulsars, noisedict, custom_models, fixture arrays) of fixture G8 (examples/make_fake_array.py)."""
+    g = golden("g8_example_workflow.npz")
+    nd = golden("g8_noisedict_dr2_newsys_trim.json")
+    cm = golden("g8_custom_models_newsys_trim.json")
+    return [EnterpriseStandin(g, i) for i in range(len(g["names"]))], nd, cm, g

@@ -105,3 +105,30 @@ def test_fused_checksums_match_full_pass(c3):
     finally:
         ctx.set_option(_capi.OPT_FUSE_CHECKSUMS, 0)
         ctx.batch_set_white(None, [], [])
+
+
+def test_tail_batch_below_mfma_min_real_is_split_invariant(c3):
+    """A streamed job whose last batch is smaller than FPTA_OPT_MFMA_MIN_REAL (16) draws it on the job's path, not
+    the direct one: checksums are bit-identical for batch 4096 (tail 1), 4097 (one batch), 1000 (tail 97) and 13
+    realizations at a time; in-library streaming, per-batch consumers and the two-context driver agree."""
+    from fakepta_amd import _capi
+    from fakepta_amd.batch import simulate_sharded
+    psrs, sim, ctx = c3
+    n = 4097
+    want = simulate_sharded(sim, n, seed=SEED, real0=11, batch=4097)
+    for batch in (4096, 1000):
+        np.testing.assert_array_equal(simulate_sharded(sim, n, seed=SEED, real0=11, batch=batch), want)
+    np.testing.assert_array_equal(
+        simulate_sharded(sim, n, seed=SEED, real0=11, batch=4096, on_batch=lambda s, first, k: None), want)
+    assert ctx.get_option(_capi.OPT_MFMA_MIN_REAL) == 16  # the context's own setting is restored
+    small = simulate_sharded(sim, 40, seed=SEED, real0=11 + 4000, batch=13)
+    np.testing.assert_array_equal(small, want[4000:4040])
+    m = _capi.MultiContext([0, 0])
+    try:
+        m.set_toas(sim.offs, sim.toas, sim.freqs)
+        for s in sim.segments:
+            m.add_signal(s["kind"], s["f"], s["amp"], idx=s["idx"], L=s["L"], mask=s["mask"])
+        np.testing.assert_array_equal(m.synth_checksums(SEED, 11, n, batch=2048), want)  # shards 2048 + 2049
+        np.testing.assert_array_equal(m.synth_checksums(SEED, 11 + 4000, 40, batch=7), want[4000:4040])
+    finally:
+        m.close()

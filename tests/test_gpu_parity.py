@@ -188,6 +188,107 @@ def test_reference_script_imports_reproduce_g4(golden):
     assert_parity(np.concatenate([p.residuals for p in psrs]), g["residuals"], TOL)
 
 
+def _g8_workflow(golden):
+    """examples/make_fake_array.py:34-47 through the drop-in, on fixture G8's stand-in EPTA pulsars with the
+    reference's own noisedict / custom_models JSON."""
+    from fakepta.correlated_noises import add_common_correlated_noise
+    from fakepta.fake_pta import copy_array
+    from tests.helpers import g8_inputs
+    psrs_0, nd, cm, g = g8_inputs(golden)
+    np.random.seed(int(g["seed"]))
+    psrs = copy_array(psrs_0, nd, cm)
+    for psr in psrs:
+        psr.make_ideal()
+        psr.add_white_noise()
+        psr.add_red_noise()
+        psr.add_dm_noise()
+        psr.add_chromatic_noise()
+    noise = np.concatenate([p.residuals for p in psrs])
+    add_common_correlated_noise(psrs, log10_A=-15., gamma=13 / 3, orf='hd')
+    return psrs, g, noise
+
+
+def test_example_workflow_g8(golden):
+    """Fixture G8: copy_array + noisedict-driven add_red_noise() / add_dm_noise() / add_chromatic_noise() with
+    ragged per-pulsar mode counts (RN 10-99, DM 11-100, Sv 93, None) and the HD GWB reproduce the reference's
+    residuals, signal_model entries and noisedicts."""
+    psrs, g, noise = _g8_workflow(golden)
+    want = golden("g8_example_workflow.json")
+    assert_parity(noise, g["residuals_noise"], TOL)
+    assert_parity(np.concatenate([p.residuals for p in psrs]), g["residuals"], TOL)
+    for i, p in enumerate(psrs):
+        assert p.noisedict == want["noisedicts"][p.name]
+        assert sorted(p.signal_model) == sorted(want["signal_models"][p.name])
+        for sig, meta in want["signal_models"][p.name].items():
+            sm, key = p.signal_model[sig], f"{i}_{sig}"
+            assert sm["nbin"] == meta["nbin"] and float(sm["idx"]) == meta["idx"]
+            np.testing.assert_array_equal(sm["f"], g[key + "_f"])
+            np.testing.assert_array_equal(sm["psd"], g[key + "_psd"])
+            tol = 1e-15 if sig != "gw_common" else 1e-10
+            np.testing.assert_allclose(sm["fourier"], g[key + "_fourier"], rtol=tol,
+                                       atol=tol * np.abs(g[key + "_fourier"]).max())
+            assert_parity(p.reconstruct_signal([sig]), g[key + "_reconstruct"], TOL)
+
+
+@pytest.mark.parametrize("path", [0, 1, 2, 3, 4])
+def test_example_workflow_batch_vs_oracle(golden, capi, path):
+    """BatchSimulator on the G8 array: per-pulsar signals with ragged mode counts (zero-amplitude padding up
+    to the largest), pulsars without a signal, multi-backend white noise, on real-MJD epochs; every synthesis
+    path vs the oracle."""
+    from fakepta_amd.batch import BatchSimulator
+    psrs, _, _ = _g8_workflow(golden)
+    sim = BatchSimulator(psrs, white=True)
+    assert [s["name"] for s in sim.segments] == ["red_noise", "gw_common", "dm_gp", "chrom_gp"]
+    segs = oracle_segments(sim)
+    shipped = sim.ctx.options()
+    sim.ctx.set_option(capi.OPT_SYNTH_PATH, path)
+    try:
+        for real0, R in ((0, 24), (70001, 5)):
+            got = sim.synth(R, seed=17, real0=real0)
+            want = O.batch_synth(sim.offs, sim.toas, sim.freqs, segs, 17, real0, R, sigma=sim.sigma)
+            assert_parity(got, want, TOL)
+    finally:
+        sim.ctx.set_options(shipped)
+
+
+def test_common_components_not_len_f_g9(golden):
+    """Fixture G9 (correlated_noises.py:140-160): with 40 frequencies and components=30 the drop-in injects 30
+    modes, stores f / psd with 40 entries and fourier [2, 30], and leaves np.random where the reference does;
+    with 20 frequencies it injects them all, draws one more pair and raises the reference's IndexError."""
+    from fakepta import correlated_noises as cn
+    from fakepta import fake_pta as fp
+    from fakepta_amd.batch import BatchSimulator
+    g = golden("g9_common_components.npz")
+    np.random.seed(9)
+    psrs = fp.make_fake_array(npsrs=8, Tobs=8, ntoas=90, gaps=True, toaerr=1e-7, isotropic=True,
+                              backends=["A.1400", "B.800"], custom_model={"RN": None, "DM": None, "Sv": None})
+    np.testing.assert_array_equal(np.concatenate([p.toas for p in psrs]), g["toas"])
+    for p in psrs:
+        p.make_ideal()
+    cn.add_common_correlated_noise(psrs, orf="hd", components=30, f_psd=g["long_f"], log10_A=-14.5, gamma=13 / 3,
+                                   idx=2)
+    sm = psrs[0].signal_model["gw_common"]
+    assert sm["nbin"] == 30 and len(sm["f"]) == 40
+    np.testing.assert_array_equal(sm["psd"], g["long_psd"])
+    fourier = np.array([p.signal_model["gw_common"]["fourier"] for p in psrs])
+    np.testing.assert_allclose(fourier, g["long_fourier"], rtol=1e-10, atol=1e-10 * np.abs(fourier).max())
+    assert_parity(np.concatenate([p.residuals for p in psrs]), g["long_residuals"], TOL)
+    assert_parity(np.concatenate([p.reconstruct_signal(["gw_common"]) for p in psrs]), g["long_reconstruct"], TOL)
+    assert_parity(np.concatenate(fp.reconstruct_array(psrs, ["gw_common"])), g["long_reconstruct"], TOL)
+    np.testing.assert_array_equal(np.random.standard_normal(4), g["long_next_draw"])
+    assert BatchSimulator(psrs, white=False).segments[0]["f"].shape == (30,)
+    np.random.seed(19)
+    for p in psrs:
+        p.make_ideal()
+    with pytest.raises(IndexError, match=str(g["short_error"])):
+        cn.add_common_correlated_noise(psrs, orf="hd", components=30, f_psd=g["long_f"][:20], log10_A=-14.5,
+                                       gamma=13 / 3)
+    assert_parity(np.concatenate([p.residuals for p in psrs]), g["short_residuals"], TOL)
+    fourier = np.array([p.signal_model["gw_common"]["fourier"] for p in psrs])
+    np.testing.assert_allclose(fourier, g["short_fourier"], rtol=1e-10, atol=1e-10 * np.abs(fourier).max())
+    np.testing.assert_array_equal(np.random.standard_normal(4), g["short_next_draw"])
+
+
 def test_reconstruct_array_and_common_reinject():
     """One-launch array reconstruct == per-pulsar reconstruct_signal; re-injecting a common signal
     replaces it (correlated_noises.py:133-134)."""

@@ -150,3 +150,22 @@ def test_reference_import_paths():
         m = importlib.import_module(mod)
         for n in names:
             assert hasattr(m, n), (mod, n)
+
+
+def test_copy_array_noisedict_lookup_g8(golden):
+    """copy_array with the reference's shipped EPTA noisedict / custom_models (fixture G8): the name-keyed
+    init_noisedict branch, per-pulsar custom models, copied TOA attributes (fake_pta.py:76-147, 687-712)."""
+    from fakepta import fake_pta as fp
+    from tests.helpers import g8_inputs
+    psrs_0, nd, cm, g = g8_inputs(golden)
+    want = golden("g8_example_workflow.json")
+    np.random.seed(int(g["seed"]))
+    psrs = fp.copy_array(psrs_0, nd, cm)
+    assert [p.name for p in psrs] == list(g["names"])
+    np.testing.assert_array_equal(np.concatenate([p.freqs for p in psrs]), g["copied_freqs"])
+    for p in psrs:
+        # the final noisedict adds the GWB's keys (update_noisedict, correlated_noises.py:128-129)
+        assert p.noisedict == {k: v for k, v in want["noisedicts"][p.name].items() if not k.startswith("gw_common")}
+        assert p.Tspan == want["Tspan"][p.name]
+        assert p.custom_model == cm[p.name]
+        assert list(p.backends) == sorted(set(p.backend_flags))

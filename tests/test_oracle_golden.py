@@ -102,6 +102,27 @@ def test_common_correlated(golden, orf):
     assert_parity(rec, g[f"{orf}_reconstruct"], 1e-12)
 
 
+def test_common_components_not_len_f_g9(golden):
+    """components != len(f_psd) (correlated_noises.py:140-160): 30 modes of a 40-frequency grid are injected and
+    stored with the full f / psd; with 20 frequencies the loop fails at mode 20 (IndexError), as in fixture G9."""
+    g = golden("g9_common_components.npz")
+    offs, toas, freqs = g["offs"], g["toas"], g["freqs"]
+    P = len(offs) - 1
+    tl = [toas[offs[i]:offs[i + 1]] for i in range(P)]
+    fl = [freqs[offs[i]:offs[i + 1]] for i in range(P)]
+    L = O.mvn_factor(O.orf_hd(g["pos"]))
+    assert len(g["long_f"]) == 40 and len(g["long_psd"]) == 40 and int(g["long_nbin"]) == 30
+    res, fourier = O.common_synth_loop(tl, fl, g["long_f"], g["long_psd"], g["long_z"], L, 2.0, components=30)
+    np.testing.assert_allclose(fourier, g["long_fourier"], rtol=1e-12, atol=1e-12 * np.abs(fourier).max())
+    assert_parity(np.concatenate(res), g["long_residuals"], 1e-12)
+    rec = np.concatenate([O.reconstruct_loop(tl[i], fl[i], g["long_f"][:30], g["long_fourier"][i], 2.0)
+                          for i in range(P)])
+    assert_parity(rec, g["long_reconstruct"], 1e-12)
+    f20 = g["long_f"][:20]
+    with pytest.raises(IndexError, match=str(g["short_error"])):
+        O.common_synth_loop(tl, fl, f20, O.powerlaw(f20, -14.5, 13 / 3), g["short_z"], L, 0.0, components=30)
+
+
 def test_philox_known_answers():
     kat = [((0, 0, 0, 0), (0, 0), (0x6627e8d5, 0xe169c58d, 0xbc57ac4c, 0x9b00dbd8)),
            ((0xffffffff,) * 4, (0xffffffff,) * 2, (0x408f276d, 0x41c83b0e, 0xa20bc7c6, 0x6d5451fd)),

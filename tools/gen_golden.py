@@ -24,6 +24,20 @@ Fixture map:
   g7_ref_pulsars.pkl  4 Pulsar objects pickled by the reference (class fakepta.fake_pta.Pulsar)
   g7_ref_pulsars.npz  the reference's reconstruct_signal() on them, then its residuals after
                       np.random.seed(32) + add_red_noise (replace) + add_common_correlated_noise
+  g8_example_workflow.npz + g8_example_workflow.json
+                      examples/make_fake_array.py:31-47 with the reference's own shipped
+                      examples/simulated_data/{noisedict,custom_models}_*newsys_trim.json (copied here as
+                      data: g8_noisedict_dr2_newsys_trim.json, g8_custom_models_newsys_trim.json): copy_array
+                      of 26 stand-in multi-backend EPTA pulsars (the example's pickle is a private file),
+                      then make_ideal / add_white_noise / add_red_noise() / add_dm_noise() /
+                      add_chromatic_noise() with no kwargs (noisedict-driven), then the HD GWB
+  g9_common_components.npz
+                      add_common_correlated_noise with len(f_psd) != components
+                      (correlated_noises.py:142-160): 40 frequencies, components=30 (30 modes injected,
+                      psd/f stored with 40 entries); and 20 frequencies, components=30 (IndexError after
+                      the first 20 modes and one more draw pair)
+
+Run a subset with  python tools/gen_golden.py g8 g9
 """
 import json
 import os
@@ -303,16 +317,163 @@ def gen_g7(fp, cn):
     np.savez_compressed(os.path.join(OUT, "g7_ref_pulsars.npz"), **d)
 
 
+G8_ND = "g8_noisedict_dr2_newsys_trim.json"
+G8_CM = "g8_custom_models_newsys_trim.json"
+
+
+def g8_standin_arrays(noisedict, names, seed=2024):
+    """Inputs of the stand-in ENTERPRISE pulsars: per pulsar the backends its noisedict names (EPTA
+    multi-backend flags, e.g. 'EFF.P217.1380'), ragged per-backend observing campaigns on real-MJD epochs
+    (seconds), 1-2 sub-band TOAs per epoch at the flag's frequency +- 64 MHz, TOA errors 10^U(-7,-5.5), and
+    the sky position read from the J-name. Returns flat arrays + CSR offsets (all data, no objects)."""
+    rng = np.random.default_rng(seed)
+    day = 86400.0
+    toas, freqs, errs, flags, offs, theta, phi = [], [], [], [], [0], [], []
+    for name in names:
+        bks = sorted({k[len(name) + 1:-len("_efac")] for k in noisedict
+                      if k.startswith(name + "_") and k.endswith("_efac")})
+        sgn = 1.0 if name[5] == "+" else -1.0
+        dec = sgn * (int(name[6:8]) + int(name[8:10]) / 60.0)
+        theta.append(np.pi / 2 - np.pi / 180.0 * dec)
+        phi.append(2 * np.pi * (int(name[1:3]) + int(name[3:5]) / 60.0) / 24.0)
+        t, f, b = [], [], []
+        for bk in bks:
+            start = rng.uniform(50500.0, 56500.0)
+            end = min(59500.0, start + rng.uniform(900.0, 3000.0))
+            ep = np.arange(start, end, rng.uniform(25.0, 60.0))
+            ep = ep[rng.random(len(ep)) < 0.8]
+            ep = ep + rng.normal(0.0, 1.0, size=len(ep))
+            nsub = int(rng.integers(1, 3))
+            nominal = float(bk.split(".")[-1])
+            for j in range(nsub):
+                t.append(ep * day + 900.0 * j)
+                f.append(nominal + (0.0 if nsub == 1 else (-64.0 if j == 0 else 64.0)) + np.zeros(len(ep)))
+                b += [bk] * len(ep)
+        t = np.concatenate(t)
+        order = np.argsort(t, kind="stable")
+        toas.append(t[order])
+        freqs.append(np.concatenate(f)[order])
+        flags += list(np.array(b)[order])
+        errs.append(10 ** rng.uniform(-7.0, -5.5, size=len(t)))
+        offs.append(offs[-1] + len(t))
+    return dict(names=np.array(names), offs=np.array(offs, dtype=np.int64), toas=np.concatenate(toas),
+                freqs=np.concatenate(freqs), toaerrs=np.concatenate(errs), backend_flags=np.array(flags),
+                theta=np.array(theta), phi=np.array(phi))
+
+
+class _EnterprisePulsar:
+    """Stand-in for an enterprise.pulsar.Pulsar: exactly the attributes copy_array reads
+    (fake_pta.py:687-712)."""
+
+    def __init__(self, a, i):
+        lo, hi = a["offs"][i], a["offs"][i + 1]
+        self.name = str(a["names"][i])
+        self.toas = a["toas"][lo:hi].copy()
+        self.freqs = a["freqs"][lo:hi].copy()
+        self.toaerrs = a["toaerrs"][lo:hi].copy()
+        self.backend_flags = a["backend_flags"][lo:hi].copy()
+        self.residuals = np.zeros(hi - lo)
+        self.theta, self.phi = float(a["theta"][i]), float(a["phi"][i])
+        self.Mmat = np.stack([np.ones(hi - lo), self.toas - self.toas[0]], 1)
+        self.fitpars = ["Offset", "F0"]
+        self.pdist = (1.0, 0.2)
+        self.planetssb = None
+        self.pos_t = None
+
+
+def gen_g8(fp, cn):
+    import shutil
+    ex = os.path.join(ref_shim.REF, "examples", "simulated_data")
+    shutil.copyfile(os.path.join(ex, "noisedict_dr2_newsys_trim.json"), os.path.join(OUT, G8_ND))
+    shutil.copyfile(os.path.join(ex, "custom_models_newsys_trim.json"), os.path.join(OUT, G8_CM))
+    noisedict = json.load(open(os.path.join(OUT, G8_ND)))
+    custom_models = json.load(open(os.path.join(OUT, G8_CM)))
+    names = sorted(custom_models)
+    a = g8_standin_arrays(noisedict, names)
+    psrs_0 = [_EnterprisePulsar(a, i) for i in range(len(names))]
+    np.random.seed(8)
+    psrs = fp.copy_array(psrs_0, noisedict, custom_models)            # examples/make_fake_array.py:34
+    d = dict(a)
+    d["seed"] = np.array(8)
+    for p in psrs:                                                     # :37-43
+        p.make_ideal()
+        p.add_white_noise()
+        p.add_red_noise()
+        p.add_dm_noise()
+        p.add_chromatic_noise()
+    d["residuals_noise"] = np.concatenate([p.residuals for p in psrs])
+    cn.add_common_correlated_noise(psrs, log10_A=-15., gamma=13 / 3, orf="hd")   # :47
+    d["residuals"] = np.concatenate([p.residuals for p in psrs])
+    d["copied_freqs"] = np.concatenate([p.freqs for p in psrs])
+    models = {}
+    for i, p in enumerate(psrs):
+        models[p.name] = {}
+        for sig, sm in p.signal_model.items():
+            key = f"{i}_{sig}"
+            d[key + "_f"] = np.asarray(sm["f"], float)
+            d[key + "_psd"] = np.asarray(sm["psd"], float)
+            d[key + "_fourier"] = np.asarray(sm["fourier"], float)
+            d[key + "_reconstruct"] = p.reconstruct_signal([sig])
+            models[p.name][sig] = {"nbin": int(sm["nbin"]), "idx": float(sm["idx"]), "spectrum": sm["spectrum"]}
+    np.savez_compressed(os.path.join(OUT, "g8_example_workflow.npz"), **d)
+    with open(os.path.join(OUT, "g8_example_workflow.json"), "w") as fh:
+        json.dump({"noisedicts": {p.name: {k: float(v) for k, v in p.noisedict.items()} for p in psrs},
+                   "signal_models": models, "Tspan": {p.name: float(p.Tspan) for p in psrs},
+                   "source": "examples/make_fake_array.py:31-47 via tools/gen_golden.py gen_g8"},
+                  fh, indent=0, sort_keys=True)
+
+
+def gen_g9(fp, cn):
+    """add_common_correlated_noise when len(f_psd) != components (correlated_noises.py:118-160)."""
+    np.random.seed(9)
+    psrs = fp.make_fake_array(npsrs=8, Tobs=8, ntoas=90, gaps=True, toaerr=1e-7, isotropic=True,
+                              backends=["A.1400", "B.800"], custom_model={"RN": None, "DM": None, "Sv": None})
+    tspan = max(p.toas.max() for p in psrs) - min(p.toas.min() for p in psrs)
+    d = dict(offs=np.concatenate([[0], np.cumsum([len(p.toas) for p in psrs])]),
+             toas=np.concatenate([p.toas for p in psrs]), freqs=np.concatenate([p.freqs for p in psrs]))
+    d["pos"] = np.array([p.pos for p in psrs])
+    P = len(psrs)
+    f40 = np.arange(1, 41) / tspan
+    for p in psrs:
+        p.make_ideal()
+    z = _draw_record(lambda: cn.add_common_correlated_noise(psrs, orf="hd", components=30, f_psd=f40, log10_A=-14.5,
+                                                            gamma=13 / 3, idx=2), 2 * 30 * P)
+    d["long_z"] = z.reshape(30, 2, P)
+    sm = psrs[0].signal_model["gw_common"]
+    d["long_f"], d["long_psd"], d["long_nbin"] = sm["f"], sm["psd"], np.array(sm["nbin"])
+    d["long_fourier"] = np.array([p.signal_model["gw_common"]["fourier"] for p in psrs])
+    d["long_residuals"] = np.concatenate([p.residuals for p in psrs])
+    d["long_reconstruct"] = np.concatenate([p.reconstruct_signal(["gw_common"]) for p in psrs])
+    d["long_next_draw"] = np.random.standard_normal(4)
+    np.random.seed(19)
+    for p in psrs:
+        p.make_ideal()
+    f20 = np.arange(1, 21) / tspan
+    st = np.random.get_state()
+    try:
+        cn.add_common_correlated_noise(psrs, orf="hd", components=30, f_psd=f20, log10_A=-14.5, gamma=13 / 3)
+        raise AssertionError("reference accepted len(f_psd) < components")
+    except IndexError as e:
+        d["short_error"] = np.array(str(e))
+    st_after = np.random.get_state()
+    np.random.set_state(st)
+    d["short_z"] = np.random.standard_normal(2 * 21 * P).reshape(21, 2, P)
+    np.random.set_state(st_after)
+    d["short_residuals"] = np.concatenate([p.residuals for p in psrs])
+    d["short_fourier"] = np.array([p.signal_model["gw_common"]["fourier"] for p in psrs])
+    d["short_next_draw"] = np.random.standard_normal(4)
+    np.savez_compressed(os.path.join(OUT, "g9_common_components.npz"), **d)
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
     fp, cn, sp = ref_shim.load_reference()
-    gen_g1(sp)
-    gen_g2(fp)
-    gen_g3(fp, cn)
-    gen_g4(fp)
-    gen_g5()
-    gen_g6(fp)
-    gen_g7(fp, cn)
+    which = set(sys.argv[1:]) or {"g1", "g2", "g3", "g4", "g5", "g6", "g7", "g8", "g9"}
+    for key, fn in (("g1", lambda: gen_g1(sp)), ("g2", lambda: gen_g2(fp)), ("g3", lambda: gen_g3(fp, cn)),
+                    ("g4", lambda: gen_g4(fp)), ("g5", gen_g5), ("g6", lambda: gen_g6(fp)),
+                    ("g7", lambda: gen_g7(fp, cn)), ("g8", lambda: gen_g8(fp, cn)), ("g9", lambda: gen_g9(fp, cn))):
+        if key in which:
+            fn()
     for fn in sorted(os.listdir(OUT)):
         print(fn, os.path.getsize(os.path.join(OUT, fn)))
 
