@@ -13,10 +13,12 @@ nothing is copied back inside it. Weak scaling: rank g of G owns realizations (s
 rank 0. Strong scaling (the job is fixed); one step = the whole job.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3]
-    (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
+    (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N; run without a launcher,
+    --gpus N > 1 starts that launcher as a child process before anything touches a GPU)
 
-RCCL (torch.distributed backend "nccl") carries only the barrier, the max-over-ranks time and the
-checksum gather; the data path has no collective.
+One process per GPU. RCCL over xGMI (the library's own communicator, fpta_comm_*, on the kernels' HIP runtime;
+fakepta_amd.batch.RcclComm) carries only the barrier, the max-over-ranks time and the checksum gather; the data
+path has no collective. The rank processes never import torch (one HIP runtime per process).
 """
 import argparse
 import glob
@@ -54,8 +56,8 @@ def parse():
     ap.add_argument("--npsr", type=int, default=100)
     ap.add_argument("--ntoa", type=int, default=2000)
     ap.add_argument("--seed", type=int, default=1234)
-    ap.add_argument("--cpu-sample", type=int, default=8,
-                    help="realizations timed for the loop-faithful CPU baseline (0: skip both CPU legs)")
+    ap.add_argument("--cpu-sample", type=int, default=4,
+                    help="re-drawn realizations timed for the reference-faithful CPU baseline (0: skip both CPU legs)")
     ap.add_argument("--path", type=int, default=0, help="synthesis path: 0 auto, 1 direct, 2 MFMA, 3 VALU, 4 gridded")
     ap.add_argument("--grid-mfma", type=int, default=-1,
                     help="gridded path kernels on MFMA: bit 0 DFT, bit 1 interpolation (-1: library default)")
@@ -65,7 +67,9 @@ def parse():
                     help="FPTA_OPT_OVERLAP: 1 pipelined blocks (side stream), 0 one stream (-1: library default)")
     ap.add_argument("--exact-launches", type=int, default=5,
                     help="launches of the exact fused kernel (path 3) timed after the run for roofline_exact")
-    ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL on ROCm) or gloo (CPU rehearsal)")
+    ap.add_argument("--dist-backend", default="rccl", choices=("rccl", "gloo"),
+                    help="rccl: the library's RCCL communicator (one rank per GPU); gloo: torch.distributed on the "
+                         "CPU (rehearsal of several ranks on one card)")
     ap.add_argument("--traffic", default="",
                     help="PMC-derived HBM bytes per launch (profiles/*traffic.json, tools/collect_traffic.py); "
                          "default: the record matching the kernel and shape")
@@ -107,37 +111,51 @@ def cpu_model():
     return "unknown"
 
 
-def cpu_baseline_loop(sim, psrs, n_sample, seed):
-    """Oracle loop-faithful restatement (the reference's per-mode elementwise structure,
-    fake_pta.py:385-387 / correlated_noises.py:153-160), 1 thread, n_sample realizations."""
+def baseline_segments(sim):
+    """The bench layout as the reference's injectors see it: per-pulsar (f, psd) and the common signal's (f, psd, ORF)
+    (psd = amp^2 / df; the ORF = L L^T of the batch factor)."""
     from oracle import fakepta_oracle as O
-    P = len(psrs)
+    segs = []
+    for s in sim.segments:
+        if s["kind"] == 0:
+            df = np.diff(np.concatenate([np.zeros((s["f"].shape[0], 1)), s["f"]], 1), axis=1)
+            segs.append(dict(kind=0, f=s["f"], psd=s["amp"] ** 2 / df, idx=s["idx"]))
+        else:
+            segs.append(dict(kind=1, f=s["f"], psd=s["amp"] ** 2 / O.delta_f(s["f"]), idx=s["idx"],
+                             orf=s["L"] @ s["L"].T))
+    return segs
+
+
+def cpu_baseline_loop(toas_list, freqs_list, segs, n_sample, seed):
+    """n_sample re-drawn realizations with the reference's own operations at its cost, 1 thread
+    (oracle.redraw_loop: per mode elementwise passes, the stored signal's reconstruct subtracted before each re-draw
+    as fake_pta.py:266-267 / correlated_noises.py:133-134 do, an SVD of the ORF per multivariate_normal call). The
+    first realization (no stored signal yet) is not timed. Returns seconds per realization."""
+    from oracle import fakepta_oracle as O
+    rs = np.random.RandomState(seed)
+    res = [np.zeros(len(t)) for t in toas_list]
+    stored = {}
+    O.redraw_loop(toas_list, freqs_list, segs, res, stored, rs)
     t0 = time.perf_counter()
-    for r in range(n_sample):
-        rng = np.random.default_rng(seed + r)
-        res = [np.zeros(len(p.toas)) for p in psrs]
-        for s in sim.segments:
-            if s["kind"] == 0:
-                for p in range(P):
-                    nm = s["f"].shape[1]
-                    psd = s["amp"][p] ** 2 / O.delta_f(s["f"][p])
-                    coeffs = O.gp_coeffs_from_z(psd, rng.standard_normal(2 * nm))
-                    O.gp_synth_loop(psrs[p].toas, psrs[p].freqs, s["f"][p], coeffs, s["idx"], residuals=res[p])
-            else:
-                nm = len(s["f"])
-                psd = s["amp"] ** 2 / O.delta_f(s["f"])
-                z = rng.standard_normal((nm, 2, P))
-                out, _ = O.common_synth_loop([p.toas for p in psrs], [p.freqs for p in psrs], s["f"], psd, z,
-                                             s["L"], s["idx"])
-                for p in range(P):
-                    res[p] += out[p]
-    return time.perf_counter() - t0
+    for _ in range(n_sample):
+        O.redraw_loop(toas_list, freqs_list, segs, res, stored, rs)
+    return (time.perf_counter() - t0) / n_sample
+
+
+def blas_threads():
+    """Threads numpy's BLAS actually runs with (threadpoolctl), or None."""
+    try:
+        from threadpoolctl import threadpool_info
+        n = [i.get("num_threads") for i in threadpool_info() if i.get("user_api") == "blas"]
+        return max(n) if n else None
+    except Exception:
+        return None
 
 
 def cpu_baseline_vectorised(sim, psrs, n_real, seed):
-    """the vectorised F.A restatement on all the host threads BLAS is given
-    (OMP_NUM_THREADS): per pulsar the basis F [n_p x K_p] (built once per batch, as a CPU user would),
-    the draws, the ORF mix x = L z and one GEMM F @ A [K_p x n_real]."""
+    """the vectorised F.A restatement on the threads numpy's BLAS runs with: per pulsar the
+    basis F [n_p x K_p] (built once per batch, as a CPU user would), the draws, the ORF mix x = L z and one GEMM
+    F @ A [K_p x n_real]."""
     from oracle import fakepta_oracle as O
     P = len(psrs)
     rng = np.random.default_rng(seed)
@@ -165,22 +183,26 @@ def cpu_baseline_vectorised(sim, psrs, n_real, seed):
 
 def cpu_baseline(sim, psrs, n_sample, seed):
     n_toa = sim.n_toa
-    dt_loop = cpu_baseline_loop(sim, psrs, n_sample, seed)
+    segs = baseline_segments(sim)
+    dt_loop = cpu_baseline_loop([p.toas for p in psrs], [p.freqs for p in psrs], segs, n_sample, seed)
     threads = os.environ.get("OMP_NUM_THREADS", "")
     n_vec = 64
     dt_vec = cpu_baseline_vectorised(sim, psrs, n_vec, seed)
     while dt_vec < 2.0 and n_vec < 4096:  # grow the sample to a few seconds of CPU work
         n_vec *= 4
         dt_vec = cpu_baseline_vectorised(sim, psrs, n_vec, seed)
-    cores = int(threads) if threads.isdigit() else os.cpu_count()
-    vec = dict(value=n_toa * n_vec / dt_vec, unit="samples/s", cores=cores, kind="port",
+    used = blas_threads()
+    vec = dict(value=n_toa * n_vec / dt_vec, unit="samples/s", cores=used, kind="port",
                sample=f"{n_vec} realizations, vectorised F.A (numpy {np.__version__} BLAS GEMM per pulsar), "
-                      f"{dt_vec:.2f} s")
-    return dict(value=n_toa * n_sample / dt_loop, unit="samples/s", cores=1, kind="port",
-                sample=f"{n_sample} realizations of the bench array, oracle loop-faithful restatement "
-                       f"(per-mode elementwise numpy as fake_pta.py:385-387), 1 thread, {dt_loop:.2f} s",
+                      f"{dt_vec:.2f} s on {used} BLAS thread(s) (OMP_NUM_THREADS={threads or 'unset'}; the GPU "
+                      f"box's CPU share is 16 of its {os.cpu_count()} host CPUs)")
+    return dict(value=n_toa / dt_loop, unit="samples/s", cores=1, kind="port",
+                sample=f"{n_sample} re-drawn realizations of the bench array with the reference's operations "
+                       f"(oracle.redraw_loop: fake_pta.py:266-267 + 370-387, correlated_noises.py:133-134 + "
+                       f"146-160, SVD per multivariate_normal), 1 thread, {dt_loop:.2f} s per realization; "
+                       f"same-host ratio to the reference itself: profiles/r03_cpu_crosscheck.json",
                 cpu_model=cpu_model(), nproc=os.cpu_count(), omp_num_threads=threads or None,
-                vectorised_all_cores=vec)
+                vectorised_blas_threads=vec)
 
 
 def pmc_traffic(kernel, info, R, path_arg, layout=None):
@@ -251,22 +273,60 @@ def isolated_grid(ctx, capi, sim, seed, R, launches):
         ctx.set_option(capi.OPT_PROFILE, 0)
 
 
+def launch_ranks(n):
+    """--gpus N > 1 without a launcher: run this command under torchrun as N rank processes (a child process;
+    nothing here has touched a GPU) and return its exit status."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    print(f"bench.py: --gpus {n} without a launcher: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    return subprocess.call(cmd)
+
+
+def hip_runtimes_mapped():
+    """HIP runtime libraries mapped into this process (one expected: the library's ROCm 7.2 libamdhip64)."""
+    try:
+        with open("/proc/self/maps") as fh:
+            return sorted({line.split()[-1] for line in fh if "libamdhip64" in line})
+    except OSError:
+        return None
+
+
 def main():
     args = parse()
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
+    world = int(world_env or 1)
+    if world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but the launcher started {world} rank(s) (WORLD_SIZE)")
     refuse_debug_environment()
     from fakepta_amd import _capi
-    from fakepta_amd.batch import BatchSimulator, RealizationComm, shard_bounds, simulate_sharded
+    from fakepta_amd.batch import BatchSimulator, RcclComm, RealizationComm, shard_bounds, simulate_sharded
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    # one process per GPU; local ranks beyond the visible devices wrap (rehearsal of several ranks on one card
-    # with --dist-backend gloo; the driver's N-GPU runs have one rank per device)
-    ndev = max(1, _capi.device_count())
-    device = local % ndev
+    ndev = _capi.device_count()
+    if args.dist_backend == "rccl":
+        # one rank per GPU: a rank without its own device fails here instead of measuring fewer GPUs
+        if local >= ndev:
+            sys.exit(f"bench.py: rank with LOCAL_RANK {local} needs device {local}, but {ndev} device(s) are visible")
+        device = local
+    else:
+        # gloo rehearsal: several ranks may share a card (local ranks wrap over the visible devices)
+        device = local % max(ndev, 1)
     os.environ["FAKEPTA_AMD_DEVICE"] = str(device)  # the drop-in calls of build_array use the same card
-    comm = RealizationComm(backend=args.dist_backend, local_rank=device)
-    rank = comm.rank
     ctx = _capi.Context(device)
+    if args.dist_backend == "gloo":
+        comm = RealizationComm(backend="gloo", local_rank=device)
+    elif world > 1:
+        comm = RcclComm(ctx)
+    else:
+        comm = RealizationComm(world=1, rank=0, local_rank=device)  # one rank: no collective
+    rank = comm.rank
     psrs = build_array(args.npsr, args.ntoa, args.config)
     sim = BatchSimulator(psrs, white=False, ctx=ctx)
     info = ctx.batch_info()
@@ -318,9 +378,6 @@ def main():
         n_samples_total = info["n_toa"] * n_job * args.steps
 
     ctx.set_option(_capi.OPT_PROFILE, 0)
-    kstats = {name: ctx.kernel_stats(k) for name, k in
-              (("gen", _capi.K_GEN), ("mix", _capi.K_MIX), ("grid", _capi.K_GRID), ("synth", _capi.K_SYNTH),
-               ("white", _capi.K_WHITE))}
     value = n_samples_total / dt
     synth_avg_s = kernel_avg_s(ctx, _capi.K_SYNTH)
     gi = ctx.batch_grid_info()
@@ -411,7 +468,8 @@ def main():
             "roofline": roofline,
             "roofline_exact": roofline_exact,
             "pcie_inclusive": pcie,
-            "kernels_ms_per_step": {k: (v[1] / max(v[0], 1)) * (v[0] / max(args.steps, 1)) for k, v in kstats.items()},
+            "comm": {"backend": getattr(comm, "backend", "none") if world > 1 else "none (one rank)",
+                     "hip_runtimes_mapped": hip_runtimes_mapped()},
             "checksum": float(np.sum(sums[:, 1])),
             "n_checksums": int(len(sums)),
         }

@@ -75,6 +75,15 @@ _SIGS = [
     ("fpta_multi_set_white", _c_int, [_vp, _vp, _i64, _vp, _vp, _vp]),
     ("fpta_multi_set_option", _c_int, [_vp, _i32, _i64]),
     ("fpta_multi_synth", _c_int, [_vp, _u64, _i64, _i64, _i32, _vp]),
+    ("fpta_multi_set_gather", _c_int, [_vp, _i32]),
+    ("fpta_multi_last_gather", _c_int, [_vp]),
+    ("fpta_comm_unique_id", _c_int, [_vp]),
+    ("fpta_comm_init_rank", _c_int, [_ctx_p, _i32, _i32, _vp, ctypes.POINTER(_vp)]),
+    ("fpta_comm_destroy", _c_int, [_vp]),
+    ("fpta_comm_last_error", ctypes.c_char_p, [_vp]),
+    ("fpta_comm_size", _c_int, [_vp, ctypes.POINTER(_i32), ctypes.POINTER(_i32)]),
+    ("fpta_comm_max", _c_int, [_vp, ctypes.POINTER(_dbl)]),
+    ("fpta_comm_gather", _c_int, [_vp, _vp, _i64, _vp]),
 ]
 for _name, _res, _args in _SIGS:
     _fn = getattr(_lib, _name)
@@ -91,6 +100,8 @@ OPTIONS = (OPT_SYNTH_PATH, OPT_MFMA_MIN_REAL, OPT_PROFILE, OPT_ANCHOR, OPT_VALU_
            OPT_INTERP_LDS, OPT_GRID_COALESCE, OPT_INTERP_WS, OPT_SIDE_SPLIT)
 K_GEN, K_MIX, K_SYNTH, K_WHITE, K_DENSE, K_GRID = 0, 1, 2, 3, 4, 5
 BUILD_DEBUG = 1
+GATHER_AUTO, GATHER_RCCL, GATHER_HOST = 0, 1, 2
+COMM_ID_BYTES = 128
 
 
 def build_flags():
@@ -495,12 +506,73 @@ class MultiContext:
     def set_option(self, key, value):
         self._check(_lib.fpta_multi_set_option(self._h, int(key), int(value)), "fpta_multi_set_option")
 
+    def set_gather(self, mode):
+        """GATHER_AUTO (RCCL when the devices are distinct), GATHER_RCCL or GATHER_HOST (fpta_multi_set_gather)."""
+        self._check(_lib.fpta_multi_set_gather(self._h, int(mode)), "fpta_multi_set_gather")
+
+    def last_gather(self):
+        """The route the last synth_checksums took: GATHER_RCCL or GATHER_HOST (0 before any)."""
+        return int(_lib.fpta_multi_last_gather(self._h))
+
     def synth_checksums(self, seed, real0, n_real, batch=4096):
         """Per-realization (sum, sum of squares) of realizations real0 .. real0 + n_real - 1: [n_real, 2]."""
         out = np.empty((int(n_real), 2))
         self._check(_lib.fpta_multi_synth(self._h, int(seed) & 0xFFFFFFFFFFFFFFFF, int(real0), int(n_real),
                                           int(batch), _ptr(out)), "fpta_multi_synth")
         return out
+
+
+class Comm:
+    """RCCL communicator of one rank on one context (fpta_comm_*): the library's own RCCL on the kernels' HIP
+    runtime. Rank 0 makes the unique id (Comm.unique_id()); every rank passes it to Comm(ctx, nranks, rank, uid)."""
+
+    @staticmethod
+    def unique_id():
+        buf = ctypes.create_string_buffer(COMM_ID_BYTES)
+        rc = _lib.fpta_comm_unique_id(ctypes.cast(buf, _vp))
+        if rc != 0:
+            raise FptaError(f"fpta_comm_unique_id failed ({rc}): {_lib.fpta_last_error(None).decode()}")
+        return buf.raw
+
+    def __init__(self, ctx, nranks, rank, uid):
+        if len(uid) != COMM_ID_BYTES:
+            raise ValueError(f"RCCL unique id must be {COMM_ID_BYTES} bytes")
+        buf = ctypes.create_string_buffer(bytes(uid), COMM_ID_BYTES)
+        h = _vp()
+        rc = _lib.fpta_comm_init_rank(ctx._h, int(nranks), int(rank), ctypes.cast(buf, _vp), ctypes.byref(h))
+        if rc != 0:
+            raise FptaError(f"fpta_comm_init_rank(nranks={nranks}, rank={rank}) failed ({rc}): "
+                            f"{_lib.fpta_last_error(ctx._h).decode()}")
+        self._h = h
+        self.ctx = ctx  # the communicator runs on ctx's device and stream: keep it alive
+        self.nranks, self.rank = int(nranks), int(rank)
+
+    def _check(self, rc, what):
+        if rc != 0:
+            raise FptaError(f"{what} failed ({rc}): {_lib.fpta_comm_last_error(self._h).decode()}")
+
+    def max(self, x):
+        v = _dbl(float(x))
+        self._check(_lib.fpta_comm_max(self._h, ctypes.byref(v)), "fpta_comm_max")
+        return float(v.value)
+
+    def gather(self, arr):
+        """Rank 0: every rank's float64 `arr` (same shape on every rank) stacked in rank order; others: None."""
+        a = _f64(arr)
+        out = np.empty((self.nranks,) + a.shape) if self.rank == 0 else None
+        self._check(_lib.fpta_comm_gather(self._h, _ptr(a), a.size, _ptr(out)), "fpta_comm_gather")
+        return out
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _lib.fpta_comm_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 _default = {}

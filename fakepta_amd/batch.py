@@ -204,10 +204,12 @@ def shard_bounds(n_real, rank, world):
 
 
 class RealizationComm:
-    """torch.distributed plumbing of a realization-sharded job: one process per GPU launched by torchrun
-    (WORLD_SIZE / RANK / LOCAL_RANK from the environment), backend "nccl" (= RCCL over xGMI on ROCm) for
-    GPU ranks or "gloo" on CPU. The data path has no collective: only the timing barrier, a max-reduce of the
-    elapsed time and the gather of per-realization checksums to rank 0 go through it."""
+    """torch.distributed plumbing of a realization-sharded job: one process per rank launched by torchrun
+    (WORLD_SIZE / RANK / LOCAL_RANK from the environment), backend "gloo" (CPU tests, rehearsals of several ranks
+    on one card) or "nccl". GPU jobs use RcclComm instead: torch's "nccl" backend would bring torch's own HIP
+    runtime and RCCL (ROCm 7.0) into a process whose kernels run on the library's (ROCm 7.2). The data path has no
+    collective: only the timing barrier, a max-reduce of the elapsed time and the gather of per-realization
+    checksums to rank 0 go through it."""
 
     def __init__(self, backend="nccl", world=None, rank=None, local_rank=None):
         import os
@@ -267,6 +269,91 @@ class RealizationComm:
         self.dist = None
 
 
+def _exchange_unique_id(rank, world, addr, port, make_id, timeout):
+    """Rank 0 makes the RCCL unique id and serves it to ranks 1 .. world - 1 over one TCP socket at (addr, port);
+    the other ranks connect (retrying until `timeout`) and read its 128 bytes. Plain sockets: no torch import, so
+    the rank process maps one HIP runtime (the library's)."""
+    import socket
+    import time as _time
+    n = _capi.COMM_ID_BYTES
+    deadline = _time.monotonic() + timeout
+    if rank == 0:
+        uid = make_id()
+        with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as srv:
+            srv.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+            srv.bind((addr, port))
+            srv.listen(world)
+            for _ in range(world - 1):
+                srv.settimeout(max(deadline - _time.monotonic(), 0.1))
+                conn, _ = srv.accept()
+                with conn:
+                    conn.sendall(uid)
+        return uid
+    while True:
+        try:
+            with socket.create_connection((addr, port), timeout=5.0) as conn:
+                buf = b""
+                while len(buf) < n:
+                    chunk = conn.recv(n - len(buf))
+                    if not chunk:
+                        raise ConnectionError("rendezvous closed early")
+                    buf += chunk
+                return buf
+        except OSError:
+            if _time.monotonic() > deadline:
+                raise TimeoutError(f"rank {rank}: no RCCL rendezvous at {addr}:{port} within {timeout} s")
+            _time.sleep(0.2)
+
+
+class RcclComm:
+    """RCCL over xGMI for a realization-sharded job with one process per GPU, launched by
+    torchrun (WORLD_SIZE / RANK / MASTER_ADDR / MASTER_PORT from the environment). The communicator is the
+    library's own (fpta_comm_*: the system RCCL on the kernels' HIP runtime), on the rank's context and stream;
+    torch is never imported, so each rank maps one HIP runtime. Rank 0's 128-byte unique id reaches the others
+    over a TCP socket at (MASTER_ADDR, MASTER_PORT + 1) (torchrun's own store listens on MASTER_PORT;
+    FAKEPTA_AMD_RDZV_PORT overrides). Same interface as RealizationComm: barrier, max, gather_to_root, close."""
+
+    backend = "rccl"
+
+    def __init__(self, ctx, world=None, rank=None, addr=None, port=None, timeout=120.0):
+        import os
+        self.world = int(os.environ.get("WORLD_SIZE", "1")) if world is None else int(world)
+        self.rank = int(os.environ.get("RANK", "0")) if rank is None else int(rank)
+        self.local_rank = ctx.device
+        self.ctx = ctx
+        addr = addr or os.environ.get("MASTER_ADDR", "127.0.0.1")
+        if port is None:
+            port = int(os.environ.get("FAKEPTA_AMD_RDZV_PORT", int(os.environ.get("MASTER_PORT", "29500")) + 1))
+        uid = _exchange_unique_id(self.rank, self.world, addr, int(port), _capi.Comm.unique_id, timeout)
+        self.comm = _capi.Comm(ctx, self.world, self.rank, uid)
+
+    def barrier(self):
+        self.comm.max(0.0)
+
+    def max(self, x):
+        """max over ranks of a float (the job time is the slowest rank's)."""
+        return self.comm.max(x)
+
+    def gather_to_root(self, arr, rows_per_rank=None):
+        """As RealizationComm.gather_to_root: rank 0 gets every rank's rows in rank order (padded to the largest
+        count for the collective, trimmed here), the other ranks None."""
+        arr = np.ascontiguousarray(arr, dtype=np.float64)
+        if rows_per_rank is None:
+            rows_per_rank = [arr.shape[0]] * self.world
+        n_max = max(rows_per_rank)
+        pad = np.zeros((n_max,) + arr.shape[1:])
+        pad[:arr.shape[0]] = arr
+        got = self.comm.gather(pad)
+        if got is None:
+            return None
+        return np.concatenate([got[g, :n] for g, n in enumerate(rows_per_rank)])
+
+    def close(self):
+        if getattr(self, "comm", None) is not None:
+            self.comm.close()
+            self.comm = None
+
+
 def simulate_sharded(sim, n_real, seed=0, real0=0, batch=4096, comm=None, on_batch=None):
     """Realizations real0 .. real0 + n_real - 1 of `sim`'s noise model over every rank of `comm`.
 
@@ -279,7 +366,7 @@ def simulate_sharded(sim, n_real, seed=0, real0=0, batch=4096, comm=None, on_bat
     the global index), which tests/test_dist_gloo.py and tests/test_gpu_c3.py check.
 
     sim: BatchSimulator (or any object with synth(n, seed=, real0=, to_host=False) and checksums()).
-    comm: RealizationComm (default: a single-rank job)."""
+    comm: RcclComm (GPU ranks) or RealizationComm (gloo; default: a single-rank job)."""
     comm = comm if comm is not None else RealizationComm(world=1, rank=0, local_rank=0)
     G = comm.world
     lo, hi = shard_bounds(n_real, comm.rank, G)

@@ -246,6 +246,35 @@ int fpta_multi_set_white(fpta_multi* m, const double* sigma, int64_t n_blocks,
 int fpta_multi_set_option(fpta_multi* m, int32_t key, int64_t value);
 int fpta_multi_synth(fpta_multi* m, uint64_t seed, int64_t real0, int64_t n_real, int32_t batch,
                      double* checksums_out);
+/* How fpta_multi_synth brings the checksums to the host: FPTA_GATHER_RCCL keeps each device's
+ * shard on the device and gathers them to device 0 with one ncclGather over xGMI (communicators from
+ * ncclCommInitAll over the listed devices, made on first use; the devices must be distinct);
+ * FPTA_GATHER_HOST copies each device's checksums into pinned host staging; FPTA_GATHER_AUTO (default) takes
+ * RCCL when the devices are distinct. fpta_multi_last_gather: the route the last fpta_multi_synth took. */
+#define FPTA_GATHER_AUTO 0
+#define FPTA_GATHER_RCCL 1
+#define FPTA_GATHER_HOST 2
+int fpta_multi_set_gather(fpta_multi* m, int32_t mode);
+int fpta_multi_last_gather(const fpta_multi* m);
+
+/* ------------------------------------------------------------------ one process per GPU: RCCL
+ * The library's own RCCL (ROCm 7.2, the same HIP runtime as the kernels) for realization-sharded jobs with one
+ * process per GPU (fakepta_amd.batch.RcclComm; the reference loop that shards: correlated_noises.py:153-160).
+ * Rank 0 makes the 128-byte unique id (fpta_comm_unique_id) and hands it to the other ranks out of band; every
+ * rank then calls fpta_comm_init_rank on its context. Collectives run on the context's stream after all work
+ * queued there, and return when their result is on the host. Only the job barrier / max of the elapsed time and
+ * the checksum gather go through them: the data path has no collective. */
+typedef struct fpta_comm fpta_comm;
+#define FPTA_COMM_ID_BYTES 128
+int fpta_comm_unique_id(void* id);
+int fpta_comm_init_rank(fpta_ctx* ctx, int32_t nranks, int32_t rank, const void* id, fpta_comm** out);
+int fpta_comm_destroy(fpta_comm* comm);
+const char* fpta_comm_last_error(const fpta_comm* comm);
+int fpta_comm_size(const fpta_comm* comm, int32_t* nranks, int32_t* rank);
+/* *value (host) <- max over ranks of *value. Also the barrier of a timed region. */
+int fpta_comm_max(fpta_comm* comm, double* value);
+/* Every rank sends `count` doubles (host); rank 0 receives nranks * count, in rank order, into recv (host). */
+int fpta_comm_gather(fpta_comm* comm, const double* send, int64_t count, double* recv);
 
 /* ------------------------------------------------------------------ tuning / profiling */
 #define FPTA_OPT_SYNTH_PATH 1     /* 0 auto, 1 direct (sincos per basis element), 2 fp64 MFMA, 3 fp64 VALU fused,

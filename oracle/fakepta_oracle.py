@@ -222,6 +222,57 @@ def common_synth_loop(toas_list, freqs_list, f, psd, z, L, idx, freqf=1400.0, co
     return res, fourier
 
 
+def redraw_loop(toas_list, freqs_list, segs, residuals, stored, rs, freqf=1400.0):
+    """One re-drawn realization of an array's noise model with the reference's own operations, in its order and at
+    its cost (the CPU baseline of SURVEY.md §8(d)(i)):
+      * per pulsar, per per-pulsar GP (fake_pta.py:266-267, 370-387): residuals -= reconstruct_signal of the stored
+        coefficients (:538-545); coeffs = normal(0, sqrt(repeat(psd, 2))); two elementwise passes per mode, each
+        recomputing (freqf / nu)**idx;
+      * per common GP (correlated_noises.py:133-134, 146-160): residuals -= reconstruct_signal on every pulsar; per
+        mode two multivariate_normal draws (each factors the ORF by SVD, numpy's method) and two elementwise passes
+        per pulsar.
+    segs: dicts kind (0 per pulsar: f, psd [P, N]; 1 common: f, psd [N], orf [P, P]), idx. residuals: list of
+    per-pulsar arrays (updated in place). stored: {(segment, pulsar): fourier [2, N]} of the previous realization
+    (updated in place; empty on the first call). rs: numpy.random.RandomState (the reference's legacy stream)."""
+    P = len(toas_list)
+    for p in range(P):
+        toas, freqs, res = toas_list[p], freqs_list[p], residuals[p]
+        for si, sg in enumerate(segs):
+            if sg["kind"] != 0:
+                continue
+            f, psd, idx = sg["f"][p], sg["psd"][p], sg["idx"]
+            if (si, p) in stored:
+                res -= reconstruct_loop(toas, freqs, f, stored[(si, p)], idx, freqf)
+            df = delta_f(f)
+            psd2 = np.repeat(psd, 2)
+            coeffs = rs.normal(loc=0., scale=np.sqrt(psd2))
+            stored[(si, p)] = np.vstack((coeffs[::2] / df ** 0.5, coeffs[1::2] / df ** 0.5))
+            mask = np.ones(len(toas), dtype=bool)  # backend=None: an all-true mask, indexed as at :386-387
+            for i in range(len(f)):
+                res[mask] += (freqf / freqs) ** idx * df[i] ** 0.5 * coeffs[2 * i] * np.cos(2 * np.pi * f[i] * toas[mask])
+                res[mask] += (freqf / freqs) ** idx * df[i] ** 0.5 * coeffs[2 * i + 1] * np.sin(2 * np.pi * f[i] * toas[mask])
+    for si, sg in enumerate(segs):
+        if sg["kind"] != 1:
+            continue
+        f, psd, idx, orf = sg["f"], sg["psd"], sg["idx"], sg["orf"]
+        for p in range(P):
+            if (si, p) in stored:
+                residuals[p] -= reconstruct_loop(toas_list[p], freqs_list[p], f, stored[(si, p)], idx, freqf)
+            stored[(si, p)] = np.zeros((2, len(f)))
+        df = delta_f(f)
+        coeffs = np.sqrt(np.repeat(psd, 2))
+        for i in range(len(f)):
+            x_sin = rs.multivariate_normal(mean=np.zeros(P), cov=orf)
+            x_cos = rs.multivariate_normal(mean=np.zeros(P), cov=orf)
+            for n in range(P):
+                stored[(si, n)][0, i] = x_cos[n] * coeffs[2 * i] / df[i] ** 0.5
+                stored[(si, n)][1, i] = x_sin[n] * coeffs[2 * i + 1] / df[i] ** 0.5
+                t, nu = toas_list[n], freqs_list[n]
+                residuals[n] += x_cos[n] * (freqf / nu) ** idx * df[i] ** 0.5 * coeffs[2 * i] * np.cos(2 * np.pi * f[i] * t)
+                residuals[n] += x_sin[n] * (freqf / nu) ** idx * df[i] ** 0.5 * coeffs[2 * i + 1] * np.sin(2 * np.pi * f[i] * t)
+    return residuals
+
+
 # ----------------------------------------------------------------------------- white noise / ECORR
 
 def white_sigma(toaerrs, backend_flags, efac, log10_tnequad):

@@ -1,5 +1,7 @@
 """Host-side logic of the drop-in package against the reference's fixtures (CPU only:
 nothing here launches a kernel)."""
+import os
+
 import numpy as np
 import pytest
 
@@ -169,3 +171,42 @@ def test_copy_array_noisedict_lookup_g8(golden):
         assert p.Tspan == want["Tspan"][p.name]
         assert p.custom_model == cm[p.name]
         assert list(p.backends) == sorted(set(p.backend_flags))
+
+
+def test_rccl_unique_id_rendezvous_threads():
+    """RcclComm's rendezvous (fakepta_amd.batch._exchange_unique_id): rank 0 serves its 128-byte id to every other
+    rank over one TCP socket; ranks that start before the server retry. Four ranks as threads, no GPU."""
+    import socket
+    import threading
+    import time
+    from fakepta_amd.batch import _exchange_unique_id
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    uid = bytes(range(128))
+    got = {}
+
+    def run(rank):
+        if rank == 0:
+            time.sleep(0.5)  # the clients start first and retry
+        got[rank] = _exchange_unique_id(rank, 4, "127.0.0.1", port, lambda: uid, timeout=20.0)
+
+    ts = [threading.Thread(target=run, args=(r,)) for r in range(4)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(30)
+    assert got == {r: uid for r in range(4)}
+
+
+def test_bench_refuses_world_size_mismatch():
+    """bench.py --gpus N under a launcher that started a different number of ranks exits non-zero before any GPU
+    call (the driver's scaling runs cannot silently measure a different N)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if not k.startswith("FPTA_")}
+    env.update(WORLD_SIZE="3", RANK="0", LOCAL_RANK="0")
+    res = subprocess.run([sys.executable, "bench.py", "--gpus", "2"], cwd=root, env=env, capture_output=True,
+                         text=True, timeout=60)
+    assert res.returncode != 0 and "WORLD_SIZE" in res.stderr

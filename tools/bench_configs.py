@@ -7,7 +7,9 @@ c1  make_fake_array(25 psr, Tobs 10, ntoas 1000, gaps, RN30) drop-in latency, se
 c3  100-psr HD GWB30 only (K = 60), realizations streamed in batches of 4096, checksums only
 c4  1000 psr x 10k TOAs, HD GWB100 (K = 200), 1000x1000 ORF factor, R = 256
 c5  100 psr, RN30 + DM100 + Sv100 + HD30 + monopole30 + dipole30 + white + ECORR (K = 640), R = 1024
-Prints one JSON line per config: samples/s end-to-end, and per-kernel HIP-event times.
+Prints one JSON line per config: samples/s end-to-end (pipelined, no per-kernel events) and per-kernel-class
+HIP-event times of a one-stream rerun (isolated launch durations; the rocprofv3 statistics under profiles/ are the
+per-kernel record).
 """
 import argparse
 import json
@@ -28,19 +30,34 @@ def kernel_times(ctx, capi, steps):
 
 
 def timed(ctx, capi, fn, steps, warmup=2):
+    """Wall time of `steps` calls of fn (the shipped pipelined configuration, no per-kernel events)."""
     for _ in range(warmup):
         fn(0)
     ctx.synchronize()
-    ctx.set_option(capi.OPT_PROFILE, 1)
-    ctx.reset_stats()
     t0 = time.perf_counter()
     for s in range(steps):
         fn(s + warmup)
     ctx.synchronize()
-    dt = time.perf_counter() - t0
-    kt = kernel_times(ctx, capi, steps)
-    ctx.set_option(capi.OPT_PROFILE, 0)
-    return dt, kt
+    return time.perf_counter() - t0
+
+
+def isolated(ctx, capi, fn, steps, first=1000):
+    """Per-kernel-class HIP-event times per step with ONE stream (FPTA_OPT_OVERLAP 0), after the timed run: the
+    launches are serial there, so the intervals are launch durations (in the pipelined run they overlap and are
+    not). The judged per-kernel figures are the rocprofv3 kernel statistics under profiles/."""
+    ctx.set_option(capi.OPT_OVERLAP, 0)
+    try:
+        fn(first)
+        ctx.synchronize()
+        ctx.set_option(capi.OPT_PROFILE, 1)
+        ctx.reset_stats()
+        for s in range(steps):
+            fn(first + 1 + s)
+        ctx.synchronize()
+        return kernel_times(ctx, capi, steps)
+    finally:
+        ctx.set_option(capi.OPT_PROFILE, 0)
+        ctx.set_option(capi.OPT_OVERLAP, 1)
 
 
 def c1():
@@ -84,13 +101,16 @@ def c3(total):
         n = min(B, total - (s % nb) * B)
         ctx.batch_synth(1234, (s % nb) * B, n, to_host=False)
 
-    dt, kt = timed(ctx, _capi, step, nb, warmup=1)
+    dt = timed(ctx, _capi, step, nb, warmup=1)
     sums = ctx.batch_checksums()
     info = ctx.batch_info()
+    kt = isolated(ctx, _capi, step, 3)
     del cn
     return dict(config="c3", K=info["K"], realizations=total, batch=B, wall_s=dt, path=ctx.batch_grid_info()["last_path"],
-                samples_per_s=info["n_toa"] * total / dt, kernels_ms_per_batch={k: v for k, v in kt.items()},
-                last_checksum=float(sums[:, 1].sum()))
+                samples_per_s=info["n_toa"] * total / dt, isolated_kernels_ms_per_batch=kt,
+                last_checksum=float(sums[:, 1].sum()),
+                note="per-batch device-resident blocks with a full checksum pass (bench.py --config c3 is the "
+                     "sharded job with fused checksums)")
 
 
 def c4():
@@ -115,15 +135,12 @@ def c4():
     amp = np.sqrt(O.powerlaw(f, -15.0, 13 / 3) * O.delta_f(f))
     ctx.batch_set_toas(offs, toas, nu)
     ctx.batch_add_signal(1, f, amp, idx=0.0, L=L)
-    dt, kt = timed(ctx, _capi, lambda s: ctx.batch_synth(7, s * R, R, to_host=False), 5, warmup=1)
-    # kernel times with one stream (pipelined blocks share the CUs, so their HIP-event times overlap)
-    ctx.set_option(_capi.OPT_OVERLAP, 0)
-    _, kt1 = timed(ctx, _capi, lambda s: ctx.batch_synth(7, (s + 10) * R, R, to_host=False), 3, warmup=1)
-    ctx.set_option(_capi.OPT_OVERLAP, 1)
-    kt = dict(kt, isolated=kt1)
+    dt = timed(ctx, _capi, lambda s: ctx.batch_synth(7, s * R, R, to_host=False), 5, warmup=1)
+    kt1 = isolated(ctx, _capi, lambda s: ctx.batch_synth(7, s * R, R, to_host=False), 3)
     flops = 2.0 * 2 * N * P * n_p * R
     return dict(config="c4", K=2 * N, n_toa=P * n_p, realizations=R, ms_per_step=dt / 5 * 1e3,
-                samples_per_s=P * n_p * R * 5 / dt, kernels_ms_per_step=kt, path=ctx.batch_grid_info()["last_path"],
+                samples_per_s=P * n_p * R * 5 / dt, isolated_kernels_ms_per_step=kt1,
+                path=ctx.batch_grid_info()["last_path"],
                 synth_direct_equiv_tflops=flops / ((kt1["synth"] + kt1["grid"]) / 1e3) / 1e12,
                 mix_factor="cholesky" if np.all(np.triu(L, 1) == 0) else "svd",
                 mix_ms_isolated=kt1["mix"],
@@ -156,10 +173,12 @@ def c5():
     cn.add_common_correlated_noise(psrs, orf="dipole", name="eph", log10_A=-15.0, gamma=4.0)
     sim = BatchSimulator(psrs, white=True, ecorr=True, ctx=ctx)
     R = 1024
-    dt, kt = timed(ctx, _capi, lambda s: ctx.batch_synth(9, s * R, R, to_host=False), 10)
+    dt = timed(ctx, _capi, lambda s: ctx.batch_synth(9, s * R, R, to_host=False), 10)
     info = ctx.batch_info()
+    kt = isolated(ctx, _capi, lambda s: ctx.batch_synth(9, s * R, R, to_host=False), 3)
     return dict(config="c5", K=info["K"], n_toa=info["n_toa"], realizations=R, ms_per_step=dt / 10 * 1e3,
-                samples_per_s=info["n_toa"] * R * 10 / dt, kernels_ms_per_step=kt,
+                samples_per_s=info["n_toa"] * R * 10 / dt, isolated_kernels_ms_per_step=kt,
+                step_ms_per_gb_written=dt / 10 * 1e3 / (8.0 * info["n_toa"] * R / 1e9),
                 synth_direct_equiv_tflops=2.0 * info["K"] * info["n_toa"] * R / ((kt["synth"] + kt["grid"]) / 1e3) / 1e12,
                 path=ctx.batch_grid_info()["last_path"], n_ecorr_blocks=len(sim.blocks))
 
