@@ -191,6 +191,13 @@ struct fpta_ctx {
   int overlap = 1;
   int interp_ws = 1;      // gridded interpolation on the warp-specialised kernel (FPTA_OPT_INTERP_WS)
   int grid_coalesce = 1;  // gridded path: signals sharing w0 and the chromatic weight share one grid (FPTA_OPT_GRID_COALESCE)
+  int gen_mix = 1;       // common signals of 64..256 pulsars: draws and ORF mixing in one kernel (k_gen_mix,
+                         // FPTA_OPT_GEN_MIX); 0 k_gen into zbuf, then k_mix_mfma
+  int dft_gen = 1;       // gridded path: grid signals with a per-pulsar member draw their coefficients inside the DFT
+                         // (k_grid_dft_gen, FPTA_OPT_DFT_GEN): no k_gen launch, no coefficient round trip for them
+  bool gen_fused = false;  // the current block runs k_grid_dft_gen for those grid signals (set by batch_common)
+  int64_t blk_real0 = 0;   // the current block's first realization and Philox key (k_grid_dft_gen draws)
+  uint32_t blk_k0 = 0, blk_k1 = 0;
   int interp_lds = 0;    // gridded interpolation with the grid rows staged in LDS where the plan allows (measured
                          // slower on C2: 0.745 vs 0.67 ms, profiles/r02g_*; kept as an option)
   hipStream_t side = nullptr;
@@ -492,6 +499,17 @@ int wait_coef_all(fpta_ctx* c) {
   return FPTA_OK;
 }
 
+// Grid signal g of L draws inside its DFT (k_grid_dft_gen) in a gen_fused block: it has a per-pulsar member, at most
+// kDftGenTerms members and a coefficient tile that fits the kernel's LDS.
+bool grid_gen_fused(const fpta_ctx* c, const Layout& L, size_t g) {
+  if (!c->gen_fused || !L.grid.built || !L.grid.ok || g >= L.grid.members.size()) return false;
+  const std::vector<int32_t>& m = L.grid.members[g];
+  if (m.size() > (size_t)kDftGenTerms || 2 * L.grid.segs[g]->ntq > 512) return false;
+  for (int32_t i : m)
+    if (L.segs[i]->d.kind == 0) return true;
+  return false;
+}
+
 // merge: the gridded plan of L coalesces signals (GridPlan::members): after the last member of a grid signal is
 // drawn, k_coef_merge adds the other members' columns into the anchor's. coef_host (optional, with merge): the
 // per-signal coefficients [P][K][R] are downloaded before any merge and *coef_done is set.
@@ -546,9 +564,18 @@ int run_coefficients(fpta_ctx* c, Layout& L, uint64_t seed, int64_t real0, int32
   // anchor excluded) does the same: the sums then run in k_coef_merge's order, bit for bit. Not when the
   // per-signal coefficients are downloaded (they are taken before any merge) or mixed draws are returned.
   const bool mfma_mix = P >= kMixTiledMinP && R_pad % 128 == 0 && c->mix_mfma;
+  // members of grid signals that draw inside their DFT (k_grid_dft_gen): per-pulsar members are not drawn here, and
+  // the common members' mixed coefficients stay in their own columns (the DFT adds them in the merge order)
+  std::vector<char> in_fused(L.segs.size(), 0), fused_g(G.members.size(), 0);
+  for (size_t g = 0; g < G.members.size(); ++g)
+    if (grid_gen_fused(c, L, g)) {
+      fused_g[g] = 1;
+      for (int32_t i : G.members[g]) in_fused[i] = 1;
+    }
   std::vector<int32_t> fuse_into(L.segs.size(), -1);
   if (merge && !defer && mfma_mix && !x_out)
     for (size_t g = 0; g < G.members.size(); ++g) {
+      if (fused_g[g]) continue;
       bool prefix = true;
       for (int32_t i : G.members[g]) {
         if (i == G.anchor[g]) continue;
@@ -605,6 +632,12 @@ int run_coefficients(fpta_ctx* c, Layout& L, uint64_t seed, int64_t real0, int32
   for (size_t i = 0; i < L.segs.size(); ++i) {
     const SegDesc& d = L.segs[i]->d;
     hipStream_t si = stream_of(group_of[i]);  // side2 only for members of split_g (kind 0: no mixing below)
+    if (in_fused[i] && d.kind == 0) continue;  // drawn inside its grid signal's DFT
+    if (d.kind == 1 && c->gen_mix && mfma_mix && !zin && !x_out && fuse_into[i] < 0 && P <= kGenMixMaxP) {
+      KTimer kt(c, FPTA_K_MIX, st);  // draws + mixing in one kernel, into the signal's own columns
+      HIPCHK(c, launch_gen_mix(st, d, (int32_t)i, P, R, R_pad, real0, k0, k1, c->coef.as<double>(), L.K),
+             "k_gen_mix launch");
+    } else {
     {
       KTimer kt(c, FPTA_K_GEN, si);
       HIPCHK(c,
@@ -625,9 +658,10 @@ int run_coefficients(fpta_ctx* c, Layout& L, uint64_t seed, int64_t real0, int32
         HIPCHK(c, launch_mix(st, d, P, R_pad, c->zbuf.as<double>(), c->coef.as<double>(), L.K, x_out),
                "k_mix launch");
     }
+    }
     if (merge && !defer)
       for (size_t g = 0; g < G.members.size(); ++g)
-        if (G.members[g].size() > 1 && G.last[g] == (int32_t)i) {
+        if (!fused_g[g] && G.members[g].size() > 1 && G.last[g] == (int32_t)i) {
           int rc = merge_group(g);
           if (rc) return rc;
         }
@@ -640,7 +674,7 @@ int run_coefficients(fpta_ctx* c, Layout& L, uint64_t seed, int64_t real0, int32
            "coef download");
     if (coef_done) *coef_done = true;
     for (size_t g = 0; g < G.members.size(); ++g)
-      if (G.members[g].size() > 1) {
+      if (!fused_g[g] && G.members[g].size() > 1) {
         int rc = merge_group(g);
         if (rc) return rc;
       }
@@ -1133,32 +1167,66 @@ int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad, bool pipe = fa
     const bool early_free = c->coef_side && !c->coef_copy_pending;
     const int32_t split = pipe && c->split_g < gsegs.n ? c->split_g : -1;
     c->split_g = -1;
+    // the DFTs of a set of grid signals on one stream: each k_grid_dft_gen signal its own launch, the others in one
+    // k_grid_dft_mfma / k_grid_dft launch
+    auto dfts = [&](hipStream_t sd, const std::vector<int32_t>& sigs) -> int {
+      GridSegs rest{};
+      for (int32_t s : sigs) {
+        if (!grid_gen_fused(c, L, (size_t)s)) {
+          rest.s[rest.n++] = gsegs.s[s];
+          continue;
+        }
+        DftGenArgs d{};
+        d.g = gsegs.s[s];
+        std::vector<int32_t> order{G.anchor[s]};  // the merge order: anchor, then the others in layout order
+        for (int32_t i : G.members[s])
+          if (i != G.anchor[s]) order.push_back(i);
+        for (int32_t i : order) {
+          const SegDesc& sd2 = L.segs[i]->d;
+          d.term_kind[d.n_terms] = sd2.kind;
+          d.term_seg[d.n_terms] = i;
+          d.term_nm[d.n_terms] = sd2.nm;
+          d.term_col0[d.n_terms] = sd2.col0;
+          d.term_amp[d.n_terms] = sd2.amp;
+          ++d.n_terms;
+        }
+        d.coef = a.coef;
+        d.P = L.P;
+        d.K = a.K;
+        d.R_pad = R_pad;
+        d.n_real = a.n_real;
+        d.real0 = c->blk_real0;
+        d.k0 = c->blk_k0;
+        d.k1 = c->blk_k1;
+        HIPCHK(c, launch_grid_dft_gen(sd, d), "k_grid_dft_gen launch");
+      }
+      if (rest.n)
+        HIPCHK(c,
+               (c->grid_mfma & 1) ? launch_grid_dft_mfma(sd, rest, L.P, a.coef, a.K, R_pad)
+                                  : launch_grid_dft(sd, rest, L.P, a.coef, a.K, R_pad),
+               "k_grid_dft launch");
+      return FPTA_OK;
+    };
+    std::vector<int32_t> all_sigs(gsegs.n);
+    for (int32_t s = 0; s < gsegs.n; ++s) all_sigs[s] = s;
     if (pipe && split >= 0) {
       // the split signal's DFT on side2 (after its draws there), the others' on side
-      GridSegs one{}, rest{};
-      for (int32_t s = 0; s < gsegs.n; ++s) {
-        GridSegs& dst = s == split ? one : rest;
-        dst.s[dst.n++] = gsegs.s[s];
-      }
+      std::vector<int32_t> rest_sigs;
+      for (int32_t s = 0; s < gsegs.n; ++s)
+        if (s != split) rest_sigs.push_back(s);
       {
         if (c->gfree_set[gi]) HIPCHK(c, hipStreamWaitEvent(c->side2, c->ev_gfree[gi], 0), "grid buffer wait");
         KTimer kt2(c, FPTA_K_GRID, c->side2);
-        HIPCHK(c,
-               (c->grid_mfma & 1) ? launch_grid_dft_mfma(c->side2, one, L.P, a.coef, a.K, R_pad)
-                                  : launch_grid_dft(c->side2, one, L.P, a.coef, a.K, R_pad),
-               "k_grid_dft launch");
+        int rc = dfts(c->side2, {split});
+        if (rc) return rc;
       }
       HIPCHK(c, hipEventRecord(c->ev_gready2, c->side2), "event record");
       c->s2done_set = true;
-      HIPCHK(c,
-             (c->grid_mfma & 1) ? launch_grid_dft_mfma(c->side, rest, L.P, a.coef, a.K, R_pad)
-                                : launch_grid_dft(c->side, rest, L.P, a.coef, a.K, R_pad),
-             "k_grid_dft launch");
+      int rc = dfts(c->side, rest_sigs);
+      if (rc) return rc;
     } else if (pipe) {
-      HIPCHK(c,
-             (c->grid_mfma & 1) ? launch_grid_dft_mfma(c->side, gsegs, L.P, a.coef, a.K, R_pad)
-                                : launch_grid_dft(c->side, gsegs, L.P, a.coef, a.K, R_pad),
-             "k_grid_dft launch");
+      int rc = dfts(c->side, all_sigs);
+      if (rc) return rc;
     } else if (c->coef_side) {
       // one DFT launch per grid signal, each after that signal's draws (and merge) only (side stream); in the
       // order their draws complete
@@ -1178,10 +1246,8 @@ int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad, bool pipe = fa
       }
       c->coef_side = false;
     } else {
-      HIPCHK(c,
-             (c->grid_mfma & 1) ? launch_grid_dft_mfma(c->stream, gsegs, L.P, a.coef, a.K, R_pad)
-                                : launch_grid_dft(c->stream, gsegs, L.P, a.coef, a.K, R_pad),
-             "k_grid_dft launch");
+      int rc = dfts(c->stream, all_sigs);
+      if (rc) return rc;
     }
     if (pipe) {
       HIPCHK(c, hipEventRecord(c->ev_gready, c->side), "event record");
@@ -1598,6 +1664,12 @@ int fpta_set_option(fpta_ctx* c, int32_t key, int64_t value) {
     case FPTA_OPT_INTERP_LDS:
       c->interp_lds = value ? 1 : 0;
       return FPTA_OK;
+    case FPTA_OPT_DFT_GEN:
+      c->dft_gen = value ? 1 : 0;
+      return FPTA_OK;
+    case FPTA_OPT_GEN_MIX:
+      c->gen_mix = value ? 1 : 0;
+      return FPTA_OK;
     case FPTA_OPT_GRID_COALESCE:
       c->grid_coalesce = value ? 1 : 0;
       c->batch.grid.clear();
@@ -1645,6 +1717,8 @@ int fpta_get_option(fpta_ctx* c, int32_t key, int64_t* value) {
     case FPTA_OPT_GRID_COALESCE: *value = c->grid_coalesce; return FPTA_OK;
     case FPTA_OPT_INTERP_WS: *value = c->interp_ws; return FPTA_OK;
     case FPTA_OPT_SIDE_SPLIT: *value = c->side_split; return FPTA_OK;
+    case FPTA_OPT_DFT_GEN: *value = c->dft_gen; return FPTA_OK;
+    case FPTA_OPT_GEN_MIX: *value = c->gen_mix; return FPTA_OK;
   }
   return fail(c, FPTA_EINVAL, "get_option: unknown key");
 }
@@ -2002,6 +2076,12 @@ static int batch_common(fpta_ctx* c, uint64_t seed, int64_t real0, int32_t n_rea
   } else {
     int path = 0;
     if ((rc = select_path(c, L, n_real, true, &path))) return rc;
+    // grid signals with a per-pulsar member draw inside their DFT (not for validation draws or coefficient downloads,
+    // which need every signal's coefficients in the buffer)
+    c->gen_fused = path == 4 && !zin && !coeffs_out && c->dft_gen && (c->grid_mfma & 1);
+    c->blk_real0 = real0;
+    c->blk_k0 = k0;
+    c->blk_k1 = k1;
     bool coef_done = false;
     // pipelined gridded block: draws, merges and DFT on the side stream, overlapping the previous block's
     // interpolation (not for zin blocks: their draws read an upload queued on the ctx stream)
@@ -2023,6 +2103,7 @@ static int batch_common(fpta_ctx* c, uint64_t seed, int64_t real0, int32_t n_rea
                               L.n_toa, L.n_toa, n_real, real0, k0, k1),
            "k_white_pairs launch");
   }
+  c->gen_fused = false;
   if (out) HIPCHK(c, hipMemcpyAsync(out, c->out.p, out_bytes, hipMemcpyDeviceToHost, c->stream), "out download");
   if (coeffs_out && L.K > 0) {
     // [P][K][R_pad] -> [P][K][n_real]

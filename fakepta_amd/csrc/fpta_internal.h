@@ -122,6 +122,27 @@ hipError_t launch_grid_dft(hipStream_t st, GridSegs gsegs, int32_t P, const doub
 // the same two steps on v_mfma_f64_16x16x4_f64 (grid_mfma.hip)
 hipError_t launch_grid_dft_mfma(hipStream_t st, GridSegs gsegs, int32_t P, const double* coef, int32_t K,
                                 int32_t R_pad);
+// Fused draw + DFT of one grid signal with at least one per-pulsar member (k_grid_dft_gen): the B operand of every
+// MFMA step is built in registers, term by term in the grid signal's summation order (anchor first, then the other
+// members in layout order): a per-pulsar member's coefficient amp * z from its own Philox stream (the k_gen counter
+// {mode, pulsar, signal, realization}: the same draws), a common member's mixed coefficients loaded from its own
+// columns of the coefficient buffer. No k_gen launch and no coefficient round trip for per-pulsar members.
+constexpr int kDftGenTerms = 8;
+struct DftGenArgs {
+  GridSegDev g;             // the grid signal's tables and its block of the grid buffer (nm: the anchor's modes)
+  int32_t n_terms;
+  int32_t term_kind[kDftGenTerms];   // 0: generated (per-pulsar member), 1: loaded (mixed common member)
+  int32_t term_seg[kDftGenTerms];    // layout index of the member (Philox counter word 2)
+  int32_t term_nm[kDftGenTerms];     // the member's padded modes
+  int32_t term_col0[kDftGenTerms];   // loaded: first coefficient column
+  const double* term_amp[kDftGenTerms];  // generated: [P][term_nm] sqrt(S df)
+  const double* coef;       // [P][K][R_pad]
+  int32_t P, K, R_pad, n_real;
+  int64_t real0;
+  uint32_t k0, k1;
+};
+hipError_t launch_grid_dft_gen(hipStream_t st, const DftGenArgs& a);
+
 // Interpolation band of the whole layout: per chunk of <= kGridTT TOAs the band rows of every signal back to back
 // (V rows, a multiple of 4), the grid-buffer row of each and the weights of each (row, TOA).
 struct GridBand {
@@ -167,6 +188,10 @@ hipError_t launch_mix(hipStream_t st, const SegDesc& sd, int32_t P, int32_t R_pa
 // coefficients into columns acc_col0 .. (a coalesced grid signal's anchor) instead of writing the signal's own
 hipError_t launch_mix_mfma(hipStream_t st, const SegDesc& sd, int32_t P, int32_t R_pad, const double* zbuf,
                            double* coef, int32_t K, double* x_out, int32_t acc_col0 = -1);
+// draw + mixing of a common signal in one kernel (kMixTiledMinP <= P <= kGenMixMaxP): writes the signal's own columns
+constexpr int kGenMixMaxP = 256;
+hipError_t launch_gen_mix(hipStream_t st, const SegDesc& sd, int32_t seg_id, int32_t P, int32_t n_real, int32_t R_pad,
+                          int64_t real0, uint32_t k0, uint32_t k1, double* coef, int32_t K);
 hipError_t launch_mix_tiled(hipStream_t st, const SegDesc& sd, int32_t P, int32_t R_pad, const double* zbuf,
                             double* coef, int32_t K, double* x_out);
 hipError_t launch_epoch_normals(hipStream_t st, int64_t n_blocks, int32_t n_real, int64_t real0, uint32_t k0,

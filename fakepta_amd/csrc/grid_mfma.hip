@@ -189,6 +189,145 @@ __global__ __launch_bounds__(256, 3) void k_grid_dft_mfma(GridSegs gsegs, const 
       }
 }
 
+// ----------------------------------------------------------------------------- k_grid_dft_gen
+// The quarter-range DFT of k_grid_dft_mfma with the coefficients made on chip (DftGenArgs). A workgroup owns 16
+// realizations of one pulsar and nw <= 4 waves:
+//  1. every thread draws (mode, realization) coefficient pairs of the grid signal into LDS, term by term in the
+//     grid signal's summation order (per-pulsar members: Philox + Box-Muller with k_gen's counter; common members:
+//     their mixed coefficients loaded from the coefficient buffer), so each coefficient is made once per workgroup;
+//  2. wave w takes 32-row chunks w, w + nw, ... of the quarter range (rows 0 .. nf / 4): per 4-mode k-step of one
+//     parity, B[k = lg][j = lr] = the (cos, sin) pair of mode 2 (4 q + lg) + parity, realization r0 + lr (one
+//     ds_read_b128), A = table rows in pairs (one 16-byte load per table: row tile 0 -> rows j0 + 2 lr, tile 1 ->
+//     j0 + 2 lr + 1), and the same butterfly as k_grid_dft_mfma writes the grid rows.
+// D of tile h: lane (lr, lg) register g = grid row j0 + 2 (lg + 4 g) + h, realization r0 + lr (16 consecutive
+// realizations of a row per store instruction). A term's product is rounded before the sum, as k_gen stores it and
+// k_coef_merge adds it.
+__device__ __forceinline__ double opaque(double x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+
+constexpr int kDftGenMaxModes = 512;  // LDS: [modes][16 realizations][cos, sin] = 256 B per mode (128 KB at most)
+
+__global__ __launch_bounds__(256, 2) void k_grid_dft_gen(DftGenArgs d) {
+  extern __shared__ __attribute__((aligned(16))) double Bs[];  // [ntq * 2 (both parities)][16][2]
+  const int nthr = blockDim.x;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), nw = nthr >> 6;
+  const int lane = threadIdx.x & 63;
+  const int lr = lane & 15, lg = lane >> 4;
+  const int n_xb = d.R_pad >> 4;
+  const int p = blockIdx.x / n_xb, r0 = (blockIdx.x - p * n_xb) * 16;
+  const GridSegDev& gs = d.g;
+  const int n_modes = 2 * gs.ntq;  // modes held: both parities' padded range (padding modes are zero)
+  // 1. coefficients of every mode for the workgroup's 16 realizations
+  for (int idx = threadIdx.x; idx < n_modes * 16; idx += nthr) {
+    const int m = idx >> 4, rl = idx & 15;
+    const int r = r0 + rl;
+    double bc = 0.0, bs = 0.0;
+    bool first = true;
+    if (m < gs.nm)
+      for (int i = 0; i < d.n_terms; ++i) {
+        if (m >= d.term_nm[i]) continue;
+        double pc, ps;
+        if (d.term_kind[i] == 0) {
+          double zc = 0.0, zs = 0.0;
+          if (r < d.n_real) {  // padding realizations: zero, as k_gen writes them
+            const u32x4 c = {(uint32_t)m, (uint32_t)p, (uint32_t)d.term_seg[i], (uint32_t)(d.real0 + r)};
+            box_muller(philox4x32_10(c, d.k0, d.k1), zc, zs);
+          }
+          const double a = d.term_amp[i][(int64_t)p * d.term_nm[i] + m];
+          pc = opaque(a * zc);
+          ps = opaque(a * zs);
+        } else {
+          const double* cp = d.coef + ((int64_t)p * d.K + d.term_col0[i] + 2 * m) * d.R_pad + r;
+          pc = cp[0];
+          ps = cp[d.R_pad];
+        }
+        bc = first ? pc : bc + pc;
+        bs = first ? ps : bs + ps;
+        first = false;
+      }
+    *(dbl2*)(Bs + 2 * idx) = dbl2{bc, bs};
+  }
+  __syncthreads();
+  // 2. quarter-range rows, 32 per chunk
+  const int Q = gs.nf >> 2, H = gs.nf >> 1;
+  const int n_rc = (Q + 32) >> 5;
+  const int64_t tstride = (int64_t)gs.ntq * gs.ldq;
+  const int n_par[2] = {(gs.nm + 1) >> 1, gs.nm >> 1};  // modes of odd k (m = 2 t) and of even k (m = 2 t + 1)
+  double* __restrict__ gp = gs.g + (int64_t)p * gs.nf * d.R_pad + r0 + lr;
+  for (int rc = wave; rc < n_rc; rc += nw) {
+    const int j0 = 32 * rc;
+    d4 C[2][2], S[2][2];
+#pragma unroll
+    for (int par = 0; par < 2; ++par) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        C[par][h] = d4{0.0, 0.0, 0.0, 0.0};
+        S[par][h] = d4{0.0, 0.0, 0.0, 0.0};
+      }
+      const double* __restrict__ tc = gs.tq + (int64_t)(2 * par) * tstride + (int64_t)lg * gs.ldq + j0 + 2 * lr;
+      const double* __restrict__ ts = tc + tstride;
+      const int nq = (n_par[par] + 3) >> 2;
+      // operands of step q + 2 in flight while step q's MFMAs run (three sets, rotated)
+      dbl2 ac[3], as[3], bb[3];
+      auto fetch = [&](int q, int k) {
+        const int qq = min(q, nq - 1);
+        ac[k] = *(const dbl2*)(tc + (int64_t)(4 * qq) * gs.ldq);
+        as[k] = *(const dbl2*)(ts + (int64_t)(4 * qq) * gs.ldq);
+        bb[k] = *(const dbl2*)(Bs + 2 * ((2 * (4 * qq + lg) + par) * 16 + lr));
+      };
+      if (nq > 0) {
+        fetch(0, 0);
+        fetch(1, 1);
+      }
+      for (int q = 0; q < nq; q += 3) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          if (q + k >= nq) break;
+          fetch(q + k + 2, (k + 2) % 3);
+          C[par][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(ac[k].x, bb[k].x, C[par][0], 0, 0, 0);
+          C[par][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(ac[k].y, bb[k].x, C[par][1], 0, 0, 0);
+          S[par][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(as[k].x, bb[k].y, S[par][0], 0, 0, 0);
+          S[par][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(as[k].y, bb[k].y, S[par][1], 0, 0, 0);
+        }
+      }
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int j = j0 + 2 * (lg + 4 * g) + h;
+        if (j > Q) continue;
+        const double oc = C[0][h][g], os = S[0][h][g], ec = C[1][h][g], es = S[1][h][g];
+        const double pe = ec + es, me = ec - es, po = oc + os, mo = oc - os;
+        gp[(int64_t)j * d.R_pad] = pe + po;
+        gp[(int64_t)(H + j) * d.R_pad] = pe - po;
+        if (j > 0 && j < Q) {
+          gp[(int64_t)(H - j) * d.R_pad] = me - mo;
+          gp[(int64_t)(gs.nf - j) * d.R_pad] = me + mo;
+        }
+      }
+  }
+}
+
+hipError_t launch_grid_dft_gen(hipStream_t st, const DftGenArgs& a) {
+  const int32_t Q = a.g.nf / 4, n_rc = (Q + 32) / 32;
+  if (a.g.nf % 4 != 0 || !a.g.tq || a.R_pad % 16 != 0 || a.n_terms <= 0 || a.n_terms > kDftGenTerms || a.P <= 0 ||
+      a.g.ldq < 32 * n_rc || a.g.ntq < ((((a.g.nm + 1) >> 1) + 3) & ~3) || 2 * a.g.ntq > kDftGenMaxModes)
+    return hipErrorInvalidValue;
+  for (int i = 0; i < a.n_terms; ++i)
+    if (a.term_nm[i] <= 0 || a.term_nm[i] > a.g.nm || (a.term_kind[i] == 0 && !a.term_amp[i]) ||
+        (a.term_kind[i] == 1 && (!a.coef || a.term_col0[i] < 0 || a.term_col0[i] + 2 * a.term_nm[i] > a.K)))
+      return hipErrorInvalidValue;
+  const int64_t blocks = (int64_t)a.P * (a.R_pad / 16);
+  if (blocks > 0x7FFFFFFF) return hipErrorInvalidValue;
+  const int nw = std::min<int32_t>(4, n_rc);
+  const size_t lds = sizeof(double) * 2 * 16 * 2 * (size_t)a.g.ntq;
+  hipLaunchKernelGGL(k_grid_dft_gen, dim3((unsigned)blocks), dim3(64 * nw), lds, st, a);
+  return hipGetLastError();
+}
+
 // ----------------------------------------------------------------------------- k_coef_merge
 // Coalesced grid signal: the anchor's coefficient columns += every other member's (same modes k = m + 1, same w0,
 // same chromatic weight per TOA), summed in member order. Thread = 2 adjacent realizations of one column.
@@ -1107,6 +1246,89 @@ __global__ __launch_bounds__(256, OCC) void k_mix_mfma(const double* __restrict_
           if (x_out) *(dbl2*)(x_out + (int64_t)p * M + m) = dbl2{v0, v1};
         }
       }
+}
+
+// k_gen_mix: draw + ORF mixing of a common signal in one kernel (arrays of kMixTiledMinP .. kGenMixMaxP pulsars). A
+// workgroup owns mode k and 32 realizations r0 .. r0 + 31: its threads draw z[q][cos | sin][r] for every pulsar q with
+// k_gen's counter {k, q, signal, realization} (the same draws) into LDS, then wave (pulsar tile u, column half h)
+// computes coef[p][col0 + 2 k + h][r] = amp[k] sum_q L[p][q] z[q][h][r] for its 64 pulsars on fp64 MFMA (A = L from
+// the zero-padded L^T, 16-byte pairs of pulsar tiles; B = z from LDS, 16-byte pairs of realization tiles), as
+// k_mix_mfma does: the same products, summed in the same k-step order, stored as the rounded product amp * sum.
+// The zbuf round trip (write + read of P x 2 N x R doubles) and a launch are gone.
+
+__global__ __launch_bounds__(512) void k_gen_mix(SegDesc sd, int32_t seg_id, int32_t P, int32_t n_real, int32_t R_pad,
+                                                 int64_t real0, uint32_t k0, uint32_t k1, double* __restrict__ coef,
+                                                 int32_t K) {
+  extern __shared__ __attribute__((aligned(16))) double Zs[];  // [q_pad][64]: cos of 32 realizations, then sin
+  const int n_rb = R_pad >> 5;
+  const int k = blockIdx.x / n_rb, r0 = (blockIdx.x - k * n_rb) * 32;
+  const int q_pad = (P + 7) & ~7;  // k-steps of 4 in pairs: the last step may read up to 8 rows past P
+  for (int idx = threadIdx.x; idx < q_pad * 32; idx += blockDim.x) {
+    const int q = idx >> 5, rl = idx & 31;
+    double zc = 0.0, zs = 0.0;
+    if (q < P && r0 + rl < n_real) {
+      const u32x4 c = {(uint32_t)k, (uint32_t)q, (uint32_t)seg_id, (uint32_t)(real0 + r0 + rl)};
+      box_muller(philox4x32_10(c, k0, k1), zc, zs);
+    }
+    Zs[q * 64 + rl] = zc;
+    Zs[q * 64 + 32 + rl] = zs;
+  }
+  __syncthreads();
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int lr = lane & 15, lg = lane >> 4;
+  const int u = wave >> 1, h = wave & 1;  // pulsar tile (64 pulsars), column half (cos / sin)
+  const int p0 = 64 * u;
+  const int qend = sd.l_lower ? min(P, p0 + 64) : P;
+  d4 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) acc[i][0] = acc[i][1] = d4{0.0, 0.0, 0.0, 0.0};
+  const double* __restrict__ lt = sd.LT + p0 + 2 * lr;
+  const double* __restrict__ zb = Zs + 32 * h + 2 * lr;
+  auto step = [&](int q0) {
+    const int q = q0 + lg;
+    const dbl2 a0 = *(const dbl2*)(lt + (int64_t)q * sd.lt_ld);
+    const dbl2 a1 = *(const dbl2*)(lt + (int64_t)q * sd.lt_ld + 32);
+    const dbl2 b = *(const dbl2*)(zb + q * 64);
+    acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0.x, b.x, acc[0][0], 0, 0, 0);
+    acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0.x, b.y, acc[0][1], 0, 0, 0);
+    acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0.y, b.x, acc[1][0], 0, 0, 0);
+    acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0.y, b.y, acc[1][1], 0, 0, 0);
+    acc[2][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1.x, b.x, acc[2][0], 0, 0, 0);
+    acc[2][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1.x, b.y, acc[2][1], 0, 0, 0);
+    acc[3][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1.y, b.x, acc[3][0], 0, 0, 0);
+    acc[3][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1.y, b.y, acc[3][1], 0, 0, 0);
+  };
+  for (int q0 = 0; q0 < qend; q0 += 4) step(q0);
+  // D of (pulsar tile 2v + e, realization tile c): lane (lr, lg) register g = pulsar p0 + 32 v + 2 (lg + 4 g) + e,
+  // realization r0 + 2 lr + c: one 16-byte store of two adjacent realizations per (lane, pulsar)
+  const double a = sd.amp[k];
+  const int jc = 2 * k + h;
+#pragma unroll
+  for (int v = 0; v < 2; ++v)
+#pragma unroll
+    for (int e = 0; e < 2; ++e)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int p = p0 + 32 * v + 2 * (lg + 4 * g) + e;
+        if (p >= P) continue;
+        double* dst = coef + ((int64_t)p * K + sd.col0 + jc) * R_pad + r0 + 2 * lr;
+        *(dbl2*)dst = dbl2{a * acc[2 * v + e][0][g], a * acc[2 * v + e][1][g]};
+      }
+}
+
+hipError_t launch_gen_mix(hipStream_t st, const SegDesc& sd, int32_t seg_id, int32_t P, int32_t n_real, int32_t R_pad,
+                          int64_t real0, uint32_t k0, uint32_t k1, double* coef, int32_t K) {
+  const int32_t n_pt = (P + 63) / 64;
+  if (sd.kind != 1 || !sd.LT || P < 1 || P > kGenMixMaxP || R_pad % 32 != 0 || sd.lt_ld < 64 * n_pt ||
+      sd.lt_rows < ((P + 7) & ~7) || sd.col0 < 0 || sd.col0 + 2 * sd.nm > K)
+    return hipErrorInvalidValue;
+  const int64_t blocks = (int64_t)sd.nm * (R_pad / 32);
+  if (blocks > 0x7FFFFFFF) return hipErrorInvalidValue;
+  const size_t lds = sizeof(double) * 64 * (size_t)((P + 7) & ~7);
+  hipLaunchKernelGGL(k_gen_mix, dim3((unsigned)blocks), dim3(128 * n_pt), lds, st, sd, seg_id, P, n_real, R_pad, real0,
+                     k0, k1, coef, K);
+  return hipGetLastError();
 }
 
 template <int NU, int NB, int OCC>

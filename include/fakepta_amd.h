@@ -317,6 +317,13 @@ int fpta_comm_gather(fpta_comm* comm, const double* send, int64_t count, double*
                                      the largest DFT, when it has no common (ORF-mixed) member, is drawn and
                                      transformed on a second side stream, beside the other signals' draws, mixing
                                      and DFT; 0 one side stream for all. Results are identical. */
+#define FPTA_OPT_DFT_GEN 17       /* gridded path: 1 (default) a grid signal with a per-pulsar member draws its
+                                     coefficients inside its DFT kernel (k_grid_dft_gen: Philox + Box-Muller into
+                                     LDS, same counters and draws as k_gen); 0 k_gen writes them to the coefficient
+                                     buffer and k_grid_dft_mfma reads them back. Same draws; sums agree to rounding. */
+#define FPTA_OPT_GEN_MIX 18       /* common signals of 64..256 pulsars (fp64 MFMA mixing): 1 (default) draws and ORF
+                                     mixing in one kernel (k_gen_mix: normals in LDS, no zbuf round trip); 0 k_gen then
+                                     k_mix_mfma. Same draws and products; results identical. */
 int fpta_set_option(fpta_ctx* ctx, int32_t key, int64_t value);
 /* Current value of option `key` (same keys as fpta_set_option). */
 int fpta_get_option(fpta_ctx* ctx, int32_t key, int64_t* value);

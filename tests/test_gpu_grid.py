@@ -47,12 +47,14 @@ def shipped(ctx, capi):
     return opts
 
 
-@pytest.fixture(params=[1, 0], ids=["dft_mfma", "dft_valu"])
+@pytest.fixture(params=[(1, 1), (1, 0), (0, 0)], ids=["dft_gen", "dft_mfma", "dft_valu"])
 def gridded(ctx, capi, shipped, request):
-    """Gridded path with the DFT on fp64 MFMA or VALU (FPTA_OPT_GRID_MFMA bit 0; the interpolation is always
-    k_grid_interp_mfma); the context's options are restored to the shipped snapshot afterwards."""
+    """Gridded path with the DFT drawing its per-pulsar coefficients itself (k_grid_dft_gen, the default), or reading
+    them from the coefficient buffer on fp64 MFMA or VALU (FPTA_OPT_DFT_GEN 0, FPTA_OPT_GRID_MFMA bit 0); the
+    interpolation is on MFMA in every case. The context's options are restored to the shipped snapshot afterwards."""
     ctx.set_option(capi.OPT_SYNTH_PATH, 4)
-    ctx.set_option(capi.OPT_GRID_MFMA, request.param)
+    ctx.set_option(capi.OPT_GRID_MFMA, request.param[0])
+    ctx.set_option(capi.OPT_DFT_GEN, request.param[1])
     yield ctx
     ctx.set_options(shipped)
 
@@ -485,3 +487,69 @@ def test_partial_realization_blocks_write_every_sample(ctx, capi, shipped, ws, R
         np.testing.assert_allclose(sums[:, 1], (got * got).sum(axis=1), rtol=1e-10)
     finally:
         ctx.set_options(shipped)
+
+
+@pytest.mark.parametrize("layout", ["coalesced", "dm_only", "masked", "many_modes"])
+def test_dft_gen_matches_buffered_draws(ctx, capi, shipped, layout):
+    """k_grid_dft_gen (FPTA_OPT_DFT_GEN 1) draws the per-pulsar members' coefficients with k_gen's counters and sums
+    a grid signal's terms in the merge order (anchor, then the others; products rounded first): its blocks equal
+    the buffered path's (k_gen -> coefficient buffer -> k_coef_merge / mix epilogue -> k_grid_dft_mfma) bit for
+    bit, pipelined or not, over realization counts off every tile multiple; and they match the oracle."""
+    rng = np.random.default_rng(zlib_crc(layout))
+    if layout in ("coalesced", "masked"):
+        offs, toas, nu, segs = _shared_span_layout(ctx, rng, nu_const=False, with_masked=layout == "masked")
+    elif layout == "dm_only":
+        offs, toas, nu, segs = _flat_layout(ctx, rng, P=9, n_modes=100)
+    else:  # 257 modes: seven 32-row chunks of the quarter range, several per wave
+        offs, toas, nu, segs = _flat_layout(ctx, rng, P=3, n_modes=257)
+    try:
+        ctx.set_option(capi.OPT_SYNTH_PATH, 4)
+        for R, real0 in ((150, 5), (333, 1000), (16, 7)):
+            res = {}
+            for gen in (0, 1):
+                ctx.set_option(capi.OPT_DFT_GEN, gen)
+                for ov in (0, 1):
+                    ctx.set_option(capi.OPT_OVERLAP, ov)
+                    res[gen, ov] = ctx.batch_synth(13, real0, R)
+            for k in res:
+                np.testing.assert_array_equal(res[k], res[0, 0])
+            want = O.batch_synth(offs, toas, nu, segs, 13, real0, R)
+            assert_parity(res[1, 1], want, TOL)
+    finally:
+        ctx.set_options(shipped)
+
+
+def zlib_crc(s):
+    import zlib
+    return zlib.crc32(s.encode())
+
+
+@pytest.mark.parametrize("factor", ["cholesky", "svd"])
+def test_gen_mix_matches_two_kernels(ctx, capi, shipped, factor):
+    """k_gen_mix (FPTA_OPT_GEN_MIX 1) draws a common signal's normals into LDS and mixes them on fp64 MFMA in one
+    kernel: same counters, same products in the same k-step order as k_gen + k_mix_mfma, so blocks are bit-identical
+    on the gridded (with and without k_grid_dft_gen) and exact paths, for a triangular (Cholesky) and a dense (SVD)
+    ORF factor, 70 and 160 pulsars (two and three 64-pulsar tiles)."""
+    rng = np.random.default_rng(71 if factor == "cholesky" else 72)
+    for P in (70, 160):
+        offs, toas, nu = random_layout(rng, P, (40, 120))
+        ctx.batch_set_toas(offs, toas, nu)
+        f, a = per_psr_signal(rng, offs, toas, 20)
+        ctx.batch_add_signal(0, f, a)
+        fc, ac, _, pos = common_signal(rng, offs, toas, 30)
+        gam = O.orf_hd(pos)
+        L = np.linalg.cholesky(gam) if factor == "cholesky" else O.mvn_factor(gam)
+        ctx.batch_add_signal(1, fc, ac, L=L)
+        segs = [O.Segment(0, 2 * np.pi * f, a, 0.0), O.Segment(1, 2 * np.pi * fc, ac, 0.0, L=L)]
+        try:
+            for path, dft_gen in ((4, 1), (4, 0), (3, 0), (2, 0)):
+                ctx.set_option(capi.OPT_SYNTH_PATH, path)
+                ctx.set_option(capi.OPT_DFT_GEN, dft_gen)
+                res = {}
+                for gm in (0, 1):
+                    ctx.set_option(capi.OPT_GEN_MIX, gm)
+                    res[gm] = ctx.batch_synth(17, 40, 300)
+                np.testing.assert_array_equal(res[0], res[1])
+                assert_parity(res[1], O.batch_synth(offs, toas, nu, segs, 17, 40, 300), TOL)
+        finally:
+            ctx.set_options(shipped)
