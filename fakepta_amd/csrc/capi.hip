@@ -229,9 +229,17 @@ struct fpta_ctx {
   bool s2done_set = false;
   int32_t split_g = -1;
   bool coef_copy_pending = false;  // the block's coefficients are still to be downloaded after the synthesis
-  DevBuf part, part_tmp; // partial checksums [n_chunks][R_pad][2] of the last block, reduction scratch
-  bool part_ready = false;  // part holds the partials of the current block (c->out, out_R)
+  DevBuf part[2], part_tmp; // partial checksums [n_chunks][R_pad][2] (two buffers, by block), reduction scratch
+  bool part_ready = false;  // part[part_cur] holds the partials of the current block (c->out, out_R)
   int32_t part_chunks = 0, part_rpad = 0;
+  int part_cur = 0, part_next = 0;
+  // streamed jobs reduce a block's partials on their own stream (red), beside the next block's interpolation, which
+  // writes the other partials buffer; ev_pfree[i]: the reduction reading part[i] is done (the interpolation that next
+  // writes part[i] waits for it); red_pending: red has work the ctx stream has not joined
+  hipStream_t red = nullptr;
+  hipEvent_t ev_pready = nullptr, ev_pfree[2] = {nullptr, nullptr}, ev_red = nullptr;
+  bool pfree_set[2] = {false, false};
+  bool red_pending = false;
   int last_path = 0;     // synthesis path of the last batch (1 direct, 2 MFMA, 3 VALU, 4 gridded)
   std::string path_reason;  // why the last batch did not take the gridded path (empty if it did)
   // gridded path defaults: w = 15 at sigma = 1.5 (a-priori bound 1.5e-12). The measured flat-spectrum worst case at
@@ -317,6 +325,16 @@ struct KTimer {
     }
   }
 };
+
+// The ctx stream waits for everything queued on the red stream (partial-checksum reductions of streamed jobs).
+int join_red(fpta_ctx* c) {
+  if (!c->red_pending) return FPTA_OK;
+  if (!c->ev_red) HIPCHK(c, hipEventCreateWithFlags(&c->ev_red, hipEventDisableTiming), "event create");
+  HIPCHK(c, hipEventRecord(c->ev_red, c->red), "event record");
+  HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_red, 0), "red join");
+  c->red_pending = false;
+  return FPTA_OK;
+}
 
 int upload(fpta_ctx* c, DevBuf& buf, const void* src, size_t bytes, const char* what) {
   HIPCHK(c, buf.ensure(bytes), what);
@@ -1260,8 +1278,16 @@ int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad, bool pipe = fa
   }
   // partial checksums of a batch block (written into the context's own block, not accumulated)
   if (c->fuse_sums && a.out == c->out.as<double>() && !a.accumulate) {
-    HIPCHK(c, c->part.ensure(sizeof(double) * 2 * (size_t)G.n_chunks * R_pad), "partial checksums alloc");
-    a.part = c->part.as<double>();
+    const int pi = c->part_next;
+    DevBuf& pb = c->part[pi];
+    const size_t pbytes = sizeof(double) * 2 * (size_t)G.n_chunks * R_pad;
+    if (pb.cap < pbytes && c->red) HIPCHK(c, hipStreamSynchronize(c->red), "partials regrow sync");
+    HIPCHK(c, pb.ensure(pbytes), "partial checksums alloc");
+    // the reduction of the block that last wrote this buffer (on the red stream) must have read it
+    if (c->pfree_set[pi]) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_pfree[pi], 0), "partials buffer wait");
+    a.part = pb.as<double>();
+    c->part_cur = pi;
+    c->part_next = pi ^ 1;
   }
   if (pipe) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_gready, 0), "grid ready wait");
   if (pipe && c->s2done_set) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_gready2, 0), "grid ready wait");
@@ -1270,7 +1296,7 @@ int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad, bool pipe = fa
                 G.grid_rows};
   // the warp-specialised kernel for plain blocks; with fused partial checksums its reduce-scatter temporaries take
   // its VGPRs to 230 and the register kernel is faster (C3: 47.9 vs 52.5 ms per job, profiles/r02k_ab_c2c3_ws.txt)
-  if (c->interp_ws && !c->interp_lds && !a.w_on && !a.accumulate && !a.part) {
+  if (c->interp_ws && !c->interp_lds && !a.w_on && !a.accumulate && (!a.part || c->interp_ws == 2)) {
     HIPCHK(c, launch_grid_interp_ws(c->stream, a, band, R_pad), "k_grid_interp_ws launch");
   } else if (c->interp_lds && G.lds_ok && !a.w_on) {
     GridLds lds{G.groups.as<int4>(), G.urows.as<int32_t>(), G.lrows.as<int32_t>(), G.n_groups, G.lds_rows};
@@ -1615,6 +1641,12 @@ int fpta_destroy(fpta_ctx* c) {
     (void)hipStreamSynchronize(c->side2);
     (void)hipStreamDestroy(c->side2);
   }
+  if (c->red) {
+    (void)hipStreamSynchronize(c->red);
+    (void)hipStreamDestroy(c->red);
+  }
+  for (hipEvent_t e : {c->ev_pready, c->ev_pfree[0], c->ev_pfree[1], c->ev_red})
+    if (e) (void)hipEventDestroy(e);
   for (hipEvent_t e : {c->ev_s2begin, c->ev_s2done, c->ev_gready2})
     if (e) (void)hipEventDestroy(e);
   if (c->ev_begin) (void)hipEventDestroy(c->ev_begin);
@@ -1675,7 +1707,8 @@ int fpta_set_option(fpta_ctx* c, int32_t key, int64_t value) {
       c->batch.grid.clear();
       return FPTA_OK;
     case FPTA_OPT_INTERP_WS:
-      c->interp_ws = value ? 1 : 0;
+      if (value < 0 || value > 2) return fail(c, FPTA_EINVAL, "interp_ws must be 0, 1 or 2");
+      c->interp_ws = (int)value;
       return FPTA_OK;
     case FPTA_OPT_SIDE_SPLIT:
       c->side_split = value ? 1 : 0;
@@ -1734,6 +1767,8 @@ int fpta_build_flags(void) {
 int fpta_synchronize(fpta_ctx* c) {
   if (!c) return fail(nullptr, FPTA_EINVAL, "null ctx");
   HIPCHK(c, hipSetDevice(c->device), "hipSetDevice");
+  int rc = join_red(c);
+  if (rc) return rc;
   HIPCHK(c, hipStreamSynchronize(c->stream), "hipStreamSynchronize");
   return FPTA_OK;
 }
@@ -2156,16 +2191,42 @@ int fpta_batch_device_out(fpta_ctx* c, double** dptr, int64_t* ld, int32_t* n_re
   return FPTA_OK;
 }
 
-// Per-realization {sum, sum of squares} of the context's last block into c->sums (device), on the ctx stream:
-// from the interpolation's partial checksums when it wrote them for this block, else one pass over the block.
-static int launch_block_checksums(fpta_ctx* c) {
-  HIPCHK(c, c->sums.ensure(sizeof(double) * 2 * c->out_R), "sums alloc");
+// Per-realization {sum, sum of squares} of the context's last block into c->sums (device): from the interpolation's
+// partial checksums when it wrote them for this block, else one pass over the block. On the ctx stream, or (async,
+// streamed jobs with partials) on the red stream beside the next block's work; *used: the stream the sums are on.
+static int launch_block_checksums(fpta_ctx* c, bool async = false, hipStream_t* used = nullptr) {
+  hipStream_t st = c->stream;
+  if (async && c->part_ready) {
+    if (!c->red) HIPCHK(c, hipStreamCreateWithFlags(&c->red, hipStreamNonBlocking), "red stream create");
+    for (hipEvent_t* e : {&c->ev_pready, &c->ev_pfree[0], &c->ev_pfree[1]})
+      if (!*e) HIPCHK(c, hipEventCreateWithFlags(e, hipEventDisableTiming), "event create");
+    HIPCHK(c, hipEventRecord(c->ev_pready, c->stream), "event record");
+    HIPCHK(c, hipStreamWaitEvent(c->red, c->ev_pready, 0), "partials ready wait");
+    st = c->red;
+    c->red_pending = true;
+  } else {
+    int rc = join_red(c);  // sums / part_tmp / partials may still be in use there
+    if (rc) return rc;
+  }
+  if (used) *used = st;
+  if (c->sums.cap < sizeof(double) * 2 * c->out_R) {
+    HIPCHK(c, hipStreamSynchronize(st), "sums regrow sync");
+    HIPCHK(c, c->sums.ensure(sizeof(double) * 2 * c->out_R), "sums alloc");
+  }
   if (c->part_ready) {
-    HIPCHK(c, c->part_tmp.ensure(sizeof(double) * 2 * (size_t)kPartSegs * c->part_rpad), "partials scratch alloc");
+    const size_t tb = sizeof(double) * 2 * (size_t)kPartSegs * c->part_rpad;
+    if (c->part_tmp.cap < tb) {
+      HIPCHK(c, hipStreamSynchronize(st), "partials scratch regrow sync");
+      HIPCHK(c, c->part_tmp.ensure(tb), "partials scratch alloc");
+    }
     HIPCHK(c,
-           launch_part_checksums(c->stream, c->part.as<double>(), c->part_chunks, c->part_rpad, c->out_R,
+           launch_part_checksums(st, c->part[c->part_cur].as<double>(), c->part_chunks, c->part_rpad, c->out_R,
                                  c->part_tmp.as<double>(), c->sums.as<double>()),
            "k_part_reduce launch");
+    if (st == c->red) {
+      HIPCHK(c, hipEventRecord(c->ev_pfree[c->part_cur], c->red), "event record");
+      c->pfree_set[c->part_cur] = true;
+    }
   } else {
     HIPCHK(c, launch_checksums(c->stream, c->out.as<double>(), c->out_ld, c->out_ld, c->out_R, c->sums.as<double>()),
            "k_checksums launch");
@@ -2334,12 +2395,16 @@ int multi_fail(fpta_multi* m, int i, int rc) {
   return rc;
 }
 
-// k_checksums of the context's last block -> host (pinned) dst [n_real][2], asynchronously on the ctx stream.
-int checksums_async(fpta_ctx* c, double* dst) {
-  int rc = launch_block_checksums(c);
+// checksums of the context's last block -> dst [n_real][2] (pinned host, or device with d2d), asynchronously: on the
+// red stream beside the next block when the interpolation wrote partials, else on the ctx stream.
+int checksums_async(fpta_ctx* c, double* dst, bool d2d = false) {
+  hipStream_t st = nullptr;
+  int rc = launch_block_checksums(c, true, &st);
   if (rc) return rc;
-  HIPCHK(c, hipMemcpyAsync(dst, c->sums.p, sizeof(double) * 2 * c->out_R, hipMemcpyDeviceToHost, c->stream),
-         "sums download");
+  HIPCHK(c,
+         hipMemcpyAsync(dst, c->sums.p, sizeof(double) * 2 * c->out_R,
+                        d2d ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, st),
+         "sums copy");
   return FPTA_OK;
 }
 }  // namespace
@@ -2525,18 +2590,18 @@ static int stream_checksums(fpta_multi* m, uint64_t seed, int64_t real0, int64_t
       if ((rc = batch_common(c, seed, real0 + first, n, nullptr, 0, nullptr, nullptr, true)))
         rc = multi_fail(m, (int)g, rc);
       else if (use_rccl) {
-        rc = launch_block_checksums(c);
-        if (!rc) {
-          hipError_t e = hipMemcpyAsync(m->shard[g]->as<double>() + 2 * (first - beg[g]), c->sums.p,
-                                        sizeof(double) * 2 * n, hipMemcpyDeviceToDevice, c->stream);
-          if (e != hipSuccess) rc = hip_fail(c, e, "multi_synth shard copy");
-        }
-        if (rc) rc = multi_fail(m, (int)g, rc);
+        if ((rc = checksums_async(c, m->shard[g]->as<double>() + 2 * (first - beg[g]), true)))
+          rc = multi_fail(m, (int)g, rc);
       } else if ((rc = checksums_async(c, stage[g] + 2 * (first - beg[g])))) {
         rc = multi_fail(m, (int)g, rc);
       }
     }
     if (!any) break;
+  }
+  for (int64_t g = 0; g < G && !rc; ++g) {  // the reductions and copies on each device's red stream come first
+    fpta_ctx* c = m->ctx[g];
+    (void)hipSetDevice(c->device);
+    if ((rc = join_red(c))) rc = multi_fail(m, (int)g, rc);
   }
   if (use_rccl && !rc) {
     // every device's shard to device 0 in one collective (pad rows beyond a shard's count are dropped below)

@@ -297,8 +297,8 @@ __global__ __launch_bounds__(1024) void k_chol_solve(const double* __restrict__ 
 }
 
 // ----------------------------------------------------------------------------- k_dense_normals
-// ZT[t][r] for the batched dense draws: ctr = (t, 0xFFFFFFFF, 0xFFFFFFF2, g >> 1), pick [g & 1],
-// g = real0 + r (oracle: white_normals_rpairs(..., stream=DENSE_STREAM)). Zero outside
+// ZT[t][r] for the batched dense draws: quad_normal(t, DENSE stream, g), g = real0 + r (oracle:
+// quad_normals(..., stream=DENSE_STREAM)). Zero outside
 // [0,n) x [0,n_real). grid (ldz / 256, rows).
 __global__ __launch_bounds__(256) void k_dense_normals(int64_t n, int32_t n_real, int64_t real0, uint32_t k0,
                                                        uint32_t k1, double* __restrict__ ZT, int64_t ldz) {
@@ -306,11 +306,7 @@ __global__ __launch_bounds__(256) void k_dense_normals(int64_t n, int32_t n_real
   const int64_t t = blockIdx.y;
   double z = 0.0;
   if (t < n && r < n_real) {
-    const int64_t g = real0 + r;
-    const u32x4 c = {(uint32_t)t, kWhitePsrWord, kDenseStream, (uint32_t)(g >> 1)};
-    double z0, z1;
-    box_muller(philox4x32_10(c, k0, k1), z0, z1);
-    z = (g & 1) ? z1 : z0;
+    z = quad_normal((uint64_t)t, kDenseStream, (uint64_t)(real0 + r), k0, k1);
   }
   ZT[t * ldz + r] = z;
 }

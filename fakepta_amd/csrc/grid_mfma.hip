@@ -219,35 +219,51 @@ __global__ __launch_bounds__(256, 2) void k_grid_dft_gen(DftGenArgs d) {
   const int p = blockIdx.x / n_xb, r0 = (blockIdx.x - p * n_xb) * 16;
   const GridSegDev& gs = d.g;
   const int n_modes = 2 * gs.ntq;  // modes held: both parities' padded range (padding modes are zero)
-  // 1. coefficients of every mode for the workgroup's 16 realizations
-  for (int idx = threadIdx.x; idx < n_modes * 16; idx += nthr) {
-    const int m = idx >> 4, rl = idx & 15;
+  // 1. coefficients of every mode for the workgroup's 16 realizations, a realization pair per thread and mode (one
+  //    Philox call per pair and generated term)
+  for (int idx = threadIdx.x; idx < n_modes * 8; idx += nthr) {
+    const int m = idx >> 3, rl = 2 * (idx & 7);
     const int r = r0 + rl;
-    double bc = 0.0, bs = 0.0;
+    double bc[2] = {0.0, 0.0}, bs[2] = {0.0, 0.0};
     bool first = true;
     if (m < gs.nm)
       for (int i = 0; i < d.n_terms; ++i) {
         if (m >= d.term_nm[i]) continue;
-        double pc, ps;
+        double pc[2], ps[2];
         if (d.term_kind[i] == 0) {
-          double zc = 0.0, zs = 0.0;
+          double z[4] = {0.0, 0.0, 0.0, 0.0};
+          const uint64_t g = (uint64_t)(d.real0 + r);
           if (r < d.n_real) {  // padding realizations: zero, as k_gen writes them
-            const u32x4 c = {(uint32_t)m, (uint32_t)p, (uint32_t)d.term_seg[i], (uint32_t)(d.real0 + r)};
-            box_muller(philox4x32_10(c, d.k0, d.k1), zc, zs);
+            if ((g & 1) == 0) {
+              gp_pair2((uint32_t)m, (uint32_t)p, (uint32_t)d.term_seg[i], g, d.k0, d.k1, z);
+            } else {
+              gp_normal2((uint32_t)m, (uint32_t)p, (uint32_t)d.term_seg[i], g, d.k0, d.k1, z[0], z[1]);
+              gp_normal2((uint32_t)m, (uint32_t)p, (uint32_t)d.term_seg[i], g + 1, d.k0, d.k1, z[2], z[3]);
+            }
+            if (r + 1 >= d.n_real) z[2] = z[3] = 0.0;
           }
           const double a = d.term_amp[i][(int64_t)p * d.term_nm[i] + m];
-          pc = opaque(a * zc);
-          ps = opaque(a * zs);
+          pc[0] = opaque(a * z[0]);
+          ps[0] = opaque(a * z[1]);
+          pc[1] = opaque(a * z[2]);
+          ps[1] = opaque(a * z[3]);
         } else {
           const double* cp = d.coef + ((int64_t)p * d.K + d.term_col0[i] + 2 * m) * d.R_pad + r;
-          pc = cp[0];
-          ps = cp[d.R_pad];
+          const dbl2 vc = *(const dbl2*)cp, vs = *(const dbl2*)(cp + d.R_pad);
+          pc[0] = vc.x;
+          pc[1] = vc.y;
+          ps[0] = vs.x;
+          ps[1] = vs.y;
         }
-        bc = first ? pc : bc + pc;
-        bs = first ? ps : bs + ps;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          bc[h] = first ? pc[h] : bc[h] + pc[h];
+          bs[h] = first ? ps[h] : bs[h] + ps[h];
+        }
         first = false;
       }
-    *(dbl2*)(Bs + 2 * idx) = dbl2{bc, bs};
+    *(dbl2*)(Bs + 2 * (m * 16 + rl)) = dbl2{bc[0], bs[0]};
+    *(dbl2*)(Bs + 2 * (m * 16 + rl + 1)) = dbl2{bc[1], bs[1]};
   }
   __syncthreads();
   // 2. quarter-range rows, 32 per chunk
@@ -356,12 +372,19 @@ hipError_t launch_coef_merge(hipStream_t st, const CoefMerge& m, int32_t P, int3
   return hipGetLastError();
 }
 
-// White-noise normals of (TOA t, global realizations g, g + 1 of the pair containing g): the
-// realization-paired stream of oracle.white_normals_rpairs (same words as kernels.hip white_pair).
-__device__ __forceinline__ void mfma_white_pair(int64_t t, int64_t g, uint32_t k0, uint32_t k1, double& z0,
-                                                double& z1) {
-  const u32x4 c = {(uint32_t)t, kWhitePsrWord, kWhiteStream, (uint32_t)(g >> 1)};
-  box_muller(philox4x32_10(c, k0, k1), z0, z1);
+// White-noise normals (oracle quad_normals on the white stream, the words of kernels.hip white_pair).
+// quad: the white normals of TOAs t, t + 1 and realizations g, g + 1 (z[2 e + h]: TOA t + e, realization g + h) from one
+// Philox call when t and g are even, else one call per value (a pulsar's first chunk at an odd TOA offset, or an odd
+// first realization).
+__device__ __forceinline__ void white_quad(int64_t t, int64_t g, uint32_t k0, uint32_t k1, double (&z)[4]) {
+  if (((t | g) & 1) == 0) {
+    quad4((uint64_t)t, kWhiteStream, (uint64_t)g, k0, k1, z);
+  } else {
+#pragma unroll
+    for (int e = 0; e < 2; ++e)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) z[2 * e + h] = quad_normal((uint64_t)(t + e), kWhiteStream, (uint64_t)(g + h), k0, k1);
+  }
 }
 
 // ----------------------------------------------------------------------------- k_grid_interp_mfma
@@ -404,42 +427,38 @@ __device__ __forceinline__ void interp_white(const SynthArgs& a, const InterpTil
   const int tt = 2 * lr;  // this lane's even TOA in the chunk; tt + 1 the odd one
   if (tt >= t.cnt) return;
   const int64_t tg = ld_uniform(a.offs + t.p) + t.y + tt;
-  {
+  const bool two = tt + 1 < t.cnt;
+  double sg[2] = {0.0, 0.0}, es[2] = {0.0, 0.0};
+  int ep[2] = {-1, -1};
 #pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      if (tt + e >= t.cnt) break;
-      const int64_t te = tg + e;
-      const double sg = a.w_sigma ? a.w_sigma[te] : 0.0;
-      const int ep = a.w_block_of ? a.w_block_of[te] : -1;
-      const double es = ep >= 0 ? a.w_esig[ep] : 0.0;
+  for (int e = 0; e < 2; ++e) {
+    if (e == 1 && !two) break;
+    sg[e] = a.w_sigma ? a.w_sigma[tg + e] : 0.0;
+    ep[e] = a.w_block_of ? a.w_block_of[tg + e] : -1;
+    es[e] = ep[e] >= 0 ? a.w_esig[ep[e]] : 0.0;
+  }
 #pragma unroll
-      for (int m = 0; m < NP; ++m) {
+  for (int m = 0; m < NP; ++m) {
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int rl = t.r0 + 32 * m + 2 * (lg + 4 * g);  // batch index of acc[e][2m][g]; acc[e][2m + 1][g]: rl + 1
-          double x0 = acc[e][2 * m][g], x1 = acc[e][2 * m + 1][g];
-          if (a.w_sigma) {
-            const int64_t g0 = a.real0 + rl;  // parity uniform over the launch (rl even)
-            double z0, z1;
-            mfma_white_pair(te, g0, a.k0, a.k1, z0, z1);
-            if (g0 & 1) {  // (g0, g0 + 1) straddle two pairs
-              double y0, y1;
-              mfma_white_pair(te, g0 + 1, a.k0, a.k1, y0, y1);
-              x0 = fma(sg, z1, x0);
-              x1 = fma(sg, y0, x1);
-            } else {
-              x0 = fma(sg, z0, x0);
-              x1 = fma(sg, z1, x1);
-            }
-          }
-          if (ep >= 0) {
-            if (rl < a.n_real) x0 = fma(es, a.w_zb[(int64_t)rl * a.w_nblocks + ep], x0);
-            if (rl + 1 < a.n_real) x1 = fma(es, a.w_zb[(int64_t)(rl + 1) * a.w_nblocks + ep], x1);
-          }
-          acc[e][2 * m][g] = x0;
-          acc[e][2 * m + 1][g] = x1;
-        }
+    for (int g = 0; g < 4; ++g) {
+      // acc[e][2m + h][g]: TOA tg + e, batch realization rl + h
+      const int rl = t.r0 + 32 * m + 2 * (lg + 4 * g);
+      if (a.w_sigma) {
+        double z[4];
+        white_quad(tg, a.real0 + rl, a.k0, a.k1, z);
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+#pragma unroll
+          for (int h = 0; h < 2; ++h) acc[e][2 * m + h][g] = fma(sg[e], z[2 * e + h], acc[e][2 * m + h][g]);
       }
+#pragma unroll
+      for (int e = 0; e < 2; ++e)
+        if (ep[e] >= 0) {
+#pragma unroll
+          for (int h = 0; h < 2; ++h)
+            if (rl + h < a.n_real)
+              acc[e][2 * m + h][g] = fma(es[e], a.w_zb[(int64_t)(rl + h) * a.w_nblocks + ep[e]], acc[e][2 * m + h][g]);
+        }
     }
   }
 }
@@ -1092,8 +1111,12 @@ hipError_t launch_grid_interp_ws(hipStream_t st, const SynthArgs& a, const GridB
   }
   // persistent: one workgroup per CU (the 4-slot ring takes 4 x 17 KB = 68 KB of the 160 KB LDS)
   const int64_t grid = std::min<int64_t>((tiles + 7) / 8 * 8, ((int64_t)n_cu + 7) / 8 * 8);
-  if (a.part) return hipErrorInvalidValue;  // fused partial checksums take k_grid_interp_mfma (faster there)
-  hipLaunchKernelGGL(k_grid_interp_ws<false>, dim3((unsigned)grid), dim3(512), 0, st, a, band, (int32_t)tiles, R_pad, a.out);
+  if (a.part)
+    hipLaunchKernelGGL(k_grid_interp_ws<true>, dim3((unsigned)grid), dim3(512), 0, st, a, band, (int32_t)tiles, R_pad,
+                       a.out);
+  else
+    hipLaunchKernelGGL(k_grid_interp_ws<false>, dim3((unsigned)grid), dim3(512), 0, st, a, band, (int32_t)tiles, R_pad,
+                       a.out);
   return hipGetLastError();
 }
 
@@ -1263,15 +1286,22 @@ __global__ __launch_bounds__(512) void k_gen_mix(SegDesc sd, int32_t seg_id, int
   const int n_rb = R_pad >> 5;
   const int k = blockIdx.x / n_rb, r0 = (blockIdx.x - k * n_rb) * 32;
   const int q_pad = (P + 7) & ~7;  // k-steps of 4 in pairs: the last step may read up to 8 rows past P
-  for (int idx = threadIdx.x; idx < q_pad * 32; idx += blockDim.x) {
-    const int q = idx >> 5, rl = idx & 31;
-    double zc = 0.0, zs = 0.0;
-    if (q < P && r0 + rl < n_real) {
-      const u32x4 c = {(uint32_t)k, (uint32_t)q, (uint32_t)seg_id, (uint32_t)(real0 + r0 + rl)};
-      box_muller(philox4x32_10(c, k0, k1), zc, zs);
+  for (int idx = threadIdx.x; idx < q_pad * 16; idx += blockDim.x) {  // a realization pair per thread and pulsar
+    const int q = idx >> 4, rl = 2 * (idx & 15);
+    double z[4] = {0.0, 0.0, 0.0, 0.0};
+    const int r = r0 + rl;
+    if (q < P && r < n_real) {
+      const uint64_t g = (uint64_t)(real0 + r);
+      if ((g & 1) == 0) {
+        gp_pair2((uint32_t)k, (uint32_t)q, (uint32_t)seg_id, g, k0, k1, z);
+      } else {
+        gp_normal2((uint32_t)k, (uint32_t)q, (uint32_t)seg_id, g, k0, k1, z[0], z[1]);
+        gp_normal2((uint32_t)k, (uint32_t)q, (uint32_t)seg_id, g + 1, k0, k1, z[2], z[3]);
+      }
+      if (r + 1 >= n_real) z[2] = z[3] = 0.0;
     }
-    Zs[q * 64 + rl] = zc;
-    Zs[q * 64 + 32 + rl] = zs;
+    *(dbl2*)(Zs + q * 64 + rl) = dbl2{z[0], z[2]};
+    *(dbl2*)(Zs + q * 64 + 32 + rl) = dbl2{z[1], z[3]};
   }
   __syncthreads();
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);

@@ -19,39 +19,51 @@
 namespace fpta {
 
 // ----------------------------------------------------------------------------- k_gen
-// grid (ceil(R_pad/256), nm, P). One Philox call per (mode, pulsar, segment, realization)
-// gives the (cos, sin) pair of that mode. Writes every entry of the realization padding.
+// grid (ceil(R_pad/512), nm, P): thread = realization pair (r, r + 1), r even. One Philox call per (mode, pulsar,
+// segment, global realization pair) gives the (cos, sin) pairs of both realizations (philox.h gp_pair2). Writes every
+// entry of the realization padding.
 __global__ __launch_bounds__(256) void k_gen(SegDesc sd, int32_t seg_id, int32_t P, int32_t n_real,
                                              int32_t R_pad, int64_t real0, uint32_t k0, uint32_t k1,
                                              const double* __restrict__ zin, int32_t zin_nseg,
                                              int32_t zin_nm, double* __restrict__ coef, int32_t K,
                                              double* __restrict__ zbuf) {
-  const int r = blockIdx.x * 256 + threadIdx.x;
+  const int r = (blockIdx.x * 256 + threadIdx.x) * 2;
   if (r >= R_pad) return;
   const int k = blockIdx.y;
   const int p = blockIdx.z;
-  double zc = 0.0, zs = 0.0;
-  if (r < n_real) {
-    if (zin) {
-      if (k < zin_nm) {
-        const double* zz = zin + ((((int64_t)r * zin_nseg + seg_id) * P + p) * zin_nm + k) * 2;
-        zc = zz[0];
-        zs = zz[1];
+  double zc[2] = {0.0, 0.0}, zs[2] = {0.0, 0.0};
+  if (zin) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+      if (r + h < n_real && k < zin_nm) {
+        const double* zz = zin + ((((int64_t)(r + h) * zin_nseg + seg_id) * P + p) * zin_nm + k) * 2;
+        zc[h] = zz[0];
+        zs[h] = zz[1];
       }
+  } else if (r < n_real) {
+    const uint64_t g = (uint64_t)(real0 + r);
+    if ((g & 1) == 0) {
+      double z[4];
+      gp_pair2((uint32_t)k, (uint32_t)p, (uint32_t)seg_id, g, k0, k1, z);
+      zc[0] = z[0];
+      zs[0] = z[1];
+      zc[1] = z[2];
+      zs[1] = z[3];
     } else {
-      const u32x4 c = {(uint32_t)k, (uint32_t)p, (uint32_t)seg_id, (uint32_t)(real0 + r)};
-      box_muller(philox4x32_10(c, k0, k1), zc, zs);
+      gp_normal2((uint32_t)k, (uint32_t)p, (uint32_t)seg_id, g, k0, k1, zc[0], zs[0]);
+      gp_normal2((uint32_t)k, (uint32_t)p, (uint32_t)seg_id, g + 1, k0, k1, zc[1], zs[1]);
     }
+    if (r + 1 >= n_real) zc[1] = zs[1] = 0.0;
   }
   if (sd.kind == 0) {
     const double a = sd.amp[(int64_t)p * sd.nm + k];
     double* cp = coef + ((int64_t)p * K + sd.col0 + 2 * k) * R_pad + r;
-    cp[0] = a * zc;
-    cp[R_pad] = a * zs;
+    *(double2*)cp = make_double2(a * zc[0], a * zc[1]);
+    *(double2*)(cp + R_pad) = make_double2(a * zs[0], a * zs[1]);
   } else {
     double* zp = zbuf + ((int64_t)p * sd.nm + k) * 2 * R_pad + r;
-    zp[0] = zc;
-    zp[R_pad] = zs;
+    *(double2*)zp = make_double2(zc[0], zc[1]);
+    *(double2*)(zp + R_pad) = make_double2(zs[0], zs[1]);
   }
 }
 
@@ -456,12 +468,13 @@ __global__ __launch_bounds__(256) void k_seeds(const SegDesc* __restrict__ segs,
   seeds[(int64_t)s * n_toa + t] = make_double4(ch * cn, ch * sn, 2.0 * cn, ch);
 }
 
-// White-noise normal of (TOA t, global realization g): stream paired over realizations,
-// ctr = (t, 0xFFFFFFFF, 0xFFFFFFF0, g >> 1) -> (z for g even, z for g odd) (oracle:
-// white_normals_rpairs). A lane that owns TOA t uses both outputs of one Box-Muller.
+// White-noise normals of TOA t for the realization pair containing g (oracle quad_normals on the white stream):
+// (z for the even realization, z for the odd one), two of the four normals of one Philox call.
 __device__ __forceinline__ void white_pair(int64_t t, int64_t g, uint32_t k0, uint32_t k1, double& z0, double& z1) {
-  const u32x4 c = {(uint32_t)t, kWhitePsrWord, kWhiteStream, (uint32_t)(g >> 1)};
-  box_muller(philox4x32_10(c, k0, k1), z0, z1);
+  double z[4];
+  quad4((uint64_t)t & ~(uint64_t)1, kWhiteStream, (uint64_t)g & ~(uint64_t)1, k0, k1, z);
+  z0 = z[2 * (t & 1)];
+  z1 = z[2 * (t & 1) + 1];
 }
 
 // ----------------------------------------------------------------------------- k_synth_valu_seeded
@@ -616,10 +629,7 @@ __global__ __launch_bounds__(256) void k_white(const double* __restrict__ sigma,
     if (z) {
       zt = z[(int64_t)r * n_toa + t];
     } else {
-      const u32x4 c = {(uint32_t)(t >> 1), kWhitePsrWord, kWhiteStream, (uint32_t)(real0 + r)};
-      double z0, z1;
-      box_muller(philox4x32_10(c, k0, k1), z0, z1);
-      zt = (t & 1) ? z1 : z0;
+      zt = quad_normal((uint64_t)t, kWhiteStream, (uint64_t)(real0 + r), k0, k1);
     }
     v = sigma[t] * zt;
   }
@@ -630,10 +640,7 @@ __global__ __launch_bounds__(256) void k_white(const double* __restrict__ sigma,
       if (zb) {
         zbv = zb[b];
       } else {
-        const u32x4 c = {(uint32_t)(b >> 1), kWhitePsrWord, kEcorrStream, (uint32_t)(real0 + r)};
-        double z0, z1;
-        box_muller(philox4x32_10(c, k0, k1), z0, z1);
-        zbv = (b & 1) ? z1 : z0;
+        zbv = quad_normal((uint64_t)b, kEcorrStream, (uint64_t)(real0 + r), k0, k1);
       }
       v = fma(esig[b], zbv, v);
     }
@@ -642,19 +649,23 @@ __global__ __launch_bounds__(256) void k_white(const double* __restrict__ sigma,
 }
 
 // ----------------------------------------------------------------------------- batch white / ECORR
-// k_epoch_normals: zb[r][b] for every ECORR epoch, one Philox call per epoch pair (the ECORR
-// stream of the oracle). grid (ceil(ceil(n_blocks/2)/256), n_real).
-__global__ __launch_bounds__(256) void k_epoch_normals(int64_t n_blocks, int64_t real0, uint32_t k0, uint32_t k1,
-                                                       double* __restrict__ zb) {
+// k_epoch_normals: zb[r][b] for every ECORR epoch (oracle quad_normals on the ECORR stream), one Philox call per
+// (epoch pair, global realization pair): four normals. grid (ceil(ceil(n_blocks/2)/256), realization pairs touched).
+__global__ __launch_bounds__(256) void k_epoch_normals(int64_t n_blocks, int32_t n_real, int64_t real0, uint32_t k0,
+                                                       uint32_t k1, double* __restrict__ zb) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;  // epoch pair
-  const int r = blockIdx.y;
   if (2 * i >= n_blocks) return;
-  const u32x4 c = {(uint32_t)i, kWhitePsrWord, kEcorrStream, (uint32_t)(real0 + r)};
-  double z0, z1;
-  box_muller(philox4x32_10(c, k0, k1), z0, z1);
-  double* row = zb + (int64_t)r * n_blocks;
-  row[2 * i] = z0;
-  if (2 * i + 1 < n_blocks) row[2 * i + 1] = z1;
+  const int64_t g0 = ((real0 >> 1) + blockIdx.y) * 2;  // even global realization of this pair
+  double z[4];
+  quad4((uint64_t)(2 * i), kEcorrStream, (uint64_t)g0, k0, k1, z);
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int64_t r = g0 + h - real0;
+    if (r < 0 || r >= n_real) continue;
+    double* row = zb + r * n_blocks;
+    row[2 * i] = z[h];
+    if (2 * i + 1 < n_blocks) row[2 * i + 1] = z[2 + h];
+  }
 }
 
 // k_white_pairs: out[r][t] += sigma[t] z(t, real0 + r) + ecorr[b(t)] zb[r][b(t)], one thread per
@@ -848,7 +859,8 @@ __global__ void k_philox(int64_t n, const uint32_t* __restrict__ ctr, uint32_t k
 hipError_t launch_gen(hipStream_t st, const SegDesc& sd, int32_t seg_id, int32_t P, int32_t n_real,
                       int32_t R_pad, int64_t real0, uint32_t k0, uint32_t k1, const double* zin,
                       int32_t zin_nseg, int32_t zin_nm, double* coef, int32_t K, double* zbuf) {
-  dim3 grid((R_pad + 255) / 256, sd.nm, P);
+  if (R_pad % 2 != 0) return hipErrorInvalidValue;  // realization pairs
+  dim3 grid((R_pad / 2 + 255) / 256, sd.nm, P);
   hipLaunchKernelGGL(k_gen, grid, dim3(256), 0, st, sd, seg_id, P, n_real, R_pad, real0, k0, k1, zin,
                      zin_nseg, zin_nm, coef, K, zbuf);
   return hipGetLastError();
@@ -874,8 +886,9 @@ hipError_t launch_mix_tiled(hipStream_t st, const SegDesc& sd, int32_t P, int32_
 
 hipError_t launch_epoch_normals(hipStream_t st, int64_t n_blocks, int32_t n_real, int64_t real0, uint32_t k0,
                                 uint32_t k1, double* zb) {
-  hipLaunchKernelGGL(k_epoch_normals, dim3((unsigned)(((n_blocks + 1) / 2 + 255) / 256), n_real), dim3(256), 0, st,
-                     n_blocks, real0, k0, k1, zb);
+  const int64_t npairs = ((real0 + n_real + 1) >> 1) - (real0 >> 1);
+  hipLaunchKernelGGL(k_epoch_normals, dim3((unsigned)(((n_blocks + 1) / 2 + 255) / 256), (unsigned)npairs), dim3(256), 0,
+                     st, n_blocks, n_real, real0, k0, k1, zb);
   return hipGetLastError();
 }
 

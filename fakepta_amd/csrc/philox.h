@@ -44,10 +44,96 @@ __device__ __forceinline__ void box_muller(u32x4 v, double& z0, double& z1) {
   z1 = r * s;
 }
 
+// The build's uniform -> normal map (oracle: normals4, bm_log_u32, bm_sincos2pi_u32, operation for operation): two
+// Box-Muller pairs per Philox call from 32-bit uniforms u1 = (a + 1) 2^-32 in (0, 1], u2 = b 2^-32 in [0, 1), with
+// the logarithm and sine / cosine as fixed fp64 polynomials (~3e-14 relative): about half the VALU work per normal of
+// box_muller (one Philox call per two normals, library log and sincospi).
+__device__ __forceinline__ double bm_log_u32(uint32_t a) {
+  const double n = (double)a + 1.0;  // exact
+  int e;
+  double m = frexp(n, &e);  // n = m 2^e, m in [0.5, 1)
+  if (m < 0.7071067811865476) {
+    m *= 2.0;
+    e -= 1;
+  }
+  const double k = (double)(e - 32);
+  const double s = (m - 1.0) / (m + 1.0);
+  const double s2 = s * s;
+  const double p =
+      s2 * (1.0 / 3.0 +
+            s2 * (1.0 / 5.0 + s2 * (1.0 / 7.0 + s2 * (1.0 / 9.0 + s2 * (1.0 / 11.0 + s2 * (1.0 / 13.0 + s2 * (1.0 / 15.0)))))));
+  const double lm = 2.0 * s + 2.0 * s * p;
+  return k * 6.93147180369123816490e-01 + (k * 1.90821492927058770002e-10 + lm);
+}
+
+__device__ __forceinline__ void bm_sincos2pi_u32(uint32_t b, double& sn, double& cs) {
+  const double u = (double)b * 0x1.0p-32;  // [0, 1), exact
+  const double q = rint(4.0 * u);          // nearest quarter turn 0 .. 4
+  const double y = u - 0.25 * q;           // exact, [-1/8, 1/8]
+  const double a = y * 6.283185307179586;
+  const double x2 = a * a;
+  const double sa =
+      a + a * x2 *
+              (-1.0 / 6.0 +
+               x2 * (1.0 / 120.0 +
+                     x2 * (-1.0 / 5040.0 + x2 * (1.0 / 362880.0 + x2 * (-1.0 / 39916800.0 + x2 * (1.0 / 6227020800.0))))));
+  const double ca =
+      1.0 + x2 * (-1.0 / 2.0 +
+                  x2 * (1.0 / 24.0 +
+                        x2 * (-1.0 / 720.0 +
+                              x2 * (1.0 / 40320.0 +
+                                    x2 * (-1.0 / 3628800.0 + x2 * (1.0 / 479001600.0 + x2 * (-1.0 / 87178291200.0)))))));
+  const int qi = (int)q & 3;
+  sn = qi == 0 ? sa : (qi == 1 ? ca : (qi == 2 ? -sa : -ca));
+  cs = qi == 0 ? ca : (qi == 1 ? -sa : (qi == 2 ? -ca : sa));
+}
+
+// four standard normals of one Philox output: (z0, z1) from (x, y), (z2, z3) from (z, w)
+__device__ __forceinline__ void normals4(u32x4 v, double (&z)[4]) {
+  double s, c;
+  const double r0 = sqrt(-2.0 * bm_log_u32(v.x));
+  bm_sincos2pi_u32(v.y, s, c);
+  z[0] = r0 * c;
+  z[1] = r0 * s;
+  const double r1 = sqrt(-2.0 * bm_log_u32(v.z));
+  bm_sincos2pi_u32(v.w, s, c);
+  z[2] = r1 * c;
+  z[3] = r1 * s;
+}
+
+// GP coefficient normals (oracle gp_normals): ctr = (mode, pulsar, signal, g >> 1); realization g takes normals
+// 2 (g & 1), 2 (g & 1) + 1 as (cos, sin). gp_pair2: both realizations g, g + 1 of an even g from one call.
+__device__ __forceinline__ void gp_normal2(uint32_t k, uint32_t p, uint32_t seg, uint64_t g, uint32_t k0, uint32_t k1,
+                                           double& zc, double& zs) {
+  double z[4];
+  normals4(philox4x32_10({k, p, seg, (uint32_t)(g >> 1)}, k0, k1), z);
+  zc = (g & 1) ? z[2] : z[0];
+  zs = (g & 1) ? z[3] : z[1];
+}
+__device__ __forceinline__ void gp_pair2(uint32_t k, uint32_t p, uint32_t seg, uint64_t g_even, uint32_t k0,
+                                         uint32_t k1, double (&z)[4]) {
+  normals4(philox4x32_10({k, p, seg, (uint32_t)(g_even >> 1)}, k0, k1), z);
+}
+
 // Stream words for the non-GP draws (kept identical to the oracle).
 constexpr uint32_t kWhitePsrWord = 0xFFFFFFFFu;
 constexpr uint32_t kWhiteStream = 0xFFFFFFF0u;
 constexpr uint32_t kEcorrStream = 0xFFFFFFF1u;
 constexpr uint32_t kDenseStream = 0xFFFFFFF2u;  // dense-covariance draws (fpta_noise_draw)
 
+}  // namespace fpta
+
+namespace fpta {
+// One normal of an indexed stream paired over both index and realization (oracle quad_normals): ctr = (i >> 1,
+// 0xFFFFFFFF, stream, g >> 1), normal 2 (i & 1) + (g & 1). quad4: the four normals (i, g), (i, g + 1), (i + 1, g),
+// (i + 1, g + 1) of even i and g from one call.
+__device__ __forceinline__ double quad_normal(uint64_t i, uint32_t stream, uint64_t g, uint32_t k0, uint32_t k1) {
+  double z[4];
+  normals4(philox4x32_10({(uint32_t)(i >> 1), kWhitePsrWord, stream, (uint32_t)(g >> 1)}, k0, k1), z);
+  return z[2 * (i & 1) + (g & 1)];
+}
+__device__ __forceinline__ void quad4(uint64_t i_even, uint32_t stream, uint64_t g_even, uint32_t k0, uint32_t k1,
+                                      double (&z)[4]) {
+  normals4(philox4x32_10({(uint32_t)(i_even >> 1), kWhitePsrWord, stream, (uint32_t)(g_even >> 1)}, k0, k1), z);
+}
 }  // namespace fpta

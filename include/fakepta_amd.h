@@ -311,7 +311,7 @@ int fpta_comm_gather(fpta_comm* comm, const double* send, int64_t count, double*
 #define FPTA_OPT_INTERP_WS 15     /* gridded interpolation: 1 (default) the warp-specialised k_grid_interp_ws
                                      (producer waves stage the operands in an LDS ring, compute waves only store,
                                      so stores never delay an operand load) for blocks without fused white noise
-                                     or fused partial checksums;
+                                     or fused partial checksums; 2 also for blocks with fused partial checksums;
                                      0 the register-pipelined k_grid_interp_mfma. Results are identical. */
 #define FPTA_OPT_SIDE_SPLIT 16    /* pipelined gridded blocks (FPTA_OPT_OVERLAP): 1 (default) the grid signal with
                                      the largest DFT, when it has no common (ORF-mixed) member, is drawn and

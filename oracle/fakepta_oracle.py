@@ -351,7 +351,8 @@ def philox4x32_10(ctr, key):
 
 
 def box_muller(x):
-    """uint32 [..., 4] -> two standard normals [..., 2] (the build's fixed mapping):
+    """uint32 [..., 4] -> two standard normals [..., 2] with 53-bit uniforms (the round-1/2 mapping; kept for
+    reference and statistical comparison, no longer used by any stream):
     u1 = ((x0|x1<<32) >> 11) + 1) * 2^-53 in (0, 1], u2 = ((x2|x3<<32) >> 11) * 2^-53 in [0, 1),
     z0 = sqrt(-2 ln u1) cos(2 pi u2), z1 = sqrt(-2 ln u1) sin(2 pi u2)."""
     x = x.astype(np.uint64)
@@ -362,6 +363,69 @@ def box_muller(x):
     r = np.sqrt(-2.0 * np.log(u1))
     th = TWO_PI * u2
     return np.stack([r * np.cos(th), r * np.sin(th)], axis=-1)
+
+
+# The build's uniform -> normal map (philox.h normals4): two Box-Muller pairs per Philox call from 32-bit uniforms
+# u1 = (a + 1) 2^-32 in (0, 1], u2 = b 2^-32 in [0, 1) (as cuRAND's normal2), with the logarithm and the sine / cosine
+# evaluated by fixed fp64 polynomials that the device restates operation for operation (agreement to a few ulp; the
+# polynomials are accurate to ~3e-14 relative). |z| <= sqrt(64 ln 2) = 6.66.
+SQRT_HALF = 0.7071067811865476
+LN2_HI, LN2_LO = 6.93147180369123816490e-01, 1.90821492927058770002e-10
+_LOG_C = (1.0 / 3.0, 1.0 / 5.0, 1.0 / 7.0, 1.0 / 9.0, 1.0 / 11.0, 1.0 / 13.0, 1.0 / 15.0)
+_SIN_C = (-1.0 / 6.0, 1.0 / 120.0, -1.0 / 5040.0, 1.0 / 362880.0, -1.0 / 39916800.0, 1.0 / 6227020800.0)
+_COS_C = (-1.0 / 2.0, 1.0 / 24.0, -1.0 / 720.0, 1.0 / 40320.0, -1.0 / 3628800.0, 1.0 / 479001600.0,
+          -1.0 / 87178291200.0)
+
+
+def _horner(x, coefs):
+    acc = np.full_like(x, coefs[-1])
+    for c in coefs[-2::-1]:
+        acc = c + x * acc
+    return acc
+
+
+def bm_log_u32(a):
+    """log((a + 1) 2^-32) for uint32 a: frexp to m in [sqrt(1/2), sqrt(2)), log m = 2 atanh((m - 1) / (m + 1)) by its
+    series to s^15, plus (e - 32) ln 2 in two parts."""
+    n = np.asarray(a, dtype=np.uint32).astype(np.float64) + 1.0
+    m, e = np.frexp(n)
+    low = m < SQRT_HALF
+    m = np.where(low, 2.0 * m, m)
+    e = np.where(low, e - 1, e)
+    k = (e - 32).astype(np.float64)
+    sv = (m - 1.0) / (m + 1.0)
+    s2 = sv * sv
+    p = s2 * _horner(s2, _LOG_C)
+    lm = 2.0 * sv + 2.0 * sv * p
+    return k * LN2_HI + (k * LN2_LO + lm)
+
+
+def bm_sincos2pi_u32(b):
+    """(sin, cos)(2 pi b 2^-32): nearest quarter turn q, remainder a = 2 pi (u - q / 4) in [-pi/4, pi/4] by Taylor
+    polynomials (sin to a^13, cos to a^14), then the quadrant."""
+    u = np.asarray(b, dtype=np.uint32).astype(np.float64) * 2.0 ** -32
+    q = np.rint(4.0 * u)
+    y = u - 0.25 * q
+    a = y * TWO_PI
+    x2 = a * a
+    sa = a + a * x2 * _horner(x2, _SIN_C)
+    ca = 1.0 + x2 * _horner(x2, _COS_C)
+    qi = q.astype(np.int64) & 3
+    sn = np.select([qi == 0, qi == 1, qi == 2], [sa, ca, -sa], -ca)
+    cs = np.select([qi == 0, qi == 1, qi == 2], [ca, -sa, -ca], sa)
+    return sn, cs
+
+
+def normals4(x):
+    """uint32 [..., 4] (one Philox4x32-10 output) -> four standard normals [..., 4]: (z0, z1) from (x0, x1),
+    (z2, z3) from (x2, x3); z0 = r cos, z1 = r sin, r = sqrt(-2 log u1)."""
+    x = np.asarray(x, dtype=np.uint32)
+    out = []
+    for i in (0, 2):
+        r = np.sqrt(-2.0 * bm_log_u32(x[..., i]))
+        sn, cs = bm_sincos2pi_u32(x[..., i + 1])
+        out += [r * cs, r * sn]
+    return np.stack(out, axis=-1)
 
 
 # stream identifiers (counter word 1 / 2) for the non-GP draws
@@ -377,46 +441,46 @@ def seed_key(seed):
 
 
 def gp_normals(seed, reals, p, seg, n_modes):
-    """(z_cos, z_sin) for modes 0..N-1 of pulsar p, segment seg, global realizations `reals`:
-    ctr = (mode, pulsar, segment, realization). Returns [R, N, 2]."""
-    reals = np.asarray(reals, dtype=np.uint32)
+    """(z_cos, z_sin) for modes 0..N-1 of pulsar p, segment seg, global realizations `reals`: one Philox call per
+    (mode, pulsar, segment, realization pair), ctr = (mode, pulsar, segment, g >> 1); realization g takes normals
+    (2 (g & 1), 2 (g & 1) + 1) of it. Returns [R, N, 2]."""
+    reals = np.asarray(reals, dtype=np.uint64)
     k = np.arange(n_modes, dtype=np.uint32)
     ctr = np.zeros((len(reals), n_modes, 4), dtype=np.uint32)
     ctr[..., 0] = k[None, :]
     ctr[..., 1] = p
     ctr[..., 2] = seg
-    ctr[..., 3] = reals[:, None]
-    return box_muller(philox4x32_10(ctr, seed_key(seed)))
-
-
-def white_normals_rpairs(seed, reals, n_toa, stream=WHITE_STREAM):
-    """White-noise stream: one normal per (realization, TOA), paired over REALIZATIONS so a GPU lane
-    owning a TOA uses both outputs of one Box-Muller: ctr = (t, 0xFFFFFFFF, 0xFFFFFFF0, g >> 1),
-    pick [g & 1] for global realization g. Returns [len(reals), n_toa]."""
-    reals = np.asarray(reals, dtype=np.uint64)
-    t = np.arange(n_toa, dtype=np.uint64)
-    ctr = np.zeros((len(reals), n_toa, 4), dtype=np.uint32)
-    ctr[..., 0] = t.astype(np.uint32)[None, :]
-    ctr[..., 1] = WHITE_PSR_WORD
-    ctr[..., 2] = stream
     ctr[..., 3] = (reals >> np.uint64(1)).astype(np.uint32)[:, None]
-    z = box_muller(philox4x32_10(ctr, seed_key(seed)))
-    pick = (reals & np.uint64(1)).astype(np.int64)[:, None, None]
-    return np.take_along_axis(z, np.broadcast_to(pick, z.shape[:-1] + (1,)), axis=-1)[..., 0]
+    z = normals4(philox4x32_10(ctr, seed_key(seed)))  # [R, N, 4]
+    h = 2 * (reals & np.uint64(1)).astype(np.int64)[:, None, None]
+    return np.concatenate([np.take_along_axis(z, np.broadcast_to(h, z.shape[:-1] + (1,)), axis=-1),
+                           np.take_along_axis(z, np.broadcast_to(h + 1, z.shape[:-1] + (1,)), axis=-1)], axis=-1)
 
 
-def white_normals(seed, reals, n_toa, stream=WHITE_STREAM):
-    """one normal per (realization, index), paired over the index: ctr = (i >> 1, 0xFFFFFFFF,
-    stream, r), pick [i & 1]. Used for the ECORR epoch stream (index = epoch)."""
-    reals = np.asarray(reals, dtype=np.uint32)
-    t = np.arange(n_toa, dtype=np.uint64)
-    ctr = np.zeros((len(reals), n_toa, 4), dtype=np.uint32)
+def quad_normals(seed, reals, n, stream):
+    """One normal per (realization g, index i) from a stream paired over both: ctr = (i >> 1, 0xFFFFFFFF, stream,
+    g >> 1), normal 2 (i & 1) + (g & 1) of the call. White noise (index = TOA, WHITE_STREAM), ECORR epochs (index =
+    epoch, ECORR_STREAM) and the dense draws (index = TOA, DENSE_STREAM). Returns [len(reals), n]."""
+    reals = np.asarray(reals, dtype=np.uint64)
+    t = np.arange(n, dtype=np.uint64)
+    ctr = np.zeros((len(reals), n, 4), dtype=np.uint32)
     ctr[..., 0] = (t >> np.uint64(1)).astype(np.uint32)[None, :]
     ctr[..., 1] = WHITE_PSR_WORD
     ctr[..., 2] = stream
-    ctr[..., 3] = reals[:, None]
-    z = box_muller(philox4x32_10(ctr, seed_key(seed)))
-    return np.take_along_axis(z, (t & np.uint64(1)).astype(np.int64)[None, :, None], axis=-1)[..., 0]
+    ctr[..., 3] = (reals >> np.uint64(1)).astype(np.uint32)[:, None]
+    z = normals4(philox4x32_10(ctr, seed_key(seed)))
+    pick = 2 * (t & np.uint64(1)).astype(np.int64)[None, :] + (reals & np.uint64(1)).astype(np.int64)[:, None]
+    return np.take_along_axis(z, pick[..., None], axis=-1)[..., 0]
+
+
+def white_normals_rpairs(seed, reals, n_toa, stream=WHITE_STREAM):
+    """White-noise normals [len(reals), n_toa] (quad_normals on the white stream)."""
+    return quad_normals(seed, reals, n_toa, stream)
+
+
+def white_normals(seed, reals, n, stream=WHITE_STREAM):
+    """Normals of an indexed stream, e.g. the ECORR epochs (quad_normals)."""
+    return quad_normals(seed, reals, n, stream)
 
 
 # ----------------------------------------------------------------------------- batch semantics

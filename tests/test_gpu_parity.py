@@ -45,6 +45,23 @@ def test_philox_device_bit_exact(ctx):
     np.testing.assert_array_equal(ctx.debug_philox(ctr, key), O.philox4x32_10(ctr, key))
 
 
+def test_device_normals_match_oracle(ctx):
+    """The device's normal map (philox.h normals4: 32-bit Box-Muller with fp64 polynomials) restates the oracle's
+    operation for operation: coefficients downloaded from the batch path (amp * z, k_gen) equal the oracle's to
+    1e-13 relative, for an even and an odd first realization (the realization-pair straddle)."""
+    rng = np.random.default_rng(5)
+    offs, toas, nu = random_layout(rng, 3, (30, 60))
+    ctx.batch_set_toas(offs, toas, nu)
+    f, a = per_psr_signal(rng, offs, toas, 12)
+    ctx.batch_add_signal(0, f, a)
+    for real0 in (0, 7):
+        _, co = ctx.batch_synth(77, real0, 9, coeffs=True)  # [P][K][R]
+        for p in range(3):
+            z = O.gp_normals(77, np.arange(real0, real0 + 9), p, 0, 12)  # [R, N, 2]
+            want = np.transpose(a[p][None, :, None] * z, (1, 2, 0)).reshape(24, 9)
+            np.testing.assert_allclose(co[p], want, rtol=1e-13, atol=1e-13 * np.abs(want).max())
+
+
 # ----------------------------------------------------------------------------- drop-in kernels vs fixtures
 @pytest.mark.parametrize("lab", ["rn", "dm", "sv"])
 def test_gp_accumulate_vs_reference(ctx, golden, lab):

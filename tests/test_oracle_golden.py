@@ -140,6 +140,32 @@ def test_box_muller_moments():
     assert abs(w.mean()) < 0.01 and abs(w.std() - 1) < 0.01
 
 
+def test_normal_map_accuracy_and_moments():
+    """The build's uniform -> normal map (oracle.normals4, restated on the device by philox.h normals4): its fp64
+    polynomial log and sine / cosine agree with numpy's to 5e-14 over 2e6 random words and the end points, and
+    four normals per Philox call have the standard normal's moments and tails (|z| <= sqrt(64 ln 2))."""
+    a = np.random.default_rng(0).integers(0, 2 ** 32, size=2_000_000, dtype=np.uint64).astype(np.uint32)
+    a[:3] = [0, 0xFFFFFFFF, 1]
+    ref = np.log((a.astype(np.float64) + 1.0) * 2.0 ** -32)
+    got = O.bm_log_u32(a)
+    assert got[1] == 0.0 and np.max(np.abs(got - ref)) <= 5e-14 * np.max(np.abs(ref))
+    nz = ref != 0
+    assert np.max(np.abs(got[nz] - ref[nz]) / np.abs(ref[nz])) <= 5e-14
+    u = a.astype(np.float64) * 2.0 ** -32
+    sn, cs = O.bm_sincos2pi_u32(a)
+    assert np.max(np.abs(sn - np.sin(2 * np.pi * u))) <= 5e-14 and np.max(np.abs(cs - np.cos(2 * np.pi * u))) <= 5e-14
+    ctr = np.stack([np.arange(400_000, dtype=np.uint32), np.full(400_000, 7, np.uint32),
+                    np.full(400_000, 3, np.uint32), np.arange(400_000, dtype=np.uint32) // 3], -1)
+    z = O.normals4(O.philox4x32_10(ctr, np.array([11, 12], np.uint32)))
+    assert z.shape == (400_000, 4)
+    flat = z.ravel()
+    assert abs(flat.mean()) < 5e-3 and abs(flat.std() - 1) < 5e-3
+    assert abs(np.mean(flat ** 4) - 3.0) < 0.03 and np.max(np.abs(flat)) <= np.sqrt(64 * np.log(2)) + 1e-12
+    assert abs(np.mean(np.abs(flat) > 3) - 2.6998e-3) < 3e-4
+    c = np.corrcoef(z.T)
+    assert np.max(np.abs(c - np.eye(4))) < 5e-3
+
+
 def test_batch_semantics_match_reference_loop():
     """The batch layout (per-pulsar + common segment, explicit z) reproduces the loop-faithful
     reference restatements on the same draws."""
