@@ -37,7 +37,8 @@ FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 matrix (= vector) peak, AMD datasheet (M
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 SYNTH_KERNELS = {3: ("k_synth_valu_seeded<2,16>", "fp64-valu"), 2: ("k_synth_mfma<4,2>", "fp64-mfma"),
                  1: ("k_synth_direct", "fp64-valu")}
-GRID_INTERP = {0: ("k_grid_interp_mfma<false, false, 8>", "fp64-mfma"), 1: ("k_grid_interp_ws<false>", "fp64-mfma")}
+GRID_INTERP = {0: ("k_grid_interp_mfma<false, false, 8>", "fp64-mfma"), 1: ("k_grid_interp_ws<false>", "fp64-mfma"),
+               2: ("k_grid_interp_ws<false>", "fp64-mfma"), 3: ("k_grid_interp_ws2<false>", "fp64-mfma")}
 # layout tag of the gridded plan a PMC traffic record must carry to describe the shipped interpolation kernel
 # (32-TOA chunks, every grid signal's band back to back, coalesced signals); older tags describe earlier plans
 GRID_LAYOUT = "band32c"
@@ -65,6 +66,8 @@ def parse():
                     help="gridded interpolation kernel: 1 warp-specialised, 0 register-pipelined (-1: library default)")
     ap.add_argument("--overlap", type=int, default=-1,
                     help="FPTA_OPT_OVERLAP: 1 pipelined blocks (side stream), 0 one stream (-1: library default)")
+    ap.add_argument("--opt", action="append", default=[],
+                    help="library option NAME=VALUE (e.g. DFT_GEN=0, GEN_MIX=0, INTERP_WS=2) for A/B runs; repeatable")
     ap.add_argument("--exact-launches", type=int, default=5,
                     help="launches of the exact fused kernel (path 3) timed after the run for roofline_exact")
     ap.add_argument("--dist-backend", default="rccl", choices=("rccl", "gloo"),
@@ -338,6 +341,9 @@ def main():
         ctx.set_option(_capi.OPT_INTERP_WS, args.interp_ws)
     if args.overlap >= 0:
         ctx.set_option(_capi.OPT_OVERLAP, args.overlap)
+    for kv in args.opt:
+        name, val = kv.split("=")
+        ctx.set_option(getattr(_capi, "OPT_" + name.upper()), int(val))
 
     if args.config == "c2":
         R = args.real

@@ -191,6 +191,8 @@ struct fpta_ctx {
   int overlap = 1;
   int interp_ws = 1;      // gridded interpolation on the warp-specialised kernel (FPTA_OPT_INTERP_WS)
   int grid_coalesce = 1;  // gridded path: signals sharing w0 and the chromatic weight share one grid (FPTA_OPT_GRID_COALESCE)
+  int async_sums = 0;    // streamed jobs: partial-checksum reductions on their own stream (FPTA_OPT_ASYNC_SUMS; measured
+                         // no faster on C3, profiles/r03h_ab.txt: the reductions then compete with the interpolation)
   int gen_mix = 1;       // common signals of 64..256 pulsars: draws and ORF mixing in one kernel (k_gen_mix,
                          // FPTA_OPT_GEN_MIX); 0 k_gen into zbuf, then k_mix_mfma
   int dft_gen = 1;       // gridded path: grid signals with a per-pulsar member draw their coefficients inside the DFT
@@ -1296,7 +1298,9 @@ int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad, bool pipe = fa
                 G.grid_rows};
   // the warp-specialised kernel for plain blocks; with fused partial checksums its reduce-scatter temporaries take
   // its VGPRs to 230 and the register kernel is faster (C3: 47.9 vs 52.5 ms per job, profiles/r02k_ab_c2c3_ws.txt)
-  if (c->interp_ws && !c->interp_lds && !a.w_on && !a.accumulate && (!a.part || c->interp_ws == 2)) {
+  if (c->interp_ws == 3 && !c->interp_lds && !a.w_on && !a.accumulate && !a.part) {
+    HIPCHK(c, launch_grid_interp_ws(c->stream, a, band, R_pad, true), "k_grid_interp_ws2 launch");
+  } else if (c->interp_ws && !c->interp_lds && !a.w_on && !a.accumulate && (!a.part || c->interp_ws == 2)) {
     HIPCHK(c, launch_grid_interp_ws(c->stream, a, band, R_pad), "k_grid_interp_ws launch");
   } else if (c->interp_lds && G.lds_ok && !a.w_on) {
     GridLds lds{G.groups.as<int4>(), G.urows.as<int32_t>(), G.lrows.as<int32_t>(), G.n_groups, G.lds_rows};
@@ -1702,12 +1706,15 @@ int fpta_set_option(fpta_ctx* c, int32_t key, int64_t value) {
     case FPTA_OPT_GEN_MIX:
       c->gen_mix = value ? 1 : 0;
       return FPTA_OK;
+    case FPTA_OPT_ASYNC_SUMS:
+      c->async_sums = value ? 1 : 0;
+      return FPTA_OK;
     case FPTA_OPT_GRID_COALESCE:
       c->grid_coalesce = value ? 1 : 0;
       c->batch.grid.clear();
       return FPTA_OK;
     case FPTA_OPT_INTERP_WS:
-      if (value < 0 || value > 2) return fail(c, FPTA_EINVAL, "interp_ws must be 0, 1 or 2");
+      if (value < 0 || value > 3) return fail(c, FPTA_EINVAL, "interp_ws must be 0 .. 3");
       c->interp_ws = (int)value;
       return FPTA_OK;
     case FPTA_OPT_SIDE_SPLIT:
@@ -1752,6 +1759,7 @@ int fpta_get_option(fpta_ctx* c, int32_t key, int64_t* value) {
     case FPTA_OPT_SIDE_SPLIT: *value = c->side_split; return FPTA_OK;
     case FPTA_OPT_DFT_GEN: *value = c->dft_gen; return FPTA_OK;
     case FPTA_OPT_GEN_MIX: *value = c->gen_mix; return FPTA_OK;
+    case FPTA_OPT_ASYNC_SUMS: *value = c->async_sums; return FPTA_OK;
   }
   return fail(c, FPTA_EINVAL, "get_option: unknown key");
 }
@@ -2399,7 +2407,7 @@ int multi_fail(fpta_multi* m, int i, int rc) {
 // red stream beside the next block when the interpolation wrote partials, else on the ctx stream.
 int checksums_async(fpta_ctx* c, double* dst, bool d2d = false) {
   hipStream_t st = nullptr;
-  int rc = launch_block_checksums(c, true, &st);
+  int rc = launch_block_checksums(c, c->async_sums != 0, &st);
   if (rc) return rc;
   HIPCHK(c,
          hipMemcpyAsync(dst, c->sums.p, sizeof(double) * 2 * c->out_R,

@@ -156,7 +156,9 @@ struct GridBand {
 hipError_t launch_grid_interp_mfma(hipStream_t st, const SynthArgs& a, const GridBand& band, int32_t R_pad);
 // Warp-specialised variant (producer waves stage operands in an LDS ring, compute waves never load from global memory,
 // so their stores never hold up an operand); no white epilogue, no accumulate
-hipError_t launch_grid_interp_ws(hipStream_t st, const SynthArgs& a, const GridBand& band, int32_t R_pad);
+// ws2: k_grid_interp_ws2 (64-realization compute tiles, two workgroups per CU), plain blocks only
+hipError_t launch_grid_interp_ws(hipStream_t st, const SynthArgs& a, const GridBand& band, int32_t R_pad,
+                                 bool ws2 = false);
 // LDS-staged variant: the 4 waves of a workgroup take <= kLdsGroup consecutive chunks of one pulsar for the same
 // realizations; the union of their band rows (<= kLdsRowsMax) is loaded once into LDS
 constexpr int kLdsGroup = 4, kLdsRowsMax = 144;

@@ -324,6 +324,9 @@ int fpta_comm_gather(fpta_comm* comm, const double* send, int64_t count, double*
 #define FPTA_OPT_GEN_MIX 18       /* common signals of 64..256 pulsars (fp64 MFMA mixing): 1 (default) draws and ORF
                                      mixing in one kernel (k_gen_mix: normals in LDS, no zbuf round trip); 0 k_gen then
                                      k_mix_mfma. Same draws and products; results identical. */
+#define FPTA_OPT_ASYNC_SUMS 19    /* streamed jobs (fpta_batch_synth_checksums, fpta_multi_synth): 1 a block's partial
+                                     checksums are reduced on a stream of their own, beside the next block, into one
+                                     of two partials buffers; 0 (default) on the context stream. Identical results. */
 int fpta_set_option(fpta_ctx* ctx, int32_t key, int64_t value);
 /* Current value of option `key` (same keys as fpta_set_option). */
 int fpta_get_option(fpta_ctx* ctx, int32_t key, int64_t* value);

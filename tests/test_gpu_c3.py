@@ -132,3 +132,18 @@ def test_tail_batch_below_mfma_min_real_is_split_invariant(c3):
         np.testing.assert_array_equal(m.synth_checksums(SEED, 11 + 4000, 40, batch=7), want[4000:4040])
     finally:
         m.close()
+
+
+def test_async_partial_reductions_are_bitwise_identical(c3):
+    """FPTA_OPT_ASYNC_SUMS: reducing each block's partial checksums on a stream of their own (two partials buffers,
+    beside the next block) returns the same checksums as on the context stream, in-library and two-context driver."""
+    from fakepta_amd import _capi
+    psrs, sim, ctx = c3
+    try:
+        res = {}
+        for asy in (0, 1):
+            ctx.set_option(_capi.OPT_ASYNC_SUMS, asy)
+            res[asy] = ctx.batch_synth_checksums(SEED, 99, 9000, batch=2048)
+        np.testing.assert_array_equal(res[0], res[1])
+    finally:
+        ctx.set_option(_capi.OPT_ASYNC_SUMS, 0)

@@ -449,17 +449,17 @@ def test_warp_specialised_interpolation_is_bitwise_identical(ctx, capi, shipped,
         ctx.set_option(capi.OPT_SYNTH_PATH, 4)
         ctx.set_option(capi.OPT_FUSE_CHECKSUMS, fuse)
         res = {}
-        for ws in (0, 1, 2):  # 2: the warp-specialised kernel also for fused-checksum blocks
+        for ws in (0, 1, 2, 3):  # 2: WS also for fused-checksum blocks; 3: k_grid_interp_ws2 (two workgroups per CU)
             ctx.set_option(capi.OPT_INTERP_WS, ws)
             res[ws] = (ctx.batch_synth(5, 300, R), ctx.batch_checksums())
-        for ws in (1, 2):
+        for ws in (1, 2, 3):
             np.testing.assert_array_equal(res[0][0], res[ws][0])
             np.testing.assert_array_equal(res[0][1], res[ws][1])
     finally:
         ctx.set_options(shipped)
 
 
-@pytest.mark.parametrize("ws", [0, 1, 2])
+@pytest.mark.parametrize("ws", [0, 1, 2, 3])
 @pytest.mark.parametrize("R", [1100, 1696])
 def test_partial_realization_blocks_write_every_sample(ctx, capi, shipped, ws, R):
     """Regression: R_pad not a multiple of 512 (a C3 shard's last batch of 1696) gives persistent interpolation
