@@ -1,6 +1,6 @@
 """Timings of the BASELINE configs other than the driver's headline (bench.py = C2), one GPU.
 
-    python tools/bench_configs.py [c1] [c3] [c4] [c5] [--c3-real 100000]
+    python tools/bench_configs.py [c1] [c3] [c4] [c5] [--c3-real 100000] [--opt NAME=VALUE ...]
 
 c1  make_fake_array(25 psr, Tobs 10, ntoas 1000, gaps, RN30) drop-in latency, seed 0
     (the reference: 0.045 s on the survey container's CPU)
@@ -21,6 +21,17 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+
+
+OPTS = []  # --opt NAME=VALUE: library options set on every context a config creates (A/B runs)
+
+
+def new_context(capi):
+    ctx = capi.Context(0)
+    for kv in OPTS:
+        name, val = kv.split("=")
+        ctx.set_option(getattr(capi, "OPT_" + name.upper()), int(val))
+    return ctx
 
 
 def kernel_times(ctx, capi, steps):
@@ -90,7 +101,7 @@ def c3(total):
     from fakepta_amd import _capi
     from fakepta import correlated_noises as cn
     from fakepta_amd.batch import BatchSimulator
-    ctx = _capi.Context(0)
+    ctx = new_context(_capi)
     psrs = bench.build_array(100, 2000, "c2")
     sim = BatchSimulator(psrs, signals=["gw_common"], white=False, ctx=ctx)
     B = 4096
@@ -116,7 +127,7 @@ def c3(total):
 def c4():
     from fakepta_amd import _capi
     from oracle import fakepta_oracle as O  # host-side ORF/PSD helpers only (setup, untimed)
-    ctx = _capi.Context(0)
+    ctx = new_context(_capi)
     P, n_p, N, R = 1000, 10000, 100, 256
     rng = np.random.default_rng(0)
     T = 10 * O.JULIAN_YEAR
@@ -153,7 +164,7 @@ def c5():
     from fakepta import correlated_noises as cn
     from fakepta import fake_pta as fp
     from fakepta_amd.batch import BatchSimulator
-    ctx = _capi.Context(0)
+    ctx = new_context(_capi)
     P = 100
     np.random.seed(7)
     pos = fib(P)
@@ -187,7 +198,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("configs", nargs="*", default=["c1", "c3", "c4", "c5"])
     ap.add_argument("--c3-real", type=int, default=100000)
+    ap.add_argument("--opt", action="append", default=[], help="library option NAME=VALUE (e.g. INTERP_WS=4)")
     args = ap.parse_args()
+    OPTS.extend(args.opt)
     for c in args.configs:
         res = c3(args.c3_real) if c == "c3" else globals()[c]()
         print(json.dumps(res), flush=True)
