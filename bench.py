@@ -37,8 +37,16 @@ FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 matrix (= vector) peak, AMD datasheet (M
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 SYNTH_KERNELS = {3: ("k_synth_valu_seeded<2,16>", "fp64-valu"), 2: ("k_synth_mfma<4,2>", "fp64-mfma"),
                  1: ("k_synth_direct", "fp64-valu")}
-GRID_INTERP = {0: ("k_grid_interp_mfma<false, false, 8>", "fp64-mfma"), 1: ("k_grid_interp_ws<false>", "fp64-mfma"),
-               2: ("k_grid_interp_ws<false>", "fp64-mfma"), 3: ("k_grid_interp_ws2<false>", "fp64-mfma")}
+
+
+def grid_interp_kernel(ws, part):
+    """Name of the interpolation kernel FPTA_OPT_INTERP_WS = ws launches for plain (C2) or fused-checksum (C3) blocks."""
+    p = "true" if part else "false"
+    reg = f"k_grid_interp_mfma<false, {p}, 8>"
+    return {0: reg, 1: reg if part else "k_grid_interp_ws<false>", 2: f"k_grid_interp_ws<{p}>",
+            3: reg if part else "k_grid_interp_ws2<false>"}[ws]
+
+
 # layout tag of the gridded plan a PMC traffic record must carry to describe the shipped interpolation kernel
 # (32-TOA chunks, every grid signal's band back to back, coalesced signals); older tags describe earlier plans
 GRID_LAYOUT = "band32c"
@@ -394,9 +402,7 @@ def main():
     out_bytes = 8.0 * info["n_toa"] * n_launch_real
     if path == 4:
         # the warp-specialised kernel serves plain blocks; fused-checksum blocks (c3) take the register kernel
-        kernel, pipe = GRID_INTERP[ctx.get_option(_capi.OPT_INTERP_WS) if args.config == "c2" else 0]
-        if args.config != "c2":
-            kernel = kernel.replace("false, false", "false, true")
+        kernel, pipe = grid_interp_kernel(ctx.get_option(_capi.OPT_INTERP_WS), args.config != "c2"), "fp64-mfma"
         traffic, traffic_src = pmc_traffic(kernel, info, R, args.traffic, GRID_LAYOUT)
         achieved = out_bytes / synth_avg_s / 1e9
         R_pad = -(-int(n_launch_real) // 128) * 128

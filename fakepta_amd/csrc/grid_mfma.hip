@@ -439,10 +439,29 @@ __device__ __forceinline__ void interp_white(const SynthArgs& a, const InterpTil
     ep[e] = a.w_block_of ? a.w_block_of[tg + e] : -1;
     es[e] = ep[e] >= 0 ? a.w_esig[ep[e]] : 0.0;
   }
+  // ECORR epoch normals of group (m, g), loaded one group ahead so their latency hides behind a group's Philox rounds
+  // (one group at a time, each waiting for its own loads, left the tile's 16 gathers' latencies exposed). The loads are
+  // unconditional: rows past n_real are clamped (those realizations are never stored) and a TOA without an epoch reads
+  // epoch 0 against es = 0.
+  const bool ecorr = a.w_block_of != nullptr;
+  const int64_t e0 = ep[0] >= 0 ? ep[0] : 0, e1 = ep[1] >= 0 ? ep[1] : 0;
+  auto zb_load = [&](int mg, double (&z)[2][2]) {
+    const int rl = t.r0 + 32 * (mg >> 2) + 2 * (lg + 4 * (mg & 3));
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const double* row = a.w_zb + (int64_t)min(rl + h, a.n_real - 1) * a.w_nblocks;
+      z[0][h] = row[e0];
+      z[1][h] = row[e1];
+    }
+  };
+  double zc[2][2] = {{0.0, 0.0}, {0.0, 0.0}}, zn[2][2] = {{0.0, 0.0}, {0.0, 0.0}};
+  if (ecorr) zb_load(0, zc);
 #pragma unroll
   for (int m = 0; m < NP; ++m) {
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
+      const int mg = 4 * m + g;
+      if (ecorr && mg + 1 < 4 * NP) zb_load(mg + 1, zn);
       // acc[e][2m + h][g]: TOA tg + e, batch realization rl + h
       const int rl = t.r0 + 32 * m + 2 * (lg + 4 * g);
       if (a.w_sigma) {
@@ -453,15 +472,17 @@ __device__ __forceinline__ void interp_white(const SynthArgs& a, const InterpTil
 #pragma unroll
           for (int h = 0; h < 2; ++h) acc[e][2 * m + h][g] = fma(sg[e], z[2 * e + h], acc[e][2 * m + h][g]);
       }
+      if (ecorr) {
 #pragma unroll
-      for (int e = 0; e < 2; ++e)
-        if (ep[e] >= 0) {
+        for (int e = 0; e < 2; ++e)
 #pragma unroll
-          for (int h = 0; h < 2; ++h)
-            if (rl + h < a.n_real)
-              acc[e][2 * m + h][g] = fma(es[e], a.w_zb[(int64_t)(rl + h) * a.w_nblocks + ep[e]], acc[e][2 * m + h][g]);
-        }
-      // one (m, g) group at a time: no Philox state or epoch-normal loads hoisted across groups (register budget)
+          for (int h = 0; h < 2; ++h) acc[e][2 * m + h][g] = fma(es[e], zc[e][h], acc[e][2 * m + h][g]);
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+#pragma unroll
+          for (int h = 0; h < 2; ++h) zc[e][h] = zn[e][h];
+      }
+      // one (m, g) group at a time: no Philox state hoisted across groups (register budget)
       __builtin_amdgcn_sched_barrier(0);
     }
   }
