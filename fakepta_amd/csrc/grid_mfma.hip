@@ -48,6 +48,12 @@ __device__ __forceinline__ int4 ld_uniform4(const void* p) {
 constexpr int kInterpRW = FPTA_INTERP_RW;
 constexpr int kInterpDepth = FPTA_INTERP_DEPTH;  // k_grid_interp_mfma: steps of operand prefetch (2 or 3)
 constexpr int kInterpWPC = FPTA_INTERP_WPC;
+#ifndef FPTA_WHITE_WPC
+#define FPTA_WHITE_WPC 2  // persistent workgroups per CU of the white-epilogue interpolation
+#endif
+#ifndef FPTA_ECORR_AHEAD
+#define FPTA_ECORR_AHEAD 1  // white / ECORR epilogue: groups of epoch normals loaded ahead (1 or 2)
+#endif
 
 // ----------------------------------------------------------------------------- k_grid_dft_mfma
 // Quarter-range real DFT (one radix-2 step, then GEMMs): with nf = 4 Q and theta = 2 pi k j / nf, the modes of odd k
@@ -439,7 +445,7 @@ __device__ __forceinline__ void interp_white(const SynthArgs& a, const InterpTil
     ep[e] = a.w_block_of ? a.w_block_of[tg + e] : -1;
     es[e] = ep[e] >= 0 ? a.w_esig[ep[e]] : 0.0;
   }
-  // ECORR epoch normals of group (m, g), loaded one group ahead so their latency hides behind a group's Philox rounds
+  // ECORR epoch normals of group (m, g), loaded FPTA_ECORR_AHEAD groups ahead so their latency hides behind a group's Philox rounds
   // (one group at a time, each waiting for its own loads, left the tile's 16 gathers' latencies exposed). The loads are
   // unconditional: rows past n_real are clamped (those realizations are never stored) and a TOA without an epoch reads
   // epoch 0 against es = 0.
@@ -454,14 +460,17 @@ __device__ __forceinline__ void interp_white(const SynthArgs& a, const InterpTil
       z[1][h] = row[e1];
     }
   };
-  double zc[2][2] = {{0.0, 0.0}, {0.0, 0.0}}, zn[2][2] = {{0.0, 0.0}, {0.0, 0.0}};
-  if (ecorr) zb_load(0, zc);
+  constexpr int D = FPTA_ECORR_AHEAD;  // groups of epoch normals in flight ahead of the one being added
+  double zq[D + 1][2][2];
+  if (ecorr)
+#pragma unroll
+    for (int i = 0; i < D; ++i) zb_load(i, zq[i]);
 #pragma unroll
   for (int m = 0; m < NP; ++m) {
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const int mg = 4 * m + g;
-      if (ecorr && mg + 1 < 4 * NP) zb_load(mg + 1, zn);
+      if (ecorr && mg + D < 4 * NP) zb_load(mg + D, zq[(mg + D) % (D + 1)]);
       // acc[e][2m + h][g]: TOA tg + e, batch realization rl + h
       const int rl = t.r0 + 32 * m + 2 * (lg + 4 * g);
       if (a.w_sigma) {
@@ -476,11 +485,7 @@ __device__ __forceinline__ void interp_white(const SynthArgs& a, const InterpTil
 #pragma unroll
         for (int e = 0; e < 2; ++e)
 #pragma unroll
-          for (int h = 0; h < 2; ++h) acc[e][2 * m + h][g] = fma(es[e], zc[e][h], acc[e][2 * m + h][g]);
-#pragma unroll
-        for (int e = 0; e < 2; ++e)
-#pragma unroll
-          for (int h = 0; h < 2; ++h) zc[e][h] = zn[e][h];
+          for (int h = 0; h < 2; ++h) acc[e][2 * m + h][g] = fma(es[e], zq[mg % (D + 1)][e][h], acc[e][2 * m + h][g]);
       }
       // one (m, g) group at a time: no Philox state hoisted across groups (register budget)
       __builtin_amdgcn_sched_barrier(0);
@@ -1335,7 +1340,7 @@ hipError_t launch_grid_interp_mfma(hipStream_t st, const SynthArgs& a, const Gri
   }
   // persistent grid: kInterpWPC workgroups per CU (16-TOA tiles, profiles/r01_sweep_interp_wpc.txt: 1 -> 1.06 ms,
   // 2 -> 0.74, 3 -> 0.81; 32-TOA tiles: profiles/r02_interp_variants.txt)
-  const int64_t want = (int64_t)n_cu * kInterpWPC;
+  const int64_t want = (int64_t)n_cu * (a.w_on ? FPTA_WHITE_WPC : kInterpWPC);
   const int64_t grid = std::min<int64_t>((tiles + 7) / 8 * 8, (want + 7) / 8 * 8);
   // partial checksums are a separate instantiation: their reduce-scatter registers never weigh on the plain kernel
   auto kernel = a.w_on ? (a.part ? k_grid_interp_mfma<true, true, RW> : k_grid_interp_mfma<true, false, RW>)

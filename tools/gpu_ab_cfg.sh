@@ -2,7 +2,8 @@
 # A/B of library options on one box, for C2 / C3 (bench.py) and C4 / C5 (tools/bench_configs.py), alternating variants,
 # two repetitions; optional GPU test selection first.
 #   bash tools/gpu_ab_cfg.sh <tag> "<pytest -k expr or empty>" <c2|c3|c4|c5> "<opts 1>" "<opts 2>" ...
-# opts are NAME=VALUE library options separated by spaces ("" = the library defaults).
+# opts are NAME=VALUE library options separated by spaces ("" = the library defaults); LIB=<path.so> runs that variant
+# on another build of the library (make -C fakepta_amd/csrc variant ...).
 set -o pipefail
 tag=$1; kexpr=$2; cfg=$3; shift 3
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
@@ -17,7 +18,11 @@ for rep in 1 2; do
   i=0
   for v in "$@"; do
     flags=""
-    for kv in $v; do flags="$flags --opt $kv"; done
+    lib=fakepta_amd/lib/libfakepta_amd.so
+    for kv in $v; do
+      case $kv in LIB=*) lib=${kv#LIB=} ;; *) flags="$flags --opt $kv" ;; esac
+    done
+    export FAKEPTA_AMD_LIB=$lib
     log=gpurun_out/${tag}_${cfg}_v${i}_r$rep.log
     case $cfg in
       c2) timeout -k 10 300 python -u bench.py --cpu-sample 0 --steps 30 --exact-launches 3 $flags > $log 2>&1 ;;
