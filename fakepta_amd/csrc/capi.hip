@@ -192,7 +192,7 @@ struct fpta_ctx {
   int interp_ws = 1;      // gridded interpolation on the warp-specialised kernel (FPTA_OPT_INTERP_WS)
   int grid_coalesce = 1;  // gridded path: signals sharing w0 and the chromatic weight share one grid (FPTA_OPT_GRID_COALESCE)
   int async_sums = 0;    // streamed jobs: partial-checksum reductions on their own stream (FPTA_OPT_ASYNC_SUMS; measured
-                         // no faster on C3, profiles/r03h_ab.txt: the reductions then compete with the interpolation)
+                         // no faster on C3, profiles/r03h_ab_c3_async_sums.txt: the reductions then compete with the interpolation)
   int gen_mix = 1;       // common signals of 64..256 pulsars: draws and ORF mixing in one kernel (k_gen_mix,
                          // FPTA_OPT_GEN_MIX); 0 k_gen into zbuf, then k_mix_mfma
   int dft_gen = 1;       // gridded path: grid signals with a per-pulsar member draw their coefficients inside the DFT

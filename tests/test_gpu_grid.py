@@ -5,7 +5,8 @@ phase grid (real DFT) and a banded exponential-of-semicircle interpolation (DESI
 It is an approximation with a bounded aliasing error: at the shipped defaults (width 15,
 oversampling 1.5; a-priori bound exp(-pi w sqrt(1 - 1/sigma)) = 1.5e-12) the error is <= ~6e-12
 relative for a FLAT spectrum (every mode weighs equally, the worst case) and smaller for red
-spectra (width 14 reached 3.2e-11 on these cases: profiles/r02_gputest1.log). Tolerance: the suite's
+spectra (width 14 reaches 3.1e-11 on these cases: tools/grid_width_errors.py, profiles/r03l_grid_width_errors.jsonl).
+Tolerance: the suite's
 1e-10; the accuracy tests below also check the tighter bound GRID_TOL the defaults are
 designed for, AT the shipped defaults (the fixture restores the context's own options after every test
 instead of writing fixed values).
