@@ -557,8 +557,10 @@ __device__ __forceinline__ void interp_partials(const SynthArgs& a, const Interp
     }
     const int mm = lr >> 2, gg = lr & 3;
     const int rl = 32 * mm + 2 * (lg + 4 * gg);  // realization of (tile 2mm, register gg); rl + 1: tile 2mm + 1
-    *(dbl2*)(pp + 2 * rl) = dbl2{x[0], x[1]};
-    *(dbl2*)(pp + 2 * rl + 2) = dbl2{x[2], x[3]};
+    // non-temporal, as the block's own stores: the partials are read back by k_part_reduce from HBM (0.41 GB per
+    // C3 batch), and L2-allocating them would evict the grid rows the next chunks re-read
+    __builtin_nontemporal_store(dbl2{x[0], x[1]}, (dbl2*)(pp + 2 * rl));
+    __builtin_nontemporal_store(dbl2{x[2], x[3]}, (dbl2*)(pp + 2 * rl + 2));
   }
 }
 
