@@ -16,7 +16,7 @@ import json, sys
 d = json.loads([l for l in open(sys.argv[1]) if l.startswith("{")][0])
 r = d["roofline"]
 print("C2", round(d["value"] / 1e11, 3), "e11 samples/s", round(d["ms_per_step"], 4), "ms/step; interp", round(r["avg_launch_ms"], 4),
-      "iso", r.get("isolated", {}).get("avg_launch_ms"), "dft iso", r.get("isolated", {}).get("dft_avg_launch_ms"))
+      "iso", r.get("isolated", {}).get("avg_launch_ms"), "dft iso", r.get("isolated", {}).get("dft_ms_per_block"))
 PY
 for c in "$@"; do
   if [ "$c" = c3 ]; then

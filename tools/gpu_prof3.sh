@@ -7,7 +7,7 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 o=gpurun_out/$tag
 timeout -k 10 300 python -u bench.py --cpu-sample 0 --steps 30 "$@" > ${o}_bench.log 2>&1 || { tail -20 ${o}_bench.log; exit 1; }
-grep '^{' ${o}_bench.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']; print('C2', d['value'], d['ms_per_step'], 'interp', r['avg_launch_ms'], 'iso', r.get('isolated',{}).get('avg_launch_ms'), r.get('isolated',{}).get('dft_avg_launch_ms'))"
+grep '^{' ${o}_bench.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']; print('C2', d['value'], d['ms_per_step'], 'interp', r['avg_launch_ms'], 'iso', r.get('isolated',{}).get('avg_launch_ms'), r.get('isolated',{}).get('dft_ms_per_block'))"
 for ov in 1 0; do
   timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d ${o}_c2ov$ov -o run -- python bench.py --steps 12 --cpu-sample 0 --exact-launches 0 --overlap $ov "$@" > ${o}_c2ov$ov.log 2>&1 || { tail -20 ${o}_c2ov$ov.log; exit 1; }
   echo "== C2 overlap $ov"; python tools/trace_steps.py ${o}_c2ov$ov/run_kernel_trace.csv --last 8
