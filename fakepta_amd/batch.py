@@ -39,7 +39,14 @@ def batch_factor(orf_mat):
     try:
         return np.ascontiguousarray(np.linalg.cholesky(orf_mat))
     except np.linalg.LinAlgError:
-        return orf_factor(orf_mat)
+        # singular ORF (monopole: rank 1, dipole: rank 3): the SVD factor with the directions of numerically zero
+        # variance (singular values <= 1e-12 of the largest, i.e. rounding noise of a rank-r matrix) set to exact
+        # zeros, so the device mixes (and draws normals for) only the first r columns; L L^T changes by <= 1e-12
+        # relative
+        _, s, _ = np.linalg.svd(orf_mat)
+        L = orf_factor(orf_mat)
+        L[:, s <= 1e-12 * s[0]] = 0.0
+        return np.ascontiguousarray(L)
 
 
 class BatchSimulator:

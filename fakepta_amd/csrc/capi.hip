@@ -469,6 +469,15 @@ int layout_add_signal(fpta_ctx* c, Layout& L, int32_t kind, int32_t nm, const do
           break;
         }
     d.l_lower = low ? 1 : 0;
+    // trailing all-zero columns of L (exact zeros): skipping them changes no sum
+    int32_t nq = 0;
+    for (int32_t p = 0; p < P; ++p)
+      for (int32_t q = P - 1; q >= nq; --q)
+        if (Lmat[(size_t)p * P + q] != 0.0) {
+          nq = q + 1;
+          break;
+        }
+    d.n_q = std::max(nq, 1);
   }
   L.K += 2 * nmp;
   L.segs.push_back(s);

@@ -21,6 +21,8 @@ struct SegDesc {
   int32_t col0;         // first coefficient column of this segment (cos of mode 0)
   int32_t harmonic;     // 1: w[k] == (k+1) w[0] to rounding -> angle-addition recurrence
   int32_t l_lower;      // kind 1: L is lower-triangular (Cholesky factor) -> triangular mixing
+  int32_t n_q;          // kind 1: columns of L up to its last nonzero one (a rank-r factor of a singular ORF, e.g.
+                        // monopole r = 1, dipole r = 3): the mix sums q < n_q and draws no normals past them
 };
 
 struct SynthArgs {

@@ -1376,7 +1376,8 @@ __device__ __forceinline__ dbl2 add_rounded_product(dbl2 o, double a, double v0,
 template <int NU, int NB, int OCC>
 __global__ __launch_bounds__(256, OCC) void k_mix_mfma(const double* __restrict__ LT, int32_t lt_ld,
                                                      const double* __restrict__ amp, int32_t P, int64_t M,
-                                                     int32_t R_pad, int32_t lower, int32_t n_pt, int32_t n_cb,
+                                                     int32_t R_pad, int32_t lower, int32_t n_q, int32_t n_pt,
+                                                     int32_t n_cb,
                                                      const double* __restrict__ zbuf, double* __restrict__ coef,
                                                      int32_t K, int32_t col0, double* __restrict__ x_out,
                                                      int32_t add_into) {
@@ -1389,7 +1390,7 @@ __global__ __launch_bounds__(256, OCC) void k_mix_mfma(const double* __restrict_
   const int lr = lane & 15, lg = lane >> 4;
   const int p0 = pt * 32 * NU;
   const int64_t m0 = ((int64_t)cb * 4 + wave) * 32 * NB;
-  const int qend = lower ? min(P, p0 + 32 * NU) : P;
+  const int qend = min(lower ? min(P, p0 + 32 * NU) : P, n_q);
   d4 acc[2 * NU][2 * NB];
 #pragma unroll
   for (int u = 0; u < 2 * NU; ++u)
@@ -1474,7 +1475,7 @@ __global__ __launch_bounds__(512) void k_gen_mix(SegDesc sd, int32_t seg_id, int
     const int q = idx >> 4, rl = 2 * (idx & 15);
     double z[4] = {0.0, 0.0, 0.0, 0.0};
     const int r = r0 + rl;
-    if (q < P && r < n_real) {
+    if (q < sd.n_q && r < n_real) {  // columns q >= n_q of L are zero: their normals are never needed
       const uint64_t g = (uint64_t)(real0 + r);
       if ((g & 1) == 0) {
         gp_pair2((uint32_t)k, (uint32_t)q, (uint32_t)seg_id, g, k0, k1, z);
@@ -1493,7 +1494,7 @@ __global__ __launch_bounds__(512) void k_gen_mix(SegDesc sd, int32_t seg_id, int
   const int lr = lane & 15, lg = lane >> 4;
   const int u = wave >> 1, h = wave & 1;  // pulsar tile (64 pulsars), column half (cos / sin)
   const int p0 = 64 * u;
-  const int qend = sd.l_lower ? min(P, p0 + 64) : P;
+  const int qend = min(sd.l_lower ? min(P, p0 + 64) : P, sd.n_q);
   d4 acc[4][2];
 #pragma unroll
   for (int i = 0; i < 4; ++i) acc[i][0] = acc[i][1] = d4{0.0, 0.0, 0.0, 0.0};
@@ -1558,7 +1559,8 @@ hipError_t launch_mix_mfma_t(hipStream_t st, const SegDesc& sd, int32_t P, int32
   const int64_t blocks = (n_cb + 7) / 8 * 8 * n_pt;
   if (blocks > 0x7FFFFFFF || n_cb > 0x7FFFFFFF) return hipErrorInvalidValue;
   hipLaunchKernelGGL((k_mix_mfma<NU, NB, OCC>), dim3((unsigned)blocks), dim3(256), 0, st, sd.LT, sd.lt_ld, sd.amp, P,
-                     M, R_pad, sd.l_lower, n_pt, (int32_t)n_cb, zbuf, coef, K, acc_col0 >= 0 ? acc_col0 : sd.col0,
+                     M, R_pad, sd.l_lower, std::max(1, std::min(sd.n_q, P)), n_pt, (int32_t)n_cb, zbuf, coef, K,
+                     acc_col0 >= 0 ? acc_col0 : sd.col0,
                      x_out, acc_col0 >= 0 ? 1 : 0);
   return hipGetLastError();
 }

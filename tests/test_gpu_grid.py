@@ -526,21 +526,26 @@ def zlib_crc(s):
     return zlib.crc32(s.encode())
 
 
-@pytest.mark.parametrize("factor", ["cholesky", "svd"])
+@pytest.mark.parametrize("factor", ["cholesky", "svd", "dipole_rank3"])
 def test_gen_mix_matches_two_kernels(ctx, capi, shipped, factor):
     """k_gen_mix (FPTA_OPT_GEN_MIX 1) draws a common signal's normals into LDS and mixes them on fp64 MFMA in one
     kernel: same counters, same products in the same k-step order as k_gen + k_mix_mfma, so blocks are bit-identical
     on the gridded (with and without k_grid_dft_gen) and exact paths, for a triangular (Cholesky) and a dense (SVD)
-    ORF factor, 70 and 160 pulsars (two and three 64-pulsar tiles)."""
-    rng = np.random.default_rng(71 if factor == "cholesky" else 72)
+    ORF factor and the batch path's rank-3 factor of the singular dipole ORF (columns past the third exactly zero:
+    both kernels mix, and k_gen_mix draws, only those three), 70 and 160 pulsars (two and three 64-pulsar tiles)."""
+    from fakepta_amd.batch import batch_factor
+    rng = np.random.default_rng({"cholesky": 71, "svd": 72}.get(factor, 73))
     for P in (70, 160):
         offs, toas, nu = random_layout(rng, P, (40, 120))
         ctx.batch_set_toas(offs, toas, nu)
         f, a = per_psr_signal(rng, offs, toas, 20)
         ctx.batch_add_signal(0, f, a)
         fc, ac, _, pos = common_signal(rng, offs, toas, 30)
-        gam = O.orf_hd(pos)
-        L = np.linalg.cholesky(gam) if factor == "cholesky" else O.mvn_factor(gam)
+        gam = O.orf_hd(pos) if factor != "dipole_rank3" else O.orf_dipole(pos)
+        L = np.linalg.cholesky(gam) if factor == "cholesky" else (O.mvn_factor(gam) if factor == "svd" else
+                                                                   batch_factor(gam))
+        if factor == "dipole_rank3":
+            assert np.all(L[:, 3:] == 0) and np.any(L[:, 2] != 0)
         ctx.batch_add_signal(1, fc, ac, L=L)
         segs = [O.Segment(0, 2 * np.pi * f, a, 0.0), O.Segment(1, 2 * np.pi * fc, ac, 0.0, L=L)]
         try:

@@ -537,11 +537,12 @@ def test_batch_split_invariance_bitwise(ctx):
 
 
 @pytest.mark.parametrize("mix_mfma", [1, 0], ids=["mfma", "valu"])
-@pytest.mark.parametrize("factor", ["cholesky", "svd"])
+@pytest.mark.parametrize("factor", ["cholesky", "svd", "rank3"])
 def test_tiled_mix_vs_oracle(ctx, capi, factor, mix_mfma):
     """P >= 64 takes the GEMM mix: k_mix_mfma (default) or the register-tiled VALU k_mix_tiled
-    (FPTA_OPT_MIX_MFMA 0), triangular when L is a Cholesky factor; P = 150 is not a multiple of the 64-pulsar
-    tile. Both against the oracle, and the two mixes' coefficients against each other."""
+    (FPTA_OPT_MIX_MFMA 0), triangular when L is a Cholesky factor, over the leading nonzero columns only for the
+    batch path's rank-3 factor of the singular dipole ORF, dense for numpy's full SVD factor; P = 150 is not a
+    multiple of the 64-pulsar tile. Both against the oracle, and the two mixes' coefficients against each other."""
     ctx.set_option(capi.OPT_MIX_MFMA, mix_mfma)
     from fakepta_amd.batch import batch_factor
     rng = np.random.default_rng(21)
@@ -549,9 +550,15 @@ def test_tiled_mix_vs_oracle(ctx, capi, factor, mix_mfma):
     offs, toas, nu = random_layout(rng, P, (5, 40))
     ctx.batch_set_toas(offs, toas, nu)
     f, amp, _, pos = common_signal(rng, offs, toas, 17)
-    gam = O.orf_hd(pos) if factor == "cholesky" else O.orf_monopole(pos)
-    L = batch_factor(gam)
-    assert (np.allclose(L, np.tril(L)) if factor == "cholesky" else not np.allclose(L, np.tril(L)))
+    if factor == "cholesky":
+        L = batch_factor(O.orf_hd(pos))
+        assert np.allclose(L, np.tril(L))
+    elif factor == "svd":
+        L = O.mvn_factor(O.orf_monopole(pos))  # numpy's full factor: every column nonzero (rounding noise)
+        assert not np.allclose(L, np.tril(L)) and np.all(np.any(L != 0, axis=0))
+    else:
+        L = batch_factor(O.orf_dipole(pos))
+        assert np.all(L[:, 3:] == 0) and not np.allclose(L, np.tril(L))
     ctx.batch_add_signal(1, f, amp, idx=0.0, L=L)
     f2, a2 = per_psr_signal(rng, offs, toas, 5)
     ctx.batch_add_signal(0, f2, a2, idx=4.0)
