@@ -442,12 +442,24 @@ def main():
                     "traffic_source": traffic_src, "flops_per_launch": flops, "avg_launch_ms": synth_avg_s * 1e3,
                     "write_GBps": out_bytes / synth_avg_s / 1e9}
 
+    if path == 4:
+        # the HBM rate plain streaming stores reach on this part (torch fill of 6.5 GB, tools/store_rate.py): the
+        # practical write ceiling beside the 8 TB/s spec the fraction above is taken against
+        try:
+            with open(os.path.join(ROOT, "profiles", "r03u_store_rate.json")) as fh:
+                sr = json.load(fh)
+            roofline["achievable_write"] = {"fill_GBps": sr["fill_TBps"] * 1e3,
+                                            "copy_rw_GBps": sr["copy_TBps_read_plus_write"] * 1e3,
+                                            "frac_of_fill": roofline["achieved"] / (sr["fill_TBps"] * 1e3),
+                                            "source": "profiles/r03u_store_rate.json (tools/store_rate.py)"}
+        except (OSError, ValueError, KeyError):
+            pass
     if path == 4 and args.config == "c2" and args.exact_launches > 0:
         t_int, t_dft = isolated_grid(ctx, _capi, sim, args.seed, R, args.exact_launches)
         roofline["isolated"] = {"note": "same batch, one stream (no co-running draws / DFT), after the timed run",
                                 "avg_launch_ms": t_int * 1e3, "achieved": out_bytes / t_int / 1e9,
                                 "frac": out_bytes / t_int / 1e9 / HBM_PEAK_GBS, "dft_ms_per_block": t_dft * 1e3}
-        if t_dft > 0:  # (k_psr_fused runs the DFT inside the synthesis kernel: no separate launch)
+        if t_dft > 0:  # a layout whose DFT runs inside the synthesis kernel records no separate launch
             dft_tf = 2.0 * gi["fma_dft"] * (-(-R // 128) * 128) / t_dft / 1e12
             roofline["isolated"].update(dft_TFLOPs=dft_tf, dft_frac_fp64_peak=dft_tf / FP64_PEAK_TFLOPS)
     pcie = None
