@@ -193,8 +193,9 @@ struct fpta_ctx {
   int grid_coalesce = 1;  // gridded path: signals sharing w0 and the chromatic weight share one grid (FPTA_OPT_GRID_COALESCE)
   int async_sums = 0;    // streamed jobs: partial-checksum reductions on their own stream (FPTA_OPT_ASYNC_SUMS; measured
                          // no faster on C3, profiles/r03h_ab_c3_async_sums.txt: the reductions then compete with the interpolation)
-  int gen_mix = 1;       // common signals of 64..256 pulsars: draws and ORF mixing in one kernel (k_gen_mix,
-                         // FPTA_OPT_GEN_MIX); 0 k_gen into zbuf, then k_mix_mfma
+  int gen_mix = 2;       // common signals of 64..256 pulsars: draws and ORF mixing in one kernel (k_gen_mix,
+                         // FPTA_OPT_GEN_MIX; 2: 16-realization waves, C3 -3.7 % vs 1, profiles/r03z_gen_mix_waves.txt);
+                         // 0 k_gen into zbuf, then k_mix_mfma
   int dft_gen = 1;       // gridded path: grid signals with a per-pulsar member draw their coefficients inside the DFT
                          // (k_grid_dft_gen, FPTA_OPT_DFT_GEN): no k_gen launch, no coefficient round trip for them
   bool gen_fused = false;  // the current block runs k_grid_dft_gen for those grid signals (set by batch_common)
@@ -664,7 +665,8 @@ int run_coefficients(fpta_ctx* c, Layout& L, uint64_t seed, int64_t real0, int32
     if (in_fused[i] && d.kind == 0) continue;  // drawn inside its grid signal's DFT
     if (d.kind == 1 && c->gen_mix && mfma_mix && !zin && !x_out && fuse_into[i] < 0 && P <= kGenMixMaxP) {
       KTimer kt(c, FPTA_K_MIX, st);  // draws + mixing in one kernel, into the signal's own columns
-      HIPCHK(c, launch_gen_mix(st, d, (int32_t)i, P, R, R_pad, real0, k0, k1, c->coef.as<double>(), L.K),
+      HIPCHK(c, launch_gen_mix(st, d, (int32_t)i, P, R, R_pad, real0, k0, k1, c->coef.as<double>(), L.K,
+                               c->gen_mix == 2 ? 1 : 2),
              "k_gen_mix launch");
     } else {
     {
@@ -1713,7 +1715,8 @@ int fpta_set_option(fpta_ctx* c, int32_t key, int64_t value) {
       c->dft_gen = value ? 1 : 0;
       return FPTA_OK;
     case FPTA_OPT_GEN_MIX:
-      c->gen_mix = value ? 1 : 0;
+      if (value < 0 || value > 2) return fail(c, FPTA_EINVAL, "gen_mix must be 0 .. 2");
+      c->gen_mix = (int)value;
       return FPTA_OK;
     case FPTA_OPT_ASYNC_SUMS:
       c->async_sums = value ? 1 : 0;

@@ -1464,9 +1464,13 @@ __global__ __launch_bounds__(256, OCC) void k_mix_mfma(const double* __restrict_
 // k_mix_mfma does: the same products, summed in the same k-step order, stored as the rounded product amp * sum.
 // The zbuf round trip (write + read of P x 2 N x R doubles) and a launch are gone.
 
-__global__ __launch_bounds__(512) void k_gen_mix(SegDesc sd, int32_t seg_id, int32_t P, int32_t n_real, int32_t R_pad,
-                                                 int64_t real0, uint32_t k0, uint32_t k1, double* __restrict__ coef,
-                                                 int32_t K) {
+// RH realization tiles of 16 per wave (RH = 2: waves (u, h) over 32 realizations; RH = 1: twice the waves, each on
+// 16 realizations, so a workgroup's draws and MFMA steps spread over 8 waves per 64-pulsar tile pair). The products
+// and their k-step order per coefficient are the same either way.
+template <int RH>
+__global__ __launch_bounds__(1024) void k_gen_mix(SegDesc sd, int32_t seg_id, int32_t P, int32_t n_real, int32_t R_pad,
+                                                  int64_t real0, uint32_t k0, uint32_t k1, double* __restrict__ coef,
+                                                  int32_t K) {
   extern __shared__ __attribute__((aligned(16))) double Zs[];  // [q_pad][64]: cos of 32 realizations, then sin
   const int n_rb = R_pad >> 5;
   const int k = blockIdx.x / n_rb, r0 = (blockIdx.x - k * n_rb) * 32;
@@ -1492,31 +1496,41 @@ __global__ __launch_bounds__(512) void k_gen_mix(SegDesc sd, int32_t seg_id, int
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const int lr = lane & 15, lg = lane >> 4;
-  const int u = wave >> 1, h = wave & 1;  // pulsar tile (64 pulsars), column half (cos / sin)
+  constexpr int NRH = 2 / RH;  // realization halves per (u, h)
+  const int rh = wave % NRH, uh = wave / NRH;
+  const int u = uh >> 1, h = uh & 1;  // pulsar tile (64 pulsars), column half (cos / sin)
   const int p0 = 64 * u;
   const int qend = min(sd.l_lower ? min(P, p0 + 64) : P, sd.n_q);
-  d4 acc[4][2];
+  d4 acc[4][RH];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) acc[i][0] = acc[i][1] = d4{0.0, 0.0, 0.0, 0.0};
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int e = 0; e < RH; ++e) acc[i][e] = d4{0.0, 0.0, 0.0, 0.0};
   const double* __restrict__ lt = sd.LT + p0 + 2 * lr;
-  const double* __restrict__ zb = Zs + 32 * h + 2 * lr;
+  // B operand of realization tile e: RH = 2 realizations 2 lr + e (one 16-byte pair); RH = 1 realization 16 rh + lr
+  const double* __restrict__ zb = Zs + 32 * h + (RH == 2 ? 2 * lr : 16 * rh + lr);
   auto step = [&](int q0) {
     const int q = q0 + lg;
     const dbl2 a0 = *(const dbl2*)(lt + (int64_t)q * sd.lt_ld);
     const dbl2 a1 = *(const dbl2*)(lt + (int64_t)q * sd.lt_ld + 32);
-    const dbl2 b = *(const dbl2*)(zb + q * 64);
-    acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0.x, b.x, acc[0][0], 0, 0, 0);
-    acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0.x, b.y, acc[0][1], 0, 0, 0);
-    acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0.y, b.x, acc[1][0], 0, 0, 0);
-    acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0.y, b.y, acc[1][1], 0, 0, 0);
-    acc[2][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1.x, b.x, acc[2][0], 0, 0, 0);
-    acc[2][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1.x, b.y, acc[2][1], 0, 0, 0);
-    acc[3][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1.y, b.x, acc[3][0], 0, 0, 0);
-    acc[3][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1.y, b.y, acc[3][1], 0, 0, 0);
+    double b[RH];
+    if constexpr (RH == 2) {
+      const dbl2 bv = *(const dbl2*)(zb + q * 64);
+      b[0] = bv.x;
+      b[1] = bv.y;
+    } else {
+      b[0] = zb[q * 64];
+    }
+#pragma unroll
+    for (int e = 0; e < RH; ++e) {
+      acc[0][e] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0.x, b[e], acc[0][e], 0, 0, 0);
+      acc[1][e] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0.y, b[e], acc[1][e], 0, 0, 0);
+      acc[2][e] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1.x, b[e], acc[2][e], 0, 0, 0);
+      acc[3][e] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1.y, b[e], acc[3][e], 0, 0, 0);
+    }
   };
   for (int q0 = 0; q0 < qend; q0 += 4) step(q0);
-  // D of (pulsar tile 2v + e, realization tile c): lane (lr, lg) register g = pulsar p0 + 32 v + 2 (lg + 4 g) + e,
-  // realization r0 + 2 lr + c: one 16-byte store of two adjacent realizations per (lane, pulsar)
+  // D of (pulsar tile 2v + e', realization tile): lane (lr, lg) register g = pulsar p0 + 32 v + 2 (lg + 4 g) + e'
   const double a = sd.amp[k];
   const int jc = 2 * k + h;
 #pragma unroll
@@ -1527,22 +1541,30 @@ __global__ __launch_bounds__(512) void k_gen_mix(SegDesc sd, int32_t seg_id, int
       for (int g = 0; g < 4; ++g) {
         const int p = p0 + 32 * v + 2 * (lg + 4 * g) + e;
         if (p >= P) continue;
-        double* dst = coef + ((int64_t)p * K + sd.col0 + jc) * R_pad + r0 + 2 * lr;
-        *(dbl2*)dst = dbl2{a * acc[2 * v + e][0][g], a * acc[2 * v + e][1][g]};
+        double* dst = coef + ((int64_t)p * K + sd.col0 + jc) * R_pad + r0;
+        if constexpr (RH == 2) {  // realizations 2 lr, 2 lr + 1: one 16-byte store
+          *(dbl2*)(dst + 2 * lr) = dbl2{a * acc[2 * v + e][0][g], a * acc[2 * v + e][1][g]};
+        } else {
+          dst[16 * rh + lr] = a * acc[2 * v + e][0][g];
+        }
       }
 }
 
 hipError_t launch_gen_mix(hipStream_t st, const SegDesc& sd, int32_t seg_id, int32_t P, int32_t n_real, int32_t R_pad,
-                          int64_t real0, uint32_t k0, uint32_t k1, double* coef, int32_t K) {
+                          int64_t real0, uint32_t k0, uint32_t k1, double* coef, int32_t K, int rh) {
   const int32_t n_pt = (P + 63) / 64;
   if (sd.kind != 1 || !sd.LT || P < 1 || P > kGenMixMaxP || R_pad % 32 != 0 || sd.lt_ld < 64 * n_pt ||
-      sd.lt_rows < ((P + 7) & ~7) || sd.col0 < 0 || sd.col0 + 2 * sd.nm > K)
+      sd.lt_rows < ((P + 7) & ~7) || sd.col0 < 0 || sd.col0 + 2 * sd.nm > K || (rh != 1 && rh != 2))
     return hipErrorInvalidValue;
   const int64_t blocks = (int64_t)sd.nm * (R_pad / 32);
   if (blocks > 0x7FFFFFFF) return hipErrorInvalidValue;
   const size_t lds = sizeof(double) * 64 * (size_t)((P + 7) & ~7);
-  hipLaunchKernelGGL(k_gen_mix, dim3((unsigned)blocks), dim3(128 * n_pt), lds, st, sd, seg_id, P, n_real, R_pad, real0,
-                     k0, k1, coef, K);
+  if (rh == 2)
+    hipLaunchKernelGGL(k_gen_mix<2>, dim3((unsigned)blocks), dim3(128 * n_pt), lds, st, sd, seg_id, P, n_real, R_pad,
+                       real0, k0, k1, coef, K);
+  else
+    hipLaunchKernelGGL(k_gen_mix<1>, dim3((unsigned)blocks), dim3(256 * n_pt), lds, st, sd, seg_id, P, n_real, R_pad,
+                       real0, k0, k1, coef, K);
   return hipGetLastError();
 }
 
