@@ -39,10 +39,14 @@ SYNTH_KERNELS = {3: ("k_synth_valu_seeded<2,16>", "fp64-valu"), 2: ("k_synth_mfm
                  1: ("k_synth_direct", "fp64-valu")}
 
 
-def grid_interp_kernel(ws, part):
-    """Name of the interpolation kernel FPTA_OPT_INTERP_WS = ws launches for plain (C2) or fused-checksum (C3) blocks."""
+def grid_interp_kernel(ws, part, r_pad):
+    """Name of the interpolation kernel FPTA_OPT_INTERP_WS = ws launches for plain (C2) or fused-checksum (C3) blocks
+    of R_pad realizations (the default takes the 256-realization tiles of k_grid_interp_ws2 when they waste fewer
+    realization slots than the 512 of k_grid_interp_ws, as capi.hip does)."""
     p = "true" if part else "false"
     reg = f"k_grid_interp_mfma<false, {p}, 8>"
+    if ws == 1 and not part and -(-r_pad // 256) * 256 - r_pad < -(-r_pad // 512) * 512 - r_pad:
+        ws = 3
     return {0: reg, 1: reg if part else "k_grid_interp_ws<false>", 2: f"k_grid_interp_ws<{p}>",
             3: reg if part else "k_grid_interp_ws2<false>"}[ws]
 
@@ -402,7 +406,9 @@ def main():
     out_bytes = 8.0 * info["n_toa"] * n_launch_real
     if path == 4:
         # the warp-specialised kernel serves plain blocks; fused-checksum blocks (c3) take the register kernel
-        kernel, pipe = grid_interp_kernel(ctx.get_option(_capi.OPT_INTERP_WS), args.config != "c2"), "fp64-mfma"
+        kernel = grid_interp_kernel(ctx.get_option(_capi.OPT_INTERP_WS), args.config != "c2",
+                                    -(-int(R) // 128) * 128)
+        pipe = "fp64-mfma"
         traffic, traffic_src = pmc_traffic(kernel, info, R, args.traffic, GRID_LAYOUT)
         achieved = out_bytes / synth_avg_s / 1e9
         R_pad = -(-int(n_launch_real) // 128) * 128
