@@ -311,8 +311,11 @@ int fpta_comm_gather(fpta_comm* comm, const double* send, int64_t count, double*
 #define FPTA_OPT_INTERP_WS 15     /* gridded interpolation: 1 (default) the warp-specialised k_grid_interp_ws
                                      (producer waves stage the operands in an LDS ring, compute waves only store,
                                      so stores never delay an operand load) for blocks without fused white noise
-                                     or fused partial checksums; 2 also for blocks with fused partial checksums;
-                                     0 the register-pipelined k_grid_interp_mfma. Results are identical. */
+                                     or fused partial checksums, or k_grid_interp_ws2 (256-realization tiles, two
+                                     workgroups per CU) when the padded realization count leaves fewer idle
+                                     compute waves in 256- than in 512-realization tiles (C4: R = 256); 2 ws also
+                                     for blocks with fused partial checksums; 3 ws2 for every plain block; 0 the
+                                     register-pipelined k_grid_interp_mfma. Results are identical. */
 #define FPTA_OPT_SIDE_SPLIT 16    /* pipelined gridded blocks (FPTA_OPT_OVERLAP): 1 (default) the grid signal with
                                      the largest DFT, when it has no common (ORF-mixed) member, is drawn and
                                      transformed on a second side stream, beside the other signals' draws, mixing
