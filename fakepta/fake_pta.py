@@ -100,6 +100,13 @@ class Pulsar:
         is drawn per TOA and appended to the flag (fake_pta.py:63-74; the flag array keeps
         numpy's fixed string width, as in the reference)."""
         flags = np.tile(backends, self.nepochs)
+        # every distinct flag names its frequency ('NAME.1400'): no draw, so each distinct flag is parsed once and
+        # mapped onto the TOAs (the per-TOA loop below was ~60 % of make_fake_array's host time, profiles/r05q_*)
+        uniq, inv = np.unique(flags, return_inverse=True)
+        try:
+            return np.array([float(u.split('.')[-1]) for u in uniq])[inv.reshape(-1)], flags
+        except ValueError:
+            pass  # some flag draws its frequency: per TOA, in TOA order, as the reference
         radio = []
         for i, flag in enumerate(flags):
             try:
