@@ -44,6 +44,38 @@ def test_pulsar_construction_rng_parity(golden):
     assert psr.name == str(g["name"]) and psr.Tspan == g["Tspan"]
 
 
+@pytest.mark.parametrize("backends", [["NUPPI.1400"], ["NUPPI.1400", "LEAP.1396", "X.2500"], ["backend"],
+                                      ["A.1400", "b"]])
+def test_backend_flags_fast_path_matches_per_toa_loop(backends):
+    """get_freqs_and_backends parses each distinct flag once when every flag names its frequency; otherwise it walks
+    the TOAs drawing np.random.choice(freqs) per unnamed flag, as fake_pta.py:63-74. Both give the per-TOA loop's
+    frequencies, flags (dtype included) and leave the global RNG in the same state."""
+    def per_toa(nepochs, freqs, backends):
+        flags = np.tile(backends, nepochs)
+        radio = []
+        for i, flag in enumerate(flags):
+            try:
+                radio.append(float(flag.split('.')[-1]))
+            except ValueError:
+                choice = np.random.choice(freqs)
+                flags[i] = flags[i] + '.' + str(int(choice))
+                radio.append(choice)
+        return np.array(radio), flags
+
+    class Stub:
+        nepochs = 7
+    np.random.seed(3)
+    got = fp.Pulsar.get_freqs_and_backends(Stub(), [1400, 2000], backends)
+    after_got = np.random.random()
+    np.random.seed(3)
+    want = per_toa(7, [1400, 2000], backends)
+    after_want = np.random.random()
+    np.testing.assert_array_equal(got[0], want[0])
+    assert got[0].dtype == want[0].dtype and got[1].dtype == want[1].dtype
+    np.testing.assert_array_equal(got[1], want[1])
+    assert after_got == after_want
+
+
 def test_tutorial_names(golden):
     """examples/tutorial.ipynb cell 5: names of the 25-pulsar isotropic array."""
     names = golden("g5_tutorial.json")["names_npsrs25_isotropic"]
