@@ -18,9 +18,15 @@ __host__ __device__ __forceinline__ u32x4 philox4x32_10(u32x4 c, uint32_t k0, ui
     const uint64_t p0 = (uint64_t)0xD2511F53u * c.x;
     const uint64_t p1 = (uint64_t)0xCD9E8D57u * c.z;
     u32x4 n;
+#if defined(__HIP_DEVICE_COMPILE__)
+    // gfx950's three-input bitwise op (truth table 0x96 = a ^ b ^ c): one instruction per word instead of two
+    n.x = __builtin_amdgcn_bitop3_b32((uint32_t)(p1 >> 32), c.y, k0, 0x96);
+    n.z = __builtin_amdgcn_bitop3_b32((uint32_t)(p0 >> 32), c.w, k1, 0x96);
+#else
     n.x = (uint32_t)(p1 >> 32) ^ c.y ^ k0;
-    n.y = (uint32_t)p1;
     n.z = (uint32_t)(p0 >> 32) ^ c.w ^ k1;
+#endif
+    n.y = (uint32_t)p1;
     n.w = (uint32_t)p0;
     c = n;
     k0 += 0x9E3779B9u;
@@ -44,7 +50,8 @@ __device__ __forceinline__ void box_muller(u32x4 v, double& z0, double& z1) {
   z1 = r * s;
 }
 
-// The build's uniform -> normal map (oracle: normals4, bm_log_u32, bm_sincos2pi_u32, operation for operation): two
+// The build's uniform -> normal map (oracle: normals4, bm_log_u32, bm_sincos2pi_u32, operation for operation except
+// the division in the logarithm and the square root, which are within an ulp of the oracle's IEEE results): two
 // Box-Muller pairs per Philox call from 32-bit uniforms u1 = (a + 1) 2^-32 in (0, 1], u2 = b 2^-32 in [0, 1), with
 // the logarithm and sine / cosine as fixed fp64 polynomials (~3e-14 relative): about half the VALU work per normal of
 // box_muller (one Philox call per two normals, library log and sincospi).
@@ -57,7 +64,14 @@ __device__ __forceinline__ double bm_log_u32(uint32_t a) {
     e -= 1;
   }
   const double k = (double)(e - 32);
-  const double s = (m - 1.0) / (m + 1.0);
+  // s = (m - 1) / (m + 1) from v_rcp_f64 and two Newton steps (m + 1 in [1.7, 2.5]: no scaling) plus one residual
+  // correction: within an ulp of the correctly rounded quotient the oracle takes, in 7 instructions instead of 10
+  const double num = m - 1.0, den = m + 1.0;
+  double rc = __builtin_amdgcn_rcp(den);
+  rc = fma(rc, fma(-den, rc, 1.0), rc);
+  rc = fma(rc, fma(-den, rc, 1.0), rc);
+  double s = num * rc;
+  s = fma(fma(-den, s, num), rc, s);
   const double s2 = s * s;
   const double p =
       s2 * (1.0 / 3.0 +
@@ -83,20 +97,37 @@ __device__ __forceinline__ void bm_sincos2pi_u32(uint32_t b, double& sn, double&
                         x2 * (-1.0 / 720.0 +
                               x2 * (1.0 / 40320.0 +
                                     x2 * (-1.0 / 3628800.0 + x2 * (1.0 / 479001600.0 + x2 * (-1.0 / 87178291200.0)))))));
+  // quadrant qi: (sn, cs) = (sa, ca), (ca, -sa), (-sa, -ca), (-ca, sa) as a swap and two sign-bit flips (no
+  // divergent branches; the same values)
   const int qi = (int)q & 3;
-  sn = qi == 0 ? sa : (qi == 1 ? ca : (qi == 2 ? -sa : -ca));
-  cs = qi == 0 ? ca : (qi == 1 ? -sa : (qi == 2 ? -ca : sa));
+  const bool sw = (qi & 1) != 0;
+  const double s0 = sw ? ca : sa;
+  const double c0 = sw ? sa : ca;
+  sn = __longlong_as_double(__double_as_longlong(s0) ^ ((long long)(qi & 2) << 62));
+  cs = __longlong_as_double(__double_as_longlong(c0) ^ ((long long)((qi + 1) & 2) << 62));
+}
+
+// sqrt(x) for x = -2 log u1 in [0, 45]: v_rsq_f64, one Goldschmidt step and one residual correction (within an ulp
+// of the correctly rounded root; x = 0 exactly when u1 = 1)
+__device__ __forceinline__ double bm_sqrt(double x) {
+  const double y = __builtin_amdgcn_rsq(x);
+  double g = x * y, h = 0.5 * y;
+  const double r = fma(-g, h, 0.5);
+  g = fma(g, r, g);
+  h = fma(h, r, h);
+  g = fma(fma(-g, g, x), h, g);
+  return x > 0.0 ? g : 0.0;
 }
 
 // four standard normals of one Philox output: (z0, z1) from (x, y), (z2, z3) from (z, w)
 __device__ __forceinline__ void normals4(u32x4 v, double (&z)[4]) {
   double s, c;
-  const double r0 = sqrt(-2.0 * bm_log_u32(v.x));
+  const double r0 = bm_sqrt(-2.0 * bm_log_u32(v.x));
   bm_sincos2pi_u32(v.y, s, c);
   z[0] = r0 * c;
   z[1] = r0 * s;
   __builtin_amdgcn_sched_barrier(0);  // the two pairs one after the other: half the live temporaries
-  const double r1 = sqrt(-2.0 * bm_log_u32(v.z));
+  const double r1 = bm_sqrt(-2.0 * bm_log_u32(v.z));
   bm_sincos2pi_u32(v.w, s, c);
   z[2] = r1 * c;
   z[3] = r1 * s;

@@ -368,7 +368,8 @@ def box_muller(x):
 # The build's uniform -> normal map (philox.h normals4): two Box-Muller pairs per Philox call from 32-bit uniforms
 # u1 = (a + 1) 2^-32 in (0, 1], u2 = b 2^-32 in [0, 1) (as cuRAND's normal2), with the logarithm and the sine / cosine
 # evaluated by fixed fp64 polynomials that the device restates operation for operation (agreement to a few ulp; the
-# polynomials are accurate to ~3e-14 relative). |z| <= sqrt(64 ln 2) = 6.66.
+# polynomials are accurate to ~3e-14 relative; the device's quotient in the logarithm and its square root come from
+# v_rcp_f64 / v_rsq_f64 plus Newton steps, within an ulp of the IEEE results taken here). |z| <= sqrt(64 ln 2) = 6.66.
 SQRT_HALF = 0.7071067811865476
 LN2_HI, LN2_LO = 6.93147180369123816490e-01, 1.90821492927058770002e-10
 _LOG_C = (1.0 / 3.0, 1.0 / 5.0, 1.0 / 7.0, 1.0 / 9.0, 1.0 / 11.0, 1.0 / 13.0, 1.0 / 15.0)
