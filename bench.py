@@ -48,7 +48,7 @@ def grid_interp_kernel(ws, part, r_pad):
     if ws == 1 and not part and -(-r_pad // 256) * 256 - r_pad < -(-r_pad // 512) * 512 - r_pad:
         ws = 3
     return {0: reg, 1: reg if part else "k_grid_interp_ws<false>", 2: f"k_grid_interp_ws<{p}>",
-            3: reg if part else "k_grid_interp_ws2<false>"}[ws]
+            3: reg if part else "k_grid_interp_ws2<false>", 4: f"k_grid_interp_st<false, {p}>"}[ws]
 
 
 # layout tag of the gridded plan a PMC traffic record must carry to describe the shipped interpolation kernel
@@ -85,6 +85,9 @@ def parse():
     ap.add_argument("--dist-backend", default="rccl", choices=("rccl", "gloo"),
                     help="rccl: the library's RCCL communicator (one rank per GPU); gloo: torch.distributed on the "
                          "CPU (rehearsal of several ranks on one card)")
+    ap.add_argument("--sub-configs", type=int, default=1,
+                    help="c2 at N = 1: after the timed region, compact C3 / C5 / C4-per-GPU records (keys c3, c5, "
+                         "c4_per_gpu of the line; tools/bench_configs.sub_records); 0 skips them")
     ap.add_argument("--traffic", default="",
                     help="PMC-derived HBM bytes per launch (profiles/*traffic.json, tools/collect_traffic.py); "
                          "default: the record matching the kernel and shape")
@@ -150,11 +153,32 @@ def cpu_baseline_loop(toas_list, freqs_list, segs, n_sample, seed):
     rs = np.random.RandomState(seed)
     res = [np.zeros(len(t)) for t in toas_list]
     stored = {}
-    O.redraw_loop(toas_list, freqs_list, segs, res, stored, rs)
-    t0 = time.perf_counter()
-    for _ in range(n_sample):
+    with _one_thread() as used:
         O.redraw_loop(toas_list, freqs_list, segs, res, stored, rs)
-    return (time.perf_counter() - t0) / n_sample
+        t0 = time.perf_counter()
+        for _ in range(n_sample):
+            O.redraw_loop(toas_list, freqs_list, segs, res, stored, rs)
+        dt = (time.perf_counter() - t0) / n_sample
+    return dt, used
+
+
+class _one_thread:
+    """numpy's BLAS / LAPACK pools limited to one thread (threadpoolctl) for the reference-faithful loop (the SVD
+    inside each multivariate_normal would otherwise take every OMP thread); yields the BLAS threads in force."""
+
+    def __enter__(self):
+        self._lim = None
+        try:
+            from threadpoolctl import threadpool_limits
+            self._lim = threadpool_limits(limits=1)
+        except Exception:
+            pass
+        return blas_threads()
+
+    def __exit__(self, *exc):
+        if self._lim is not None:
+            self._lim.restore_original_limits()
+        return False
 
 
 def blas_threads():
@@ -199,7 +223,7 @@ def cpu_baseline_vectorised(sim, psrs, n_real, seed):
 def cpu_baseline(sim, psrs, n_sample, seed):
     n_toa = sim.n_toa
     segs = baseline_segments(sim)
-    dt_loop = cpu_baseline_loop([p.toas for p in psrs], [p.freqs for p in psrs], segs, n_sample, seed)
+    dt_loop, loop_threads = cpu_baseline_loop([p.toas for p in psrs], [p.freqs for p in psrs], segs, n_sample, seed)
     threads = os.environ.get("OMP_NUM_THREADS", "")
     n_vec = 64
     dt_vec = cpu_baseline_vectorised(sim, psrs, n_vec, seed)
@@ -211,10 +235,12 @@ def cpu_baseline(sim, psrs, n_sample, seed):
                sample=f"{n_vec} realizations, vectorised F.A (numpy {np.__version__} BLAS GEMM per pulsar), "
                       f"{dt_vec:.2f} s on {used} BLAS thread(s) (OMP_NUM_THREADS={threads or 'unset'}; the GPU "
                       f"box's CPU share is 16 of its {os.cpu_count()} host CPUs)")
-    return dict(value=n_toa / dt_loop, unit="samples/s", cores=1, kind="port",
+    return dict(value=n_toa / dt_loop, unit="samples/s", cores=loop_threads or 1, kind="port",
+                blas_threads_in_loop=loop_threads,
                 sample=f"{n_sample} re-drawn realizations of the bench array with the reference's operations "
                        f"(oracle.redraw_loop: fake_pta.py:266-267 + 370-387, correlated_noises.py:133-134 + "
-                       f"146-160, SVD per multivariate_normal), 1 thread, {dt_loop:.2f} s per realization; "
+                       f"146-160, SVD per multivariate_normal), BLAS limited to {loop_threads} thread(s) "
+                       f"(threadpoolctl), {dt_loop:.2f} s per realization; "
                        f"same-host ratio to the reference itself: profiles/r03_cpu_crosscheck.json",
                 cpu_model=cpu_model(), nproc=os.cpu_count(), omp_num_threads=threads or None,
                 vectorised_blas_threads=vec)
@@ -406,8 +432,8 @@ def main():
     out_bytes = 8.0 * info["n_toa"] * n_launch_real
     if path == 4:
         # the warp-specialised kernel serves plain blocks; fused-checksum blocks (c3) take the register kernel
-        kernel = grid_interp_kernel(ctx.get_option(_capi.OPT_INTERP_WS), args.config != "c2",
-                                    -(-int(R) // 128) * 128)
+        kernel = gi["interp_kernel"] or grid_interp_kernel(ctx.get_option(_capi.OPT_INTERP_WS), args.config != "c2",
+                                                           -(-int(R) // 128) * 128)
         pipe = "fp64-mfma"
         traffic, traffic_src = pmc_traffic(kernel, info, R, args.traffic, GRID_LAYOUT)
         achieved = out_bytes / synth_avg_s / 1e9
@@ -513,6 +539,11 @@ def main():
             line["cpu_baseline"] = cpu_baseline(sim, psrs, args.cpu_sample, args.seed)
         else:
             line["cpu_baseline"] = None
+        if world == 1 and args.config == "c2" and args.sub_configs:
+            # the other BASELINE configs, each on its own context after the timed C2 region (value unchanged)
+            from tools import bench_configs
+            bench_configs.OPTS.extend(args.opt)
+            line.update(bench_configs.sub_records())
         print(json.dumps(line), flush=True)
     ctx.close()
     comm.close()

@@ -101,6 +101,17 @@ OPTIONS = (OPT_SYNTH_PATH, OPT_MFMA_MIN_REAL, OPT_PROFILE, OPT_ANCHOR, OPT_VALU_
            OPT_INTERP_LDS, OPT_GRID_COALESCE, OPT_INTERP_WS, OPT_SIDE_SPLIT, OPT_DFT_GEN, OPT_GEN_MIX,
            OPT_ASYNC_SUMS)
 K_GEN, K_MIX, K_SYNTH, K_WHITE, K_DENSE, K_GRID = 0, 1, 2, 3, 4, 5
+
+
+def interp_kernel_name(code):
+    """The gridded interpolation kernel of the last block (fpta_batch_grid_info_n slot 15: 1 + 4 kind + 2 white +
+    partial checksums), as rocprofv3 names it; None before any gridded block."""
+    if code <= 0:
+        return None
+    kind, white, part = (code - 1) >> 2, "true" if (code - 1) & 2 else "false", "true" if (code - 1) & 1 else "false"
+    return {0: f"k_grid_interp_mfma<{white}, {part}, 8>", 1: f"k_grid_interp_ws<{part}>",
+            2: f"k_grid_interp_ws2<{part}>", 3: f"k_grid_interp_lds<{white}, {part}>",
+            4: f"k_grid_interp_st<{white}, {part}>"}.get(kind)
 BUILD_DEBUG = 1
 GATHER_AUTO, GATHER_RCCL, GATHER_HOST = 0, 1, 2
 COMM_ID_BYTES = 128
@@ -321,6 +332,7 @@ class Context:
         d["grid_signals"] = int(d["grid_signals"])
         d["signals"] = int(d["signals"])
         d["path_reason"] = _lib.fpta_batch_path_reason(self._h).decode()
+        d["interp_kernel"] = interp_kernel_name(int(g[15]))
         return d
 
     def batch_synth(self, seed, real0, n_real, to_host=True, coeffs=False):

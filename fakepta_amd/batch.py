@@ -276,35 +276,72 @@ class RealizationComm:
         self.dist = None
 
 
-def _exchange_unique_id(rank, world, addr, port, make_id, timeout):
+_RDZV_MAGIC = b"FPTA"
+
+
+def _recv_exact(conn, n):
+    buf = b""
+    while len(buf) < n:
+        chunk = conn.recv(n - len(buf))
+        if not chunk:
+            raise ConnectionError("rendezvous connection closed early")
+        buf += chunk
+    return buf
+
+
+def _exchange_unique_id(rank, world, addr, port, make_id, timeout, n_bytes=None):
     """Rank 0 makes the RCCL unique id and serves it to ranks 1 .. world - 1 over one TCP socket at (addr, port);
-    the other ranks connect (retrying until `timeout`) and read its 128 bytes. Plain sockets: no torch import, so
-    the rank process maps one HIP runtime (the library's)."""
+    the other ranks connect (retrying until `timeout`) and read its bytes. Plain sockets: no torch import, so the
+    rank process maps one HIP runtime (the library's).
+
+    Protocol: a rank sends b"FPTA" + its rank (uint32 little-endian), reads the id and answers b"A". Rank 0 keeps
+    accepting until every rank 1 .. world - 1 has acknowledged: a peer with a wrong magic or rank, or one that drops
+    the connection before its acknowledgement, uses up no slot (a rank that failed after connecting retries and is
+    served again). Either side raises TimeoutError past `timeout` seconds."""
     import socket
+    import struct
     import time as _time
-    n = _capi.COMM_ID_BYTES
+    n = _capi.COMM_ID_BYTES if n_bytes is None else int(n_bytes)
     deadline = _time.monotonic() + timeout
     if rank == 0:
         uid = make_id()
+        if len(uid) != n:
+            raise ValueError(f"unique id of {len(uid)} bytes, expected {n}")
+        pending = set(range(1, world))
         with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as srv:
             srv.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
             srv.bind((addr, port))
-            srv.listen(world)
-            for _ in range(world - 1):
-                srv.settimeout(max(deadline - _time.monotonic(), 0.1))
-                conn, _ = srv.accept()
+            srv.listen(max(world, 8))
+            while pending:
+                left = deadline - _time.monotonic()
+                if left <= 0:
+                    raise TimeoutError(f"rank 0: RCCL rendezvous at {addr}:{port}: ranks {sorted(pending)} did not "
+                                       f"check in within {timeout} s")
+                srv.settimeout(left)
+                try:
+                    conn, _ = srv.accept()
+                except socket.timeout:
+                    continue
                 with conn:
-                    conn.sendall(uid)
+                    try:
+                        conn.settimeout(min(5.0, max(deadline - _time.monotonic(), 0.1)))
+                        hello = _recv_exact(conn, 8)
+                        peer = struct.unpack("<I", hello[4:])[0]
+                        if hello[:4] != _RDZV_MAGIC or not 1 <= peer < world:
+                            continue  # a stray or foreign connection: no slot used
+                        conn.sendall(uid)
+                        if _recv_exact(conn, 1) == b"A":
+                            pending.discard(peer)
+                    except OSError:
+                        continue  # the peer retries
         return uid
+    hello = _RDZV_MAGIC + struct.pack("<I", rank)
     while True:
         try:
             with socket.create_connection((addr, port), timeout=5.0) as conn:
-                buf = b""
-                while len(buf) < n:
-                    chunk = conn.recv(n - len(buf))
-                    if not chunk:
-                        raise ConnectionError("rendezvous closed early")
-                    buf += chunk
+                conn.sendall(hello)
+                buf = _recv_exact(conn, n)
+                conn.sendall(b"A")
                 return buf
         except OSError:
             if _time.monotonic() > deadline:

@@ -190,6 +190,7 @@ struct fpta_ctx {
   // the next (VALU Philox beside fp64 MFMA). ev_begin orders the side stream after everything queued before.
   int overlap = 1;
   int interp_ws = 1;      // gridded interpolation on the warp-specialised kernel (FPTA_OPT_INTERP_WS)
+  int last_interp = 0;    // interpolation kernel of the last gridded block: 1 + 4 kind + 2 white + part (0: none)
   int grid_coalesce = 1;  // gridded path: signals sharing w0 and the chromatic weight share one grid (FPTA_OPT_GRID_COALESCE)
   int async_sums = 0;    // streamed jobs: partial-checksum reductions on their own stream (FPTA_OPT_ASYNC_SUMS; measured
                          // no faster on C3, profiles/r03h_ab_c3_async_sums.txt: the reductions then compete with the interpolation)
@@ -969,7 +970,8 @@ int grid_build(fpta_ctx* c, Layout& L) {
   G.n_chunks = (int32_t)chunks.size();
   const int32_t n_chunks = G.n_chunks;
   // band rows of a chunk: every signal's band back to back (virtual rows voff_s ..), padded to a multiple of
-  // 4 once per chunk (k_grid_interp_mfma: 4 rows per MFMA step; pad rows re-read a valid row at weight 0)
+  // 4 once per chunk (k_grid_interp_mfma: 4 rows per MFMA step; pad rows re-read a valid row at weight 0), and to at
+  // least kGridMinV rows (k_grid_interp_st's operand lookahead never passes the next chunk)
   std::vector<int32_t> voff((size_t)n_seg * n_chunks);
   int32_t vmax = 4;
   for (int32_t ci = 0; ci < n_chunks; ++ci) {
@@ -978,7 +980,7 @@ int grid_build(fpta_ctx* c, Layout& L) {
       voff[(size_t)s * n_chunks + ci] = v;
       v += band_n[s][ci];
     }
-    chunks[ci].w = (v + 3) & ~3;
+    chunks[ci].w = std::max(kGridMinV, (v + 3) & ~3);
     vmax = std::max(vmax, chunks[ci].w);
   }
   if (vmax > kGridVMax) {
@@ -1313,16 +1315,25 @@ int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad, bool pipe = fa
   // waves idle, the 256-realization tiles of k_grid_interp_ws2 waste less (C4, R_pad = 256: half of every ws tile;
   // 6.8-7.4 vs 8.4 ms/step, profiles/r04a_c4_ws2.txt)
   const bool ws2_fits = c->interp_ws == 1 && (R_pad + 255) / 256 * 256 - R_pad < (R_pad + 511) / 512 * 512 - R_pad;
-  if ((c->interp_ws == 3 || ws2_fits) && !c->interp_lds && !a.w_on && !a.accumulate && !a.part) {
+  int kind;  // the interpolation kernel (fpta_batch_grid_info_n slot 15)
+  if (c->interp_ws == 4 && !c->interp_lds) {
+    kind = 4;
+    HIPCHK(c, launch_grid_interp_st(c->stream, a, band, R_pad), "k_grid_interp_st launch");
+  } else if ((c->interp_ws == 3 || ws2_fits) && !c->interp_lds && !a.w_on && !a.accumulate && !a.part) {
+    kind = 2;
     HIPCHK(c, launch_grid_interp_ws(c->stream, a, band, R_pad, true), "k_grid_interp_ws2 launch");
   } else if (c->interp_ws && !c->interp_lds && !a.w_on && !a.accumulate && (!a.part || c->interp_ws == 2)) {
+    kind = 1;
     HIPCHK(c, launch_grid_interp_ws(c->stream, a, band, R_pad), "k_grid_interp_ws launch");
   } else if (c->interp_lds && G.lds_ok && !a.w_on) {
+    kind = 3;
     GridLds lds{G.groups.as<int4>(), G.urows.as<int32_t>(), G.lrows.as<int32_t>(), G.n_groups, G.lds_rows};
     HIPCHK(c, launch_grid_interp_lds(c->stream, a, band, lds, R_pad), "k_grid_interp_lds launch");
   } else {
+    kind = 0;
     HIPCHK(c, launch_grid_interp_mfma(c->stream, a, band, R_pad), "k_grid_interp_mfma launch");
   }
+  c->last_interp = 1 + kind * 4 + (a.w_on ? 2 : 0) + (a.part ? 1 : 0);
   if (pipe) {  // buffer gi is free once this interpolation is done; the next block's DFT writes the other one
     HIPCHK(c, hipEventRecord(c->ev_gfree[gi], c->stream), "event record");
     c->gfree_set[gi] = true;
@@ -1730,7 +1741,7 @@ int fpta_set_option(fpta_ctx* c, int32_t key, int64_t value) {
       c->batch.grid.clear();
       return FPTA_OK;
     case FPTA_OPT_INTERP_WS:
-      if (value < 0 || value > 3) return fail(c, FPTA_EINVAL, "interp_ws must be 0 .. 3");
+      if (value < 0 || value > 4) return fail(c, FPTA_EINVAL, "interp_ws must be 0 .. 4");
       c->interp_ws = (int)value;
       return FPTA_OK;
     case FPTA_OPT_SIDE_SPLIT:
@@ -2328,7 +2339,7 @@ int fpta_batch_grid_info_n(fpta_ctx* c, double* dst, int32_t n_out) {
   out[12] = ok ? (double)G.segs.size() : 0.0;
   out[13] = (double)c->batch.segs.size();
   out[14] = ok ? G.mean_v : 0.0;
-  out[15] = 0.0;
+  out[15] = c->last_interp;
   std::memcpy(dst, out, sizeof(double) * std::min<int32_t>(n_out, FPTA_GRID_INFO_LEN));
   return FPTA_GRID_INFO_LEN;
 }

@@ -82,6 +82,7 @@ static_assert(sizeof(kSeededVariants) == sizeof(kValuVariants), "one variant ind
 
 // Gridded synthesis (grid.hip): one signal's tables as the kernels see them.
 constexpr int kGridVMax = 256;  // band rows per chunk, all signals (k_grid_interp_mfma keeps them in 4 VGPRs)
+constexpr int kGridMinV = 16;  // band rows per chunk at least (k_grid_interp_st: 4 MFMA steps, its lookahead + 1)
 constexpr int kGridTT = 32;  // TOAs per interpolation chunk (k_grid_interp_mfma: even / odd TOAs = two MFMA B-tiles)
 constexpr int kGridMI = 8;   // grid rows per wave in k_grid_dft
 #ifndef FPTA_DFT_MJ
@@ -161,6 +162,9 @@ hipError_t launch_grid_interp_mfma(hipStream_t st, const SynthArgs& a, const Gri
 // ws2: k_grid_interp_ws2 (64-realization compute tiles, two workgroups per CU), plain blocks only
 hipError_t launch_grid_interp_ws(hipStream_t st, const SynthArgs& a, const GridBand& band, int32_t R_pad,
                                  bool ws2 = false);
+// Storer-wave variant: compute waves hand finished sums to storer waves through LDS; every block kind (white / ECORR
+// epilogue, partial checksums, accumulate) with R_pad a multiple of 128
+hipError_t launch_grid_interp_st(hipStream_t st, const SynthArgs& a, const GridBand& band, int32_t R_pad);
 // LDS-staged variant: the 4 waves of a workgroup take <= kLdsGroup consecutive chunks of one pulsar for the same
 // realizations; the union of their band rows (<= kLdsRowsMax) is loaded once into LDS
 constexpr int kLdsGroup = 4, kLdsRowsMax = 144;

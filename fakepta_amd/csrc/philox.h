@@ -18,8 +18,9 @@ __host__ __device__ __forceinline__ u32x4 philox4x32_10(u32x4 c, uint32_t k0, ui
     const uint64_t p0 = (uint64_t)0xD2511F53u * c.x;
     const uint64_t p1 = (uint64_t)0xCD9E8D57u * c.z;
     u32x4 n;
-#if defined(__HIP_DEVICE_COMPILE__)
-    // gfx950's three-input bitwise op (truth table 0x96 = a ^ b ^ c): one instruction per word instead of two
+#if defined(__HIP_DEVICE_COMPILE__) && __has_builtin(__builtin_amdgcn_bitop3_b32)
+    // gfx950's three-input bitwise op (truth table 0x96 = a ^ b ^ c): one instruction per word instead of two (a
+    // target without it, e.g. ARCH=gfx942, takes the two-XOR form below: the same words)
     n.x = __builtin_amdgcn_bitop3_b32((uint32_t)(p1 >> 32), c.y, k0, 0x96);
     n.z = __builtin_amdgcn_bitop3_b32((uint32_t)(p0 >> 32), c.w, k1, 0x96);
 #else

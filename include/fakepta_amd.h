@@ -209,7 +209,9 @@ int fpta_batch_info(fpta_ctx* ctx, int64_t* info);
  * relative aliasing bound exp(-pi w sqrt(1 - 1/sigma)) of the width/oversampling options in force (auto
  * selection takes the gridded path only when it is <= 2e-12), out[10] width w, out[11] oversampling sigma,
  * out[12] grid signals of the plan (signals after FPTA_OPT_GRID_COALESCE), out[13] layout signals, out[14]
- * mean band rows per chunk (all grid signals, padded to 4).
+ * mean band rows per chunk (all grid signals, padded to 4), out[15] the interpolation kernel of the last gridded
+ * block: 0 none, else 1 + 4 kind + 2 (white / ECORR epilogue) + (fused partial checksums), kind 0
+ * k_grid_interp_mfma, 1 k_grid_interp_ws, 2 k_grid_interp_ws2, 3 k_grid_interp_lds, 4 k_grid_interp_st.
  * fpta_batch_grid_info_n writes the first min(n_out, FPTA_GRID_INFO_LEN) values and returns FPTA_GRID_INFO_LEN
  * (negative on error); fpta_batch_grid_info keeps the round-1 contract: out[0..8], host double[9]. */
 #define FPTA_GRID_INFO_LEN 16
@@ -315,7 +317,10 @@ int fpta_comm_gather(fpta_comm* comm, const double* send, int64_t count, double*
                                      workgroups per CU) when the padded realization count leaves fewer idle
                                      compute waves in 256- than in 512-realization tiles (C4: R = 256); 2 ws also
                                      for blocks with fused partial checksums; 3 ws2 for every plain block; 0 the
-                                     register-pipelined k_grid_interp_mfma. Results are identical. */
+                                     register-pipelined k_grid_interp_mfma; 4 k_grid_interp_st for every block
+                                     (compute waves hand their sums to storer waves through LDS; the storers add
+                                     white noise / ECORR, store and reduce partial checksums). Results are
+                                     identical. */
 #define FPTA_OPT_SIDE_SPLIT 16    /* pipelined gridded blocks (FPTA_OPT_OVERLAP): 1 (default) the grid signal with
                                      the largest DFT, when it has no common (ORF-mixed) member, is drawn and
                                      transformed on a second side stream, beside the other signals' draws, mixing

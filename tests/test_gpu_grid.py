@@ -450,17 +450,19 @@ def test_warp_specialised_interpolation_is_bitwise_identical(ctx, capi, shipped,
         ctx.set_option(capi.OPT_SYNTH_PATH, 4)
         ctx.set_option(capi.OPT_FUSE_CHECKSUMS, fuse)
         res = {}
-        for ws in (0, 1, 2, 3):  # 2: WS also for fused-checksum blocks; 3: k_grid_interp_ws2 (two workgroups per CU)
+        # 2: WS also for fused-checksum blocks; 3: k_grid_interp_ws2 (two workgroups per CU); 4: k_grid_interp_st
+        # (storer waves)
+        for ws in (0, 1, 2, 3, 4):
             ctx.set_option(capi.OPT_INTERP_WS, ws)
             res[ws] = (ctx.batch_synth(5, 300, R), ctx.batch_checksums())
-        for ws in (1, 2, 3):
+        for ws in (1, 2, 3, 4):
             np.testing.assert_array_equal(res[0][0], res[ws][0])
             np.testing.assert_array_equal(res[0][1], res[ws][1])
     finally:
         ctx.set_options(shipped)
 
 
-@pytest.mark.parametrize("ws", [0, 1, 2, 3])
+@pytest.mark.parametrize("ws", [0, 1, 2, 3, 4])
 @pytest.mark.parametrize("R", [1100, 1696])
 def test_partial_realization_blocks_write_every_sample(ctx, capi, shipped, ws, R):
     """Regression: R_pad not a multiple of 512 (a C3 shard's last batch of 1696) gives persistent interpolation
@@ -488,6 +490,48 @@ def test_partial_realization_blocks_write_every_sample(ctx, capi, shipped, ws, R
         np.testing.assert_allclose(sums[:, 0], got.sum(axis=1), rtol=1e-10, atol=1e-12 * np.abs(got).max())
         np.testing.assert_allclose(sums[:, 1], (got * got).sum(axis=1), rtol=1e-10)
     finally:
+        ctx.set_options(shipped)
+
+
+@pytest.mark.parametrize("fuse", [0, 1])
+@pytest.mark.parametrize("R", [128, 256, 333, 1100])
+def test_storer_interpolation_white_ecorr_is_bitwise_identical(ctx, capi, shipped, fuse, R):
+    """FPTA_OPT_INTERP_WS 4 (k_grid_interp_st: compute waves hand their sums to storer waves through LDS; the storers
+    add white noise and ECORR, store, and reduce the partial checksums) returns the register kernel's block and
+    checksums bit for bit with the white / ECORR epilogue, on a ragged layout whose pulsars start at odd TOA offsets
+    (the misaligned white-noise words), for realization counts whose last tile holds fewer than four units; and the
+    block matches the oracle."""
+    rng = np.random.default_rng(59)
+    offs, toas, nu = random_layout(rng, 9, (31, 180))
+    ctx.batch_set_toas(offs, toas, nu)
+    f, a = per_psr_signal(rng, offs, toas, 30)
+    ctx.batch_add_signal(0, f, a, idx=0.0)
+    f2, a2 = per_psr_signal(rng, offs, toas, 60)
+    ctx.batch_add_signal(0, f2, a2, idx=2.0)
+    sigma = rng.uniform(1e-7, 1e-6, offs[-1])
+    blocks = [np.arange(s, min(s + 3, offs[-1])) for s in range(0, offs[-1], 5)]
+    es = rng.uniform(1e-8, 1e-7, len(blocks))
+    ctx.batch_set_white(sigma, blocks, es)
+    try:
+        ctx.set_option(capi.OPT_SYNTH_PATH, 4)
+        ctx.set_option(capi.OPT_FUSE_CHECKSUMS, fuse)
+        res = {}
+        for ws in (0, 4):
+            ctx.set_option(capi.OPT_INTERP_WS, ws)
+            ctx.batch_synth(13, 0, R, to_host=False)
+            ctx.debug_fill_out(np.nan)
+            res[ws] = (ctx.batch_synth(13, 5, R), ctx.batch_checksums())
+        assert np.all(np.isfinite(res[4][0]))
+        np.testing.assert_array_equal(res[0][0], res[4][0])
+        np.testing.assert_array_equal(res[0][1], res[4][1])
+        block_of = -np.ones(offs[-1], dtype=np.int64)
+        for b, q in enumerate(blocks):
+            block_of[q] = b
+        segs = [O.Segment(0, 2 * np.pi * f, a, 0.0), O.Segment(0, 2 * np.pi * f2, a2, 2.0)]
+        want = O.batch_synth(offs, toas, nu, segs, 13, 5, R, sigma=sigma, block_of=block_of, ecorr_sigma=es)
+        assert_parity(res[4][0], want, TOL)
+    finally:
+        ctx.batch_set_white()
         ctx.set_options(shipped)
 
 
