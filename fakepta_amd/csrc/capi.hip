@@ -191,6 +191,7 @@ struct fpta_ctx {
   int overlap = 1;
   int interp_ws = 1;      // gridded interpolation on the warp-specialised kernel (FPTA_OPT_INTERP_WS)
   int last_interp = 0;    // interpolation kernel of the last gridded block: 1 + 4 kind + 2 white + part (0: none)
+  int ecorr_inline = 0;   // gridded white epilogue makes the ECORR epoch normals from their counters (FPTA_OPT_ECORR_INLINE)
   int grid_coalesce = 1;  // gridded path: signals sharing w0 and the chromatic weight share one grid (FPTA_OPT_GRID_COALESCE)
   int async_sums = 0;    // streamed jobs: partial-checksum reductions on their own stream (FPTA_OPT_ASYNC_SUMS; measured
                          // no faster on C3, profiles/r03h_ab_c3_async_sums.txt: the reductions then compete with the interpolation)
@@ -1325,10 +1326,12 @@ int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad, bool pipe = fa
   } else if (c->interp_ws && !c->interp_lds && !a.w_on && !a.accumulate && (!a.part || c->interp_ws == 2)) {
     kind = 1;
     HIPCHK(c, launch_grid_interp_ws(c->stream, a, band, R_pad), "k_grid_interp_ws launch");
+#ifdef FPTA_DIAG_KERNELS
   } else if (c->interp_lds && G.lds_ok && !a.w_on) {
     kind = 3;
     GridLds lds{G.groups.as<int4>(), G.urows.as<int32_t>(), G.lrows.as<int32_t>(), G.n_groups, G.lds_rows};
     HIPCHK(c, launch_grid_interp_lds(c->stream, a, band, lds, R_pad), "k_grid_interp_lds launch");
+#endif
   } else {
     kind = 0;
     HIPCHK(c, launch_grid_interp_mfma(c->stream, a, band, R_pad), "k_grid_interp_mfma launch");
@@ -1724,6 +1727,9 @@ int fpta_set_option(fpta_ctx* c, int32_t key, int64_t value) {
       c->overlap = value ? 1 : 0;
       return FPTA_OK;
     case FPTA_OPT_INTERP_LDS:
+#ifndef FPTA_DIAG_KERNELS
+      if (value) return fail(c, FPTA_EINVAL, "interp_lds: k_grid_interp_lds is a diagnostic kernel, not in this build");
+#endif
       c->interp_lds = value ? 1 : 0;
       return FPTA_OK;
     case FPTA_OPT_DFT_GEN:
@@ -1735,6 +1741,9 @@ int fpta_set_option(fpta_ctx* c, int32_t key, int64_t value) {
       return FPTA_OK;
     case FPTA_OPT_ASYNC_SUMS:
       c->async_sums = value ? 1 : 0;
+      return FPTA_OK;
+    case FPTA_OPT_ECORR_INLINE:
+      c->ecorr_inline = value ? 1 : 0;
       return FPTA_OK;
     case FPTA_OPT_GRID_COALESCE:
       c->grid_coalesce = value ? 1 : 0;
@@ -1787,16 +1796,20 @@ int fpta_get_option(fpta_ctx* c, int32_t key, int64_t* value) {
     case FPTA_OPT_DFT_GEN: *value = c->dft_gen; return FPTA_OK;
     case FPTA_OPT_GEN_MIX: *value = c->gen_mix; return FPTA_OK;
     case FPTA_OPT_ASYNC_SUMS: *value = c->async_sums; return FPTA_OK;
+    case FPTA_OPT_ECORR_INLINE: *value = c->ecorr_inline; return FPTA_OK;
   }
   return fail(c, FPTA_EINVAL, "get_option: unknown key");
 }
 
 int fpta_build_flags(void) {
+  int f = 0;
 #ifdef FPTA_DEBUG
-  return FPTA_BUILD_DEBUG;
-#else
-  return 0;
+  f |= FPTA_BUILD_DEBUG;
 #endif
+#ifdef FPTA_DIAG_KERNELS
+  f |= FPTA_BUILD_DIAG;
+#endif
+  return f;
 }
 
 int fpta_synchronize(fpta_ctx* c) {
@@ -2132,20 +2145,22 @@ static int batch_common(fpta_ctx* c, uint64_t seed, int64_t real0, int32_t n_rea
     wc.real0 = real0;
     wc.k0 = k0;
     wc.k1 = k1;
-    if (c->has_blocks) {  // ECORR epoch normals of this batch, needed by either white path
-      HIPCHK(c, c->zb_epochs.ensure(sizeof(double) * (size_t)n_real * c->n_blocks), "zb alloc");
-      wc.zb = c->zb_epochs.as<double>();
-      KTimer kt(c, FPTA_K_WHITE);
-      HIPCHK(c, launch_epoch_normals(c->stream, c->n_blocks, n_real, real0, k0, k1, c->zb_epochs.as<double>()),
-             "k_epoch_normals launch");
-    }
+  }
+  int path = 0;
+  if (!L.segs.empty() && (rc = select_path(c, L, n_real, true, &path))) return rc;
+  // ECORR epoch normals of this batch as a [R][n_epochs] block, for the exact paths and the separate white pass; the
+  // gridded interpolation's fused epilogue makes them from their counters instead (FPTA_OPT_ECORR_INLINE)
+  if (do_white && c->has_blocks && !(path == 4 && c->fuse_white && c->ecorr_inline)) {
+    HIPCHK(c, c->zb_epochs.ensure(sizeof(double) * (size_t)n_real * c->n_blocks), "zb alloc");
+    wc.zb = c->zb_epochs.as<double>();
+    KTimer kt(c, FPTA_K_WHITE);
+    HIPCHK(c, launch_epoch_normals(c->stream, c->n_blocks, n_real, real0, k0, k1, c->zb_epochs.as<double>()),
+           "k_epoch_normals launch");
   }
   bool fused = false;
   if (L.segs.empty()) {
     HIPCHK(c, hipMemsetAsync(c->out.p, 0, out_bytes, c->stream), "out memset");
   } else {
-    int path = 0;
-    if ((rc = select_path(c, L, n_real, true, &path))) return rc;
     // grid signals with a per-pulsar member draw inside their DFT (not for validation draws or coefficient downloads,
     // which need every signal's coefficients in the buffer)
     c->gen_fused = path == 4 && !zin && !coeffs_out && c->dft_gen && (c->grid_mfma & 1);

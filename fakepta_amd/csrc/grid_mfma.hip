@@ -39,9 +39,6 @@ __device__ __forceinline__ int4 ld_uniform4(const void* p) {
 #ifndef FPTA_INTERP_WPC
 #define FPTA_INTERP_WPC 2
 #endif
-#ifndef FPTA_INTERP_DIAG
-#define FPTA_INTERP_DIAG 0  // 0 in every product build
-#endif
 #ifndef FPTA_INTERP_DEPTH
 #define FPTA_INTERP_DEPTH 2
 #endif
@@ -386,6 +383,9 @@ hipError_t launch_coef_merge(hipStream_t st, const CoefMerge& m, int32_t P, int3
 __device__ __attribute__((noinline)) double white_one(uint64_t t, uint64_t g, uint32_t k0, uint32_t k1) {
   return quad_normal(t, kWhiteStream, g, k0, k1);
 }
+__device__ __attribute__((noinline)) double ecorr_one(uint64_t b, uint64_t g, uint32_t k0, uint32_t k1) {
+  return quad_normal(b, kEcorrStream, g, k0, k1);
+}
 __device__ __forceinline__ void white_quad(int64_t t, int64_t g, uint32_t k0, uint32_t k1, double (&z)[4]) {
   if (((t | g) & 1) == 0) {
     quad4((uint64_t)t, kWhiteStream, (uint64_t)g, k0, k1, z);
@@ -451,6 +451,47 @@ __device__ __forceinline__ void interp_white(const SynthArgs& a, const InterpTil
   // epoch 0 against es = 0.
   const bool ecorr = a.w_block_of != nullptr;
   const int64_t e0 = ep[0] >= 0 ? ep[0] : 0, e1 = ep[1] >= 0 ? ep[1] : 0;
+  if (ecorr && !a.w_zb) {
+    // ECORR epoch normals made here from their counters (oracle quad_normals on the ECORR stream: the words of
+    // k_epoch_normals) instead of read back from a [R][n_epochs] block: one Philox call gives epochs (2 i, 2 i + 1) x
+    // realizations (g, g + 1), so a TOA pair whose epochs share a pair takes one call per realization pair
+#pragma unroll
+    for (int m = 0; m < NP; ++m) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int rl = t.r0 + 32 * m + 2 * (lg + 4 * g);
+        const int64_t gg = a.real0 + rl;
+        double ze[2][2];  // [TOA parity][realization h]
+        if ((gg & 1) == 0) {
+          double z[4];
+          quad4((uint64_t)(e0 & ~(int64_t)1), kEcorrStream, (uint64_t)gg, a.k0, a.k1, z);
+          ze[0][0] = z[2 * (e0 & 1)];
+          ze[0][1] = z[2 * (e0 & 1) + 1];
+          if ((e1 >> 1) != (e0 >> 1)) quad4((uint64_t)(e1 & ~(int64_t)1), kEcorrStream, (uint64_t)gg, a.k0, a.k1, z);
+          ze[1][0] = z[2 * (e1 & 1)];
+          ze[1][1] = z[2 * (e1 & 1) + 1];
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            ze[i >> 1][i & 1] = ecorr_one((uint64_t)((i >> 1) ? e1 : e0), (uint64_t)(gg + (i & 1)), a.k0, a.k1);
+        }
+        if (a.w_sigma) {
+          double z[4];
+          white_quad(tg, gg, a.k0, a.k1, z);
+#pragma unroll
+          for (int e = 0; e < 2; ++e)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) acc[e][2 * m + h][g] = fma(sg[e], z[2 * e + h], acc[e][2 * m + h][g]);
+        }
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+#pragma unroll
+          for (int h = 0; h < 2; ++h) acc[e][2 * m + h][g] = fma(es[e], ze[e][h], acc[e][2 * m + h][g]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    return;
+  }
   auto zb_load = [&](int mg, double (&z)[2][2]) {
     const int rl = t.r0 + 32 * (mg >> 2) + 2 * (lg + 4 * (mg & 3));
 #pragma unroll
@@ -575,17 +616,6 @@ __device__ __forceinline__ void interp_store_rows(const SynthArgs& a, double* __
   const int tt = 2 * lr;  // this lane's even TOA in the chunk; tt + 1 the odd one
   if (tt >= t.cnt) return;
   const int64_t tg = ld_uniform(a.offs + t.p) + t.y + tt;
-#if FPTA_INTERP_DIAG == 2 || FPTA_INTERP_DIAG == 7  // diagnostic builds only: no stores (one conditional store keeps every sum live)
-  {
-    double s = 0.0;
-#pragma unroll
-    for (int e = 0; e < 2; ++e)
-#pragma unroll
-      for (int i = 0; i < RW; ++i) s += acc[e][i][0] + acc[e][i][1] + acc[e][i][2] + acc[e][i][3];
-    if (s == 12345.678) out[tg] = s;
-    return;
-  }
-#endif
   // fast path (full chunk, every realization of the tile stored, no accumulate, 16-byte aligned rows): straight-line
   // 16-byte stores from a wave-uniform row base plus one 32-bit lane offset, no per-store tests. The general path
   // below spends ~28 instructions and several branches per store, which held the SIMD's issue while the partner
@@ -630,11 +660,7 @@ __device__ __forceinline__ void interp_store_rows(const SynthArgs& a, double* __
           if (pair) v1 += o[1];
         }
         if (vec) {
-#if FPTA_INTERP_DIAG == 3  // diagnostic build only: non-temporal (streaming) stores
-          __builtin_nontemporal_store(dbl2{v0, v1}, (dbl2*)o);
-#else
           *(dbl2*)o = dbl2{v0, v1};
-#endif
         } else {
           o[0] = v0;
           if (pair) o[1] = v1;
@@ -700,27 +726,13 @@ __global__ __launch_bounds__(256, FPTA_INTERP_WPC) void k_grid_interp_mfma(Synth
     const int src = blk == 0 ? t.rr[0] : (blk == 1 ? t.rr[1] : (blk == 2 ? t.rr[2] : t.rr[3]));
     const int row = __builtin_amdgcn_ds_bpermute(((4 * qq + lg) & 63) << 2, src);
     FPTA_DCHECK(row >= 0 && row < band.grid_rows, "k_grid_interp_mfma grid row", row, band.grid_rows);
-#if FPTA_INTERP_DIAG == 1 || FPTA_INTERP_DIAG == 7  // diagnostic builds only (tools/interp_variants.sh): every step reads one L1-resident row
-    const double* __restrict__ gr = t.G0 + (int64_t)(row & 3) * R_pad;
-#else
     const double* __restrict__ gr = t.G0 + (int64_t)row * R_pad;
-#endif
 #pragma unroll
     for (int m = 0; m < NP; ++m) av[m] = *(const dbl2*)(gr + 32 * m);
     bv = *(const dbl2*)(t.Wp + 4 * kGridTT * qq);
   };
   d4 acc[2][RW];  // [TOA parity][realization tile]
   auto mfma = [&](const dbl2(&av)[NP], const dbl2& bv) {
-#if FPTA_INTERP_DIAG == 8  // diagnostic build only: accumulators pinned to AGPRs (MFMA by inline asm)
-#pragma unroll
-    for (int m = 0; m < NP; ++m) {
-      asm volatile("v_mfma_f64_16x16x4_f64 %0, %1, %2, %0" : "+a"(acc[0][2 * m]) : "v"(av[m].x), "v"(bv.x));
-      asm volatile("v_mfma_f64_16x16x4_f64 %0, %1, %2, %0" : "+a"(acc[0][2 * m + 1]) : "v"(av[m].y), "v"(bv.x));
-      asm volatile("v_mfma_f64_16x16x4_f64 %0, %1, %2, %0" : "+a"(acc[1][2 * m]) : "v"(av[m].x), "v"(bv.y));
-      asm volatile("v_mfma_f64_16x16x4_f64 %0, %1, %2, %0" : "+a"(acc[1][2 * m + 1]) : "v"(av[m].y), "v"(bv.y));
-    }
-    return;
-#endif
 #pragma unroll
     for (int m = 0; m < NP; ++m) {
       acc[0][2 * m] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m].x, bv.x, acc[0][2 * m], 0, 0, 0);
@@ -732,13 +744,6 @@ __global__ __launch_bounds__(256, FPTA_INTERP_WPC) void k_grid_interp_mfma(Synth
 
   int tile = x * per + (int)(blockIdx.x >> 3);
   if (tile >= end) return;
-#if FPTA_INTERP_DIAG == 5  // diagnostic build only: every other workgroup starts half a tile late (phase stagger)
-  if ((blockIdx.x >> 3) & 1)
-    for (int i = 0; i < 2; ++i) __builtin_amdgcn_s_sleep(127);
-#endif
-#if FPTA_INTERP_DIAG == 9  // diagnostic build only: the 8 waves of a CU start 0..7 units of ~3.4 us apart
-  for (int i = 0; i < wave + 4 * ((blockIdx.x >> 3) & 1); ++i) __builtin_amdgcn_s_sleep(127);
-#endif
   InterpTile<RW> cur;
   setup(tile, cur);
   FPTA_DCHECK(R_pad % (16 * RW) == 0, "k_grid_interp_mfma realization padding", R_pad % (16 * RW), 1);
@@ -762,11 +767,7 @@ __global__ __launch_bounds__(256, FPTA_INTERP_WPC) void k_grid_interp_mfma(Synth
 #pragma unroll
       for (int i = 0; i < RW; ++i) acc[e][i] = d4{0.0, 0.0, 0.0, 0.0};
     // each operand set is refilled kInterpDepth steps ahead right after its MFMAs
-#if FPTA_INTERP_DIAG == 4  // diagnostic build only: no band loop (the epilogue stores zeros): the store stream alone
-    for (int q = cur.nq; q < cur.nq; q += kInterpDepth) {
-#else
     for (int q = 0; q < cur.nq; q += kInterpDepth) {
-#endif
       __builtin_amdgcn_sched_barrier(0);
       mfma(a0, b0);
       __builtin_amdgcn_sched_barrier(0);
@@ -895,18 +896,6 @@ __global__ __launch_bounds__(512, 1) void k_grid_interp_ws(SynthArgs a, GridBand
     setup();
     auto issue = [&]() {
       double* slot = ring + (issued % kWsSlots) * kWsSlot;
-#if FPTA_INTERP_DIAG == 6  // diagnostic build only: the producers load nothing (stale operands, same barriers)
-      if (issued >= 0) {
-        ++issued;
-        if (++q == nq) {
-          q = 0;
-          tile += stride;
-          valid = tile < end;
-          if (valid) setup();
-        }
-        return;
-      }
-#endif
       const int4 r4 = ld_uniform4(band.rows + (int64_t)c * band.vmax + 4 * q);  // the step's 4 rows
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -985,9 +974,7 @@ __global__ __launch_bounds__(512, 1) void k_grid_interp_ws(SynthArgs a, GridBand
     for (int q = 0; q < t.nq; ++q, ++S) {
       ws_barrier();  // step S + 1 has landed; step S - 1's slot may now be refilled
       read(S + 1, a1, b1);
-#if FPTA_INTERP_DIAG != 4  // diagnostic build 4: no MFMA steps (the epilogue stores zeros)
       mfma(a0, b0);
-#endif
       ws_wait_lgkm0();
 #pragma unroll
       for (int m = 0; m < NP; ++m) a0[m] = a1[m];
@@ -1327,6 +1314,11 @@ __global__ __launch_bounds__(512, 1) void k_grid_interp_st(SynthArgs a, GridBand
         const int s = q + kStLead, s1 = s + 1;
         const bool in = s < cur.nq, in1 = s1 < cur.nq;
         const int kn = (k + kStLead) % kStSets;
+#if FPTA_ST_DIAG == 3  // diagnostic build only: operands loaded for every other step (half the load instructions)
+        if ((k & 1) == 0)
+#elif FPTA_ST_DIAG == 4  // diagnostic build only: no operand loads after the prefetch (stale operands)
+        if (false)
+#endif
         load(in ? cur.G0 : nxt.G0, in ? cur.W0 : nxt.W0, in ? s : s - cur.nq, rn, av[kn], bv[kn]);
         rn = ld_uniform4((in1 ? cur.rowp : nxt.rowp) + 4 * (in1 ? s1 : min(s1 - cur.nq, nxt.nq - 1)));
       }
@@ -1377,136 +1369,6 @@ hipError_t launch_grid_interp_st(hipStream_t st, const SynthArgs& a, const GridB
   auto kernel = a.w_on ? (a.part ? k_grid_interp_st<true, true> : k_grid_interp_st<true, false>)
                        : (a.part ? k_grid_interp_st<false, true> : k_grid_interp_st<false, false>);
   hipLaunchKernelGGL(kernel, dim3((unsigned)grid), dim3(512), 0, st, a, band, (int32_t)tiles, (int32_t)n_units, R_pad,
-                     a.out);
-  return hipGetLastError();
-}
-
-// ----------------------------------------------------------------------------- k_grid_interp_lds
-// The interpolation with the grid rows staged in LDS. A workgroup takes a group of <= 4 consecutive chunks of
-// one pulsar (host plan) for one block of 128 realizations; wave w computes chunk w of the group (the MFMA
-// structure of k_grid_interp_mfma: even/odd TOA B-tiles, realization tile pairs, 16-byte stores). The union of
-// the group's band rows over all signals (U <= kLdsRowsMax) is loaded once per workgroup with direct-to-LDS
-// 16-byte loads (one wave-instruction = one 1 KB row of 128 realizations), so a grid row shared by the group's
-// chunks (consecutive chunks' bands overlap by ~3/4) crosses the memory pipeline once instead of once per
-// chunk; A operands are then ds_read_b128 from LDS and only the weights come from global memory.
-constexpr int kLdsPitch = 130;  // doubles per LDS row: 1 KB of realizations + 16 B (rows start 4 banks apart)
-
-template <bool WHITE, bool PART>
-__global__ __launch_bounds__(256, 2) void k_grid_interp_lds(SynthArgs a, GridBand band, GridLds plan,
-                                                            int32_t n_tiles, int32_t R_pad, double* __restrict__ out) {
-  constexpr int RW = 8, NP = RW / 2;
-  extern __shared__ __attribute__((aligned(16))) double Gs[];  // [U][kLdsPitch]
-  const int per = (n_tiles + 7) >> 3;
-  const int x = blockIdx.x & 7;
-  const int stride = gridDim.x >> 3;
-  const int end = min(n_tiles, (x + 1) * per);
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  const int lr = lane & 15, lg = lane >> 4;
-  const int n_rb = R_pad / (16 * RW);
-  d4 acc[2][RW];
-  auto mfma = [&](const dbl2(&av)[NP], const dbl2& bv) {
-#pragma unroll
-    for (int m = 0; m < NP; ++m) {
-      acc[0][2 * m] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m].x, bv.x, acc[0][2 * m], 0, 0, 0);
-      acc[0][2 * m + 1] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m].y, bv.x, acc[0][2 * m + 1], 0, 0, 0);
-      acc[1][2 * m] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m].x, bv.y, acc[1][2 * m], 0, 0, 0);
-      acc[1][2 * m + 1] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m].y, bv.y, acc[1][2 * m + 1], 0, 0, 0);
-    }
-  };
-  for (int tile = x * per + (int)(blockIdx.x >> 3); tile < end; tile += stride) {
-    const int g = __builtin_amdgcn_readfirstlane(tile / n_rb);
-    const int rb = __builtin_amdgcn_readfirstlane(tile - g * n_rb);
-    const int4 gi = plan.groups[g];
-    const int c0 = __builtin_amdgcn_readfirstlane(gi.x), nc = __builtin_amdgcn_readfirstlane(gi.y);
-    const int U = __builtin_amdgcn_readfirstlane(gi.z), uoff = __builtin_amdgcn_readfirstlane(gi.w);
-    FPTA_DCHECK(U <= plan.lds_rows, "k_grid_interp_lds union rows", U, plan.lds_rows + 1);
-    const int r0 = rb * 16 * RW;
-    // the union's grid rows in registers (lane l: row l + 64 i), then wave w stages rows w, w + 4, ...
-    int ur[(kLdsRowsMax + 63) / 64];
-#pragma unroll
-    for (int i = 0; i < (kLdsRowsMax + 63) / 64; ++i) ur[i] = plan.urows[uoff + min(64 * i + lane, U - 1)];
-    __syncthreads();  // every wave is done reading the previous tile's rows
-    for (int row = wave; row < U; row += 4) {
-      const int blk = row >> 6;
-      const int src_reg = blk == 0 ? ur[0] : (blk == 1 ? ur[1] : ur[2]);
-      const int grow = __builtin_amdgcn_readlane(src_reg, row & 63);
-      FPTA_DCHECK(grow >= 0 && grow < band.grid_rows, "k_grid_interp_lds grid row", grow, band.grid_rows);
-      __builtin_amdgcn_global_load_lds((const void*)(band.g + (int64_t)grow * R_pad + r0 + 2 * lane),
-                                       (__attribute__((address_space(3))) void*)(Gs + row * kLdsPitch), 16, 0, 0);
-    }
-    __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0) expcnt(0) lgkmcnt(0): this wave's staged rows have landed
-    __syncthreads();
-    if (wave < nc) {
-      InterpTile<RW> t;
-      t.c = c0 + wave;
-      const int4 ci = band.chunks[t.c];
-      t.p = __builtin_amdgcn_readfirstlane(ci.x);
-      t.y = __builtin_amdgcn_readfirstlane(ci.y);
-      t.cnt = __builtin_amdgcn_readfirstlane(ci.z);
-      t.nq = __builtin_amdgcn_readfirstlane(ci.w) >> 2;
-      t.r0 = r0;
-      // the chunk's LDS slots in registers (lane l: band row l + 64 i), a step's 4 slots by one ds_bpermute
-      const int32_t* __restrict__ lt = plan.lrows + (int64_t)t.c * band.vmax;
-      const int V = 4 * t.nq;
-      const int rr0 = lt[min(lane, V - 1)], rr1 = lt[min(64 + lane, V - 1)];
-      const int rr2 = lt[min(128 + lane, V - 1)], rr3 = lt[min(192 + lane, V - 1)];
-      const double* __restrict__ Wp = band.wd + ((int64_t)t.c * band.vmax + lg) * kGridTT + 2 * lr;
-#pragma unroll
-      for (int e = 0; e < 2; ++e)
-#pragma unroll
-        for (int i = 0; i < RW; ++i) acc[e][i] = d4{0.0, 0.0, 0.0, 0.0};
-      auto load = [&](int qq, dbl2(&av)[NP], dbl2& bv) {
-        const int blk = qq >> 4;  // 64-row block of the step's rows (uniform)
-        const int src = blk == 0 ? rr0 : (blk == 1 ? rr1 : (blk == 2 ? rr2 : rr3));
-        const int slot = __builtin_amdgcn_ds_bpermute(((4 * qq + lg) & 63) << 2, src);
-        FPTA_DCHECK(slot >= 0 && slot < U, "k_grid_interp_lds slot", slot, U);
-        const double* gs = Gs + slot * kLdsPitch + 2 * lr;
-#pragma unroll
-        for (int m = 0; m < NP; ++m) av[m] = *(const dbl2*)(gs + 32 * m);
-        bv = *(const dbl2*)(Wp + 4 * kGridTT * qq);
-      };
-      // two operand sets, each refilled two steps ahead right after its MFMAs
-      dbl2 a0[NP], a1[NP], b0, b1;
-      load(0, a0, b0);
-      load(min(1, t.nq - 1), a1, b1);
-      for (int q = 0; q < t.nq; q += 2) {
-        mfma(a0, b0);
-        if (q + 2 < t.nq) load(q + 2, a0, b0);
-        if (q + 1 < t.nq) {
-          mfma(a1, b1);
-          if (q + 3 < t.nq) load(q + 3, a1, b1);
-        }
-      }
-      if constexpr (WHITE) interp_white<RW>(a, t, acc);
-      interp_store<PART, RW>(a, out, t, acc);
-    }
-  }
-}
-
-hipError_t launch_grid_interp_lds(hipStream_t st, const SynthArgs& a, const GridBand& band, const GridLds& lds,
-                                  int32_t R_pad) {
-  constexpr int RW = 8;
-  if (lds.n_groups <= 0 || lds.lds_rows <= 0 || lds.lds_rows > kLdsRowsMax || R_pad % (16 * RW) != 0 ||
-      band.vmax > kGridVMax)
-    return hipErrorInvalidValue;
-  const int64_t tiles = (int64_t)lds.n_groups * (R_pad / (16 * RW));
-  if (tiles > 0x7FFFFFFF) return hipErrorInvalidValue;
-  const size_t lds_bytes = sizeof(double) * (size_t)lds.lds_rows * kLdsPitch;
-  static int n_cu = 0;
-  if (!n_cu) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0)
-      n_cu = 256;
-  }
-  const int64_t per_cu = std::max<int64_t>(1, std::min<int64_t>(2, (int64_t)(160 * 1024) / (int64_t)lds_bytes));
-  const int64_t grid = std::min<int64_t>((tiles + 7) / 8 * 8, (n_cu * per_cu + 7) / 8 * 8);
-  // the white epilogue's Philox rounds do not fit beside the LDS kernel's registers (52 VGPRs spilled):
-  // white-noise blocks take k_grid_interp_mfma (launch_grid_interp_mfma)
-  if (a.w_on) return hipErrorInvalidValue;
-  auto kernel = a.part ? k_grid_interp_lds<false, true> : k_grid_interp_lds<false, false>;
-  hipLaunchKernelGGL(kernel, dim3((unsigned)grid), dim3(256), lds_bytes, st, a, band, lds, (int32_t)tiles, R_pad,
                      a.out);
   return hipGetLastError();
 }
@@ -1881,5 +1743,9 @@ hipError_t launch_part_checksums(hipStream_t st, const double* part, int32_t n_c
                      sums);
   return hipGetLastError();
 }
+
+#ifdef FPTA_DIAG_KERNELS
+#include "diag/interp_lds.inc"
+#endif
 
 }  // namespace fpta

@@ -301,7 +301,8 @@ int fpta_comm_gather(fpta_comm* comm, const double* send, int64_t count, double*
 #define FPTA_OPT_OVERLAP 12       /* batch synthesis with several signals: 1 (default) draws each signal's
                                      coefficients on a second stream so the gridded DFT of one signal overlaps
                                      the draws of the next; 0 one stream. Results are identical. */
-#define FPTA_OPT_INTERP_LDS 13    /* gridded interpolation: 1 stages each chunk group's grid rows in LDS
+#define FPTA_OPT_INTERP_LDS 13    /* diagnostic builds only (FPTA_BUILD_DIAG; the product library refuses 1):
+                                     gridded interpolation: 1 stages each chunk group's grid rows in LDS
                                      (k_grid_interp_lds) where every group fits and no white noise is fused;
                                      0 (default, faster on MI355X) the register-tiled k_grid_interp_mfma.
                                      Results are identical. */
@@ -336,12 +337,18 @@ int fpta_comm_gather(fpta_comm* comm, const double* send, int64_t count, double*
 #define FPTA_OPT_ASYNC_SUMS 19    /* streamed jobs (fpta_batch_synth_checksums, fpta_multi_synth): 1 a block's partial
                                      checksums are reduced on a stream of their own, beside the next block, into one
                                      of two partials buffers; 0 (default) on the context stream. Identical results. */
+#define FPTA_OPT_ECORR_INLINE 20  /* gridded path with fused white noise: 1 the interpolation's epilogue makes each ECORR
+                                     epoch normal from its Philox counter (the k_epoch_normals words) instead of
+                                     reading a [R][n_epochs] block written before the interpolation; 0 (default) the
+                                     block. Results are identical. */
 int fpta_set_option(fpta_ctx* ctx, int32_t key, int64_t value);
 /* Current value of option `key` (same keys as fpta_set_option). */
 int fpta_get_option(fpta_ctx* ctx, int32_t key, int64_t* value);
 /* Build flags of the loaded library: FPTA_BUILD_DEBUG when built with -DFPTA_DEBUG (make debug: per-launch
- * synchronisation and device-side bounds checks; never used for measurements). */
+ * synchronisation and device-side bounds checks; never used for measurements); FPTA_BUILD_DIAG when built with
+ * -DFPTA_DIAG_KERNELS (make variant: the measured-and-not-adopted diagnostic kernels, e.g. FPTA_OPT_INTERP_LDS). */
 #define FPTA_BUILD_DEBUG 1
+#define FPTA_BUILD_DIAG 2
 int fpta_build_flags(void);
 /* Kernel ids for fpta_kernel_stats */
 #define FPTA_K_GEN 0

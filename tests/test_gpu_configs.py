@@ -33,7 +33,12 @@ def fibonacci(P):
     return np.stack([np.cos(ph) * np.sin(th), np.sin(ph) * np.sin(th), np.cos(th)], 1)
 
 
-def test_c4_ska_scale(ctx):
+@pytest.mark.parametrize("factor", ["cholesky", "svd"])
+def test_c4_ska_scale(ctx, factor):
+    """factor "cholesky" is the one the C4 measurement runs (fakepta_amd.batch.batch_factor, as BatchSimulator: the
+    Cholesky factor of the positive-definite HD ORF, mixed by the triangular k_mix_mfma at P = 1000); "svd" is numpy's
+    multivariate_normal square root (/root/reference/fakepta/correlated_noises.py:154-155), mixed densely."""
+    from fakepta_amd.batch import batch_factor
     P, n_p, N, R, seed = 1000, 10000, 100, 256, 4242
     rng = np.random.default_rng(0)
     T = 10 * O.JULIAN_YEAR
@@ -41,7 +46,9 @@ def test_c4_ska_scale(ctx):
     toas = (np.linspace(0, T, n_p)[None, :] + rng.uniform(0, 86400, (P, 1))).ravel()
     nu = np.abs(1400.0 + rng.normal(0, 10, P * n_p))
     pos = fibonacci(P)
-    L = O.mvn_factor(O.orf_hd(pos))
+    L = batch_factor(O.orf_hd(pos)) if factor == "cholesky" else O.mvn_factor(O.orf_hd(pos))
+    if factor == "cholesky":
+        assert np.all(np.triu(L, 1) == 0)  # the triangular mixing path
     f = O.freq_grid(N, np.ptp(toas))
     amp = np.sqrt(O.powerlaw(f, -15.0, 13 / 3) * O.delta_f(f))
     ctx.batch_set_toas(offs, toas, nu)
@@ -50,7 +57,7 @@ def test_c4_ska_scale(ctx):
     assert out_none is None and co.shape == (P, 2 * N, R)
     picks = [0, 255]
     rows = np.concatenate([ctx.batch_download(r, 1) for r in picks])
-    sub = [0, 1, 333, 999]
+    sub = [0, 1, 333, 999] if factor == "svd" else [0, 1, 63, 64, 511, 512, 999]  # triangular tile edges
     w = 2 * np.pi * f
     for j, r in enumerate(picks):
         z = np.stack([O.gp_normals(seed, np.array([r]), q, 0, N)[0] for q in range(P)])  # [P, N, 2]

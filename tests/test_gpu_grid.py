@@ -288,7 +288,13 @@ def test_side_stream_draws_are_bitwise_identical(ctx, capi, shipped, path):
 def test_lds_interpolation_is_bitwise_identical(ctx, capi, shipped, fuse):
     """FPTA_OPT_INTERP_LDS: the LDS-staged interpolation (chunk groups, union rows staged once per workgroup)
     returns the register-tiled kernel's block and checksums bit for bit, on a ragged multi-signal layout with
-    pulsar boundaries inside chunk groups and unsorted TOAs."""
+    pulsar boundaries inside chunk groups and unsorted TOAs. A diagnostic kernel (measured slower, not adopted): only
+    in libraries built with -DFPTA_DIAG_KERNELS; the product library refuses the option."""
+    if not capi.build_flags() & capi.BUILD_DIAG:
+        with pytest.raises(capi.FptaError, match="diagnostic"):
+            ctx.set_option(capi.OPT_INTERP_LDS, 1)
+        assert ctx.get_option(capi.OPT_INTERP_LDS) == 0
+        return
     rng = np.random.default_rng(41)
     offs, toas, nu = random_layout(rng, 23, (31, 260))
     perm = rng.permutation(offs[1] - offs[0])
@@ -494,13 +500,15 @@ def test_partial_realization_blocks_write_every_sample(ctx, capi, shipped, ws, R
 
 
 @pytest.mark.parametrize("fuse", [0, 1])
-@pytest.mark.parametrize("R", [128, 256, 333, 1100])
-def test_storer_interpolation_white_ecorr_is_bitwise_identical(ctx, capi, shipped, fuse, R):
+@pytest.mark.parametrize("R,real0", [(128, 5), (256, 8), (333, 5), (1100, 8)])
+def test_storer_interpolation_white_ecorr_is_bitwise_identical(ctx, capi, shipped, fuse, R, real0):
     """FPTA_OPT_INTERP_WS 4 (k_grid_interp_st: compute waves hand their sums to storer waves through LDS; the storers
-    add white noise and ECORR, store, and reduce the partial checksums) returns the register kernel's block and
-    checksums bit for bit with the white / ECORR epilogue, on a ragged layout whose pulsars start at odd TOA offsets
-    (the misaligned white-noise words), for realization counts whose last tile holds fewer than four units; and the
-    block matches the oracle."""
+    add white noise and ECORR, store, and reduce the partial checksums) and FPTA_OPT_ECORR_INLINE 1 (the epilogue
+    makes the ECORR epoch normals from their Philox counters instead of reading k_epoch_normals' block) return the
+    register kernel's block and checksums bit for bit with the white / ECORR epilogue, on a ragged layout whose
+    pulsars start at odd TOA offsets (the misaligned white-noise words), at odd and even first realizations (the
+    one-normal-per-call path), for realization counts whose last tile holds fewer than four units; and the block
+    matches the oracle (/root/reference/fakepta/fake_pta.py:201-230)."""
     rng = np.random.default_rng(59)
     offs, toas, nu = random_layout(rng, 9, (31, 180))
     ctx.batch_set_toas(offs, toas, nu)
@@ -516,20 +524,22 @@ def test_storer_interpolation_white_ecorr_is_bitwise_identical(ctx, capi, shippe
         ctx.set_option(capi.OPT_SYNTH_PATH, 4)
         ctx.set_option(capi.OPT_FUSE_CHECKSUMS, fuse)
         res = {}
-        for ws in (0, 4):
+        for ws, inline in ((0, 0), (4, 0), (0, 1), (4, 1)):
             ctx.set_option(capi.OPT_INTERP_WS, ws)
+            ctx.set_option(capi.OPT_ECORR_INLINE, inline)
             ctx.batch_synth(13, 0, R, to_host=False)
             ctx.debug_fill_out(np.nan)
-            res[ws] = (ctx.batch_synth(13, 5, R), ctx.batch_checksums())
-        assert np.all(np.isfinite(res[4][0]))
-        np.testing.assert_array_equal(res[0][0], res[4][0])
-        np.testing.assert_array_equal(res[0][1], res[4][1])
+            res[ws, inline] = (ctx.batch_synth(13, real0, R), ctx.batch_checksums())
+        for key in ((4, 0), (0, 1), (4, 1)):
+            assert np.all(np.isfinite(res[key][0]))
+            np.testing.assert_array_equal(res[0, 0][0], res[key][0])
+            np.testing.assert_array_equal(res[0, 0][1], res[key][1])
         block_of = -np.ones(offs[-1], dtype=np.int64)
         for b, q in enumerate(blocks):
             block_of[q] = b
         segs = [O.Segment(0, 2 * np.pi * f, a, 0.0), O.Segment(0, 2 * np.pi * f2, a2, 2.0)]
-        want = O.batch_synth(offs, toas, nu, segs, 13, 5, R, sigma=sigma, block_of=block_of, ecorr_sigma=es)
-        assert_parity(res[4][0], want, TOL)
+        want = O.batch_synth(offs, toas, nu, segs, 13, real0, R, sigma=sigma, block_of=block_of, ecorr_sigma=es)
+        assert_parity(res[4, 1][0], want, TOL)
     finally:
         ctx.batch_set_white()
         ctx.set_options(shipped)

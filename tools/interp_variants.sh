@@ -1,4 +1,6 @@
 #!/bin/bash
+# NOTE (round 4): the FPTA_INTERP_DIAG cuts below were removed from the product source; this
+# script reproduces the round-2/3 records only on a checkout of revision 059c9cc or earlier.
 # Build (build) or time (run) compile-time variants of k_grid_interp_mfma: realization tiles per wave (RW),
 # persistent workgroups per CU (WPC), diagnostic cuts (DIAG 1: grid loads from one L1-resident row; 2: no
 # stores; 3: non-temporal stores; 4: no band loop, the store stream alone; 5: every other workgroup starts
