@@ -89,6 +89,13 @@ struct GridPlan {
   bool lds_ok = false;
   int32_t n_groups = 0, lds_rows = 0;
   DevBuf groups, urows, lrows;
+  // k_grid_interp_u plan (GridUnion): groups of <= kUnionGroup chunks with <= kUnionRowsMax union rows; per chunk the
+  // signals' band offsets and union bases; per (chunk, signal, TOA slot) the window's first band row and {d, ch}
+  bool u_ok = false;
+  int32_t u_groups = 0, u_sig = 0;
+  DevBuf ugroups, uurows, ucbase, udch, uwrow;
+  int32_t u_w[kUnionSigMax] = {0, 0};
+  double u_hw[kUnionSigMax] = {0.0, 0.0}, u_beta[kUnionSigMax] = {0.0, 0.0};
   std::vector<GridSeg*> segs;  // one per grid signal
   // grid signals (FPTA_OPT_GRID_COALESCE): members (layout signal indices, ascending), the anchor (the member with
   // the most modes: its coefficient columns receive the others' and its grid/weights serve the group) and the last
@@ -114,6 +121,8 @@ struct GridPlan {
     vmax = 0;
     lds_ok = false;
     n_groups = lds_rows = 0;
+    u_ok = false;
+    u_groups = u_sig = 0;
     grid_rows = 0;
     g_rpad = 0;
     members.clear();
@@ -191,7 +200,6 @@ struct fpta_ctx {
   int overlap = 1;
   int interp_ws = 1;      // gridded interpolation on the warp-specialised kernel (FPTA_OPT_INTERP_WS)
   int last_interp = 0;    // interpolation kernel of the last gridded block: 1 + 4 kind + 2 white + part (0: none)
-  int ecorr_inline = 0;   // gridded white epilogue makes the ECORR epoch normals from their counters (FPTA_OPT_ECORR_INLINE)
   int grid_coalesce = 1;  // gridded path: signals sharing w0 and the chromatic weight share one grid (FPTA_OPT_GRID_COALESCE)
   int async_sums = 0;    // streamed jobs: partial-checksum reductions on their own stream (FPTA_OPT_ASYNC_SUMS; measured
                          // no faster on C3, profiles/r03h_ab_c3_async_sums.txt: the reductions then compete with the interpolation)
@@ -1070,6 +1078,73 @@ int grid_build(fpta_ctx* c, Layout& L) {
   G.lds_ok = lds_ok && !groups.empty();
   G.n_groups = (int32_t)groups.size();
   G.lds_rows = umax;
+  // k_grid_interp_u plan: the same grouping under the tighter LDS budget of two workgroups per CU
+  std::vector<int4> ug;
+  std::vector<int32_t> uur, ucb, uwr;
+  bool u_ok = n_seg <= kUnionSigMax;
+  for (int32_t ci = 0; ci < n_chunks && u_ok;) {
+    const int32_t p = chunks[ci].x;
+    auto span = [&](int32_t s, int32_t n, int64_t& lo, int64_t& end) {
+      lo = band_lo[s][ci];
+      end = band_lo[s][ci] + band_n[s][ci];
+      for (int32_t k = 1; k < n; ++k) {
+        lo = std::min(lo, band_lo[s][ci + k]);
+        end = std::max(end, band_lo[s][ci + k] + (int64_t)band_n[s][ci + k]);
+      }
+    };
+    auto union_rows = [&](int32_t n) {
+      int64_t u = 0, lo, end;
+      for (int32_t s = 0; s < n_seg; ++s) {
+        span(s, n, lo, end);
+        u += end - lo;
+      }
+      return u;
+    };
+    int32_t n = 1;
+    while (n < kUnionGroup && ci + n < n_chunks && chunks[ci + n].x == p && union_rows(n + 1) <= kUnionRowsMax) ++n;
+    const int64_t U = union_rows(n);
+    if (U > kUnionRowsMax) {
+      u_ok = false;
+      break;
+    }
+    ug.push_back(make_int4(ci, n, (int32_t)U, (int32_t)uur.size()));
+    int32_t uoff = 0;
+    std::vector<int32_t> cb((size_t)n * 2 * kUnionSigMax, 0);
+    for (int32_t s = 0; s < n_seg; ++s) {
+      int64_t lo, end;
+      span(s, n, lo, end);
+      for (int64_t j = lo; j < end; ++j)
+        uur.push_back((int32_t)(rowoff[s] + (int64_t)p * nf[s] + ((j % nf[s]) + nf[s]) % nf[s]));
+      for (int32_t k = 0; k < n; ++k) {
+        const int32_t vo = voff[(size_t)s * n_chunks + ci + k];
+        cb[(size_t)k * 2 * kUnionSigMax + s] = vo;
+        cb[(size_t)k * 2 * kUnionSigMax + kUnionSigMax + s] = uoff + (int32_t)(band_lo[s][ci + k] - lo) - vo;
+      }
+      uoff += (int32_t)(end - lo);
+    }
+    for (int32_t k = 0; k < n; ++k)
+      for (int32_t s = n_seg; s < kUnionSigMax; ++s) {  // absent signals: never selected (offset past every row)
+        cb[(size_t)k * 2 * kUnionSigMax + s] = 1 << 20;
+        cb[(size_t)k * 2 * kUnionSigMax + kUnionSigMax + s] = 0;
+      }
+    ucb.insert(ucb.end(), cb.begin(), cb.end());
+    ci += n;
+  }
+  G.u_ok = u_ok && !ug.empty();
+  G.u_groups = (int32_t)ug.size();
+  G.u_sig = n_seg;
+  if (G.u_ok) {
+    uwr.assign((size_t)n_chunks * n_seg * kGridTT, -(1 << 20));  // empty TOA slots: every weight 0
+    for (int32_t s = 0; s < n_seg; ++s)
+      for (int64_t t = 0; t < N; ++t)
+        uwr[((size_t)chunk_of[t] * n_seg + s) * kGridTT + tt_of[t]] =
+            (int32_t)J[s][t] + voff[(size_t)s * n_chunks + chunk_of[t]];
+    for (int32_t s = 0; s < n_seg; ++s) {
+      G.u_w[s] = ws[s];
+      G.u_hw[s] = 0.5 * (double)ws[s];
+      G.u_beta[s] = betas[s];
+    }
+  }
   int rc;
   if ((rc = upload(c, G.chunks, chunks.data(), sizeof(int4) * chunks.size(), "grid chunks")) ||
       (rc = upload(c, G.rows, rt.data(), sizeof(int32_t) * rt.size(), "grid band rows")))
@@ -1078,6 +1153,16 @@ int grid_build(fpta_ctx* c, Layout& L) {
                    (rc = upload(c, G.urows, urows.data(), sizeof(int32_t) * urows.size(), "grid union rows")) ||
                    (rc = upload(c, G.lrows, lrt.data(), sizeof(int32_t) * lrt.size(), "grid LDS rows"))))
     return rc;
+  if (G.u_ok) {
+    if ((rc = upload(c, G.ugroups, ug.data(), sizeof(int4) * ug.size(), "union groups")) ||
+        (rc = upload(c, G.uurows, uur.data(), sizeof(int32_t) * uur.size(), "union rows")) ||
+        (rc = upload(c, G.ucbase, ucb.data(), sizeof(int32_t) * ucb.size(), "union bases")) ||
+        (rc = upload(c, G.uwrow, uwr.data(), sizeof(int32_t) * uwr.size(), "union window rows")))
+      return rc;
+    const size_t dbytes = sizeof(double) * 2 * (size_t)n_chunks * n_seg * kGridTT;
+    HIPCHK(c, G.udch.ensure(dbytes), "union weight parameters alloc");
+    HIPCHK(c, hipMemsetAsync(G.udch.p, 0, dbytes, c->stream), "union weight parameters memset");
+  }
   DevBuf d_chunk_of, d_tt_of, d_row, d_d;
   if ((rc = upload(c, d_chunk_of, chunk_of.data(), sizeof(int32_t) * N, "grid chunk_of")) ||
       (rc = upload(c, d_tt_of, tt_of.data(), sizeof(int32_t) * N, "grid tt_of")))
@@ -1143,7 +1228,8 @@ int grid_build(fpta_ctx* c, Layout& L) {
       return rc;
     HIPCHK(c,
            launch_grid_weights(c->stream, d, N, L.nu.as<double>(), d_chunk_of.as<int32_t>(), d_tt_of.as<int32_t>(),
-                               d_row.as<int32_t>(), d_d.as<double>(), ws[s], beta, vmax, G.wd.as<double>()),
+                               d_row.as<int32_t>(), d_d.as<double>(), ws[s], beta, vmax, G.wd.as<double>(),
+                               G.u_ok ? G.udch.as<double>() : nullptr, s, n_seg),
            "k_grid_weights launch");
     HIPCHK(c, hipStreamSynchronize(c->stream), "grid weights sync");  // d_row / d_d are reused
     // multiply-adds per realization: quarter range by parity on MFMA, half range on VALU
@@ -1317,7 +1403,13 @@ int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad, bool pipe = fa
   // 6.8-7.4 vs 8.4 ms/step, profiles/r04a_c4_ws2.txt)
   const bool ws2_fits = c->interp_ws == 1 && (R_pad + 255) / 256 * 256 - R_pad < (R_pad + 511) / 512 * 512 - R_pad;
   int kind;  // the interpolation kernel (fpta_batch_grid_info_n slot 15)
-  if (c->interp_ws == 4 && !c->interp_lds) {
+  if (c->interp_ws == 5 && !c->interp_lds && G.u_ok && !a.w_on) {
+    kind = 5;
+    GridUnion un{G.ugroups.as<int4>(), G.uurows.as<int32_t>(), G.ucbase.as<int32_t>(), G.udch.as<double>(),
+                 G.uwrow.as<int32_t>(), G.u_groups, G.u_sig, {G.u_w[0], G.u_w[1]}, {G.u_hw[0], G.u_hw[1]},
+                 {G.u_beta[0], G.u_beta[1]}};
+    HIPCHK(c, launch_grid_interp_u(c->stream, a, band, un, R_pad), "k_grid_interp_u launch");
+  } else if (c->interp_ws == 4 && !c->interp_lds) {
     kind = 4;
     HIPCHK(c, launch_grid_interp_st(c->stream, a, band, R_pad), "k_grid_interp_st launch");
   } else if ((c->interp_ws == 3 || ws2_fits) && !c->interp_lds && !a.w_on && !a.accumulate && !a.part) {
@@ -1742,15 +1834,12 @@ int fpta_set_option(fpta_ctx* c, int32_t key, int64_t value) {
     case FPTA_OPT_ASYNC_SUMS:
       c->async_sums = value ? 1 : 0;
       return FPTA_OK;
-    case FPTA_OPT_ECORR_INLINE:
-      c->ecorr_inline = value ? 1 : 0;
-      return FPTA_OK;
     case FPTA_OPT_GRID_COALESCE:
       c->grid_coalesce = value ? 1 : 0;
       c->batch.grid.clear();
       return FPTA_OK;
     case FPTA_OPT_INTERP_WS:
-      if (value < 0 || value > 4) return fail(c, FPTA_EINVAL, "interp_ws must be 0 .. 4");
+      if (value < 0 || value > 5) return fail(c, FPTA_EINVAL, "interp_ws must be 0 .. 5");
       c->interp_ws = (int)value;
       return FPTA_OK;
     case FPTA_OPT_SIDE_SPLIT:
@@ -1796,7 +1885,6 @@ int fpta_get_option(fpta_ctx* c, int32_t key, int64_t* value) {
     case FPTA_OPT_DFT_GEN: *value = c->dft_gen; return FPTA_OK;
     case FPTA_OPT_GEN_MIX: *value = c->gen_mix; return FPTA_OK;
     case FPTA_OPT_ASYNC_SUMS: *value = c->async_sums; return FPTA_OK;
-    case FPTA_OPT_ECORR_INLINE: *value = c->ecorr_inline; return FPTA_OK;
   }
   return fail(c, FPTA_EINVAL, "get_option: unknown key");
 }
@@ -2148,9 +2236,10 @@ static int batch_common(fpta_ctx* c, uint64_t seed, int64_t real0, int32_t n_rea
   }
   int path = 0;
   if (!L.segs.empty() && (rc = select_path(c, L, n_real, true, &path))) return rc;
-  // ECORR epoch normals of this batch as a [R][n_epochs] block, for the exact paths and the separate white pass; the
-  // gridded interpolation's fused epilogue makes them from their counters instead (FPTA_OPT_ECORR_INLINE)
-  if (do_white && c->has_blocks && !(path == 4 && c->fuse_white && c->ecorr_inline)) {
+  // ECORR epoch normals of this batch as a [R][n_epochs] block, read by every white path. (Making them from their
+  // Philox counters inside the gridded epilogue instead was measured 2x slower on C5: the epilogue is VALU-bound,
+  // profiles/round4/R4l_c5_storer_ecorr_inline_ab.txt.)
+  if (do_white && c->has_blocks) {
     HIPCHK(c, c->zb_epochs.ensure(sizeof(double) * (size_t)n_real * c->n_blocks), "zb alloc");
     wc.zb = c->zb_epochs.as<double>();
     KTimer kt(c, FPTA_K_WHITE);

@@ -34,4 +34,13 @@ __device__ __forceinline__ double chrom_factor(double freqf, double nu, double i
   return pow(x, idx);
 }
 
+// Interpolation weight of row i of a TOA's window (exponential-of-semicircle kernel, width 2 hw cells, shape beta):
+// ch phi((d - i) / hw), d the TOA's offset from the window's first row. One definition for k_grid_weights (the weight
+// tables) and k_grid_interp_u (weights made on the fly), so both give the same doubles.
+__device__ __forceinline__ double es_weight(double d, int i, double hw, double beta, double ch) {
+  const double z = (d - (double)i) / hw;
+  const double s = 1.0 - z * z;
+  return s > 0.0 ? ch * exp(beta * (sqrt(s) - 1.0)) : 0.0;
+}
+
 }  // namespace fpta

@@ -120,7 +120,8 @@ hipError_t launch_coef_merge(hipStream_t st, const CoefMerge& m, int32_t P, int3
 
 hipError_t launch_grid_weights(hipStream_t st, const SegDesc& sd, int64_t n_toa, const double* nu,
                                const int32_t* chunk_of, const int32_t* tt_of, const int32_t* row_of,
-                               const double* d_of, int32_t w, double beta, int32_t vmax, double* wd);
+                               const double* d_of, int32_t w, double beta, int32_t vmax, double* wd,
+                               double* dch = nullptr, int32_t s_idx = 0, int32_t n_sig = 1);
 hipError_t launch_grid_dft(hipStream_t st, GridSegs gsegs, int32_t P, const double* coef, int32_t K, int32_t R_pad);
 // the same two steps on v_mfma_f64_16x16x4_f64 (grid_mfma.hip)
 hipError_t launch_grid_dft_mfma(hipStream_t st, GridSegs gsegs, int32_t P, const double* coef, int32_t K,
@@ -176,6 +177,25 @@ struct GridLds {
 };
 hipError_t launch_grid_interp_lds(hipStream_t st, const SynthArgs& a, const GridBand& band, const GridLds& lds,
                                   int32_t R_pad);
+// Union-row interpolation (k_grid_interp_u): a workgroup takes a group of <= kUnionGroup consecutive chunks of one
+// pulsar for 128 realizations, stages the union of their band rows (<= kUnionRowsMax rows over all signals) in LDS
+// once, and each compute wave interpolates one chunk from it with its weights made on the fly (es_weight); layouts of
+// <= kUnionSigMax grid signals.
+constexpr int kUnionGroup = 4, kUnionRowsMax = 76, kUnionSigMax = 2, kUnionPitch = 130;
+struct GridUnion {
+  const int4* groups;    // [n_groups] {first chunk, chunks, union rows U, offset into urows}
+  const int32_t* urows;  // grid-buffer rows of each group's union (signal by signal)
+  const int32_t* cbase;  // [n_chunks][2 kUnionSigMax] per signal: first band row voff_s, union slot of band row 0 of
+                         // the signal's band minus voff_s (slot = v + base)
+  const double* dch;     // [n_chunks][n_sig][kGridTT] {d, ch} per TOA slot (double pairs)
+  const int32_t* wrow;   // [n_chunks][n_sig][kGridTT] band row of the TOA's window start (voff_s included; empty slot:
+                         // a large negative value, so every weight is 0)
+  int32_t n_groups, n_sig;
+  int32_t w[kUnionSigMax];
+  double hw[kUnionSigMax], beta[kUnionSigMax];
+};
+hipError_t launch_grid_interp_u(hipStream_t st, const SynthArgs& a, const GridBand& band, const GridUnion& un,
+                                int32_t R_pad);
 // checksums [n_real][2] from the interpolation's partials [n_chunks][R_pad][2], summed over chunks in a fixed
 // order (tmp: kPartSegs * R_pad * 2 doubles)
 constexpr int kPartSegs = 64;

@@ -33,12 +33,15 @@ typedef double dbl2 __attribute__((ext_vector_type(2)));
 // ----------------------------------------------------------------------------- k_grid_weights
 // One thread per TOA of the segment: W[chunk][row + i][tt] = ch(t) phi((d - i) / (w / 2)), i < w; row = the
 // signal's band offset in the chunk + the TOA's first row in that band (host plan), pitch vmax rows per chunk.
+// dch (optional, k_grid_interp_u's on-the-fly weights): {d, ch} of the TOA for signal s_idx of n_sig at
+// [(chunk * n_sig + s_idx) * kGridTT + tt].
 __global__ __launch_bounds__(256) void k_grid_weights(SegDesc sd, int64_t n_toa, const double* __restrict__ nu,
                                                       const int32_t* __restrict__ chunk_of,
                                                       const int32_t* __restrict__ tt_of,
                                                       const int32_t* __restrict__ row_of,
                                                       const double* __restrict__ d_of, int32_t w, double beta,
-                                                      int32_t vmax, double* __restrict__ wd) {
+                                                      int32_t vmax, double* __restrict__ wd, dbl2* __restrict__ dch,
+                                                      int32_t s_idx, int32_t n_sig) {
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (t >= n_toa) return;
   double ch = chrom_factor(sd.freqf, nu[t], sd.idx);
@@ -46,11 +49,8 @@ __global__ __launch_bounds__(256) void k_grid_weights(SegDesc sd, int64_t n_toa,
   const double d = d_of[t];
   const double hw = 0.5 * (double)w;
   double* dst = wd + ((int64_t)chunk_of[t] * vmax + row_of[t]) * kGridTT + tt_of[t];
-  for (int i = 0; i < w; ++i) {
-    const double z = (d - (double)i) / hw;
-    const double s = 1.0 - z * z;
-    dst[(int64_t)i * kGridTT] = s > 0.0 ? ch * exp(beta * (sqrt(s) - 1.0)) : 0.0;
-  }
+  for (int i = 0; i < w; ++i) dst[(int64_t)i * kGridTT] = es_weight(d, i, hw, beta, ch);
+  if (dch) dch[((int64_t)chunk_of[t] * n_sig + s_idx) * kGridTT + tt_of[t]] = dbl2{d, ch};
 }
 
 // ----------------------------------------------------------------------------- k_grid_dft
@@ -125,9 +125,10 @@ __global__ __launch_bounds__(256) void k_grid_dft(GridSegs gsegs, const double* 
 
 hipError_t launch_grid_weights(hipStream_t st, const SegDesc& sd, int64_t n_toa, const double* nu,
                                const int32_t* chunk_of, const int32_t* tt_of, const int32_t* row_of,
-                               const double* d_of, int32_t w, double beta, int32_t vmax, double* wd) {
+                               const double* d_of, int32_t w, double beta, int32_t vmax, double* wd, double* dch,
+                               int32_t s_idx, int32_t n_sig) {
   hipLaunchKernelGGL(k_grid_weights, dim3((unsigned)((n_toa + 255) / 256)), dim3(256), 0, st, sd, n_toa, nu,
-                     chunk_of, tt_of, row_of, d_of, w, beta, vmax, wd);
+                     chunk_of, tt_of, row_of, d_of, w, beta, vmax, wd, (dbl2*)dch, s_idx, n_sig);
   return hipGetLastError();
 }
 

@@ -383,9 +383,6 @@ hipError_t launch_coef_merge(hipStream_t st, const CoefMerge& m, int32_t P, int3
 __device__ __attribute__((noinline)) double white_one(uint64_t t, uint64_t g, uint32_t k0, uint32_t k1) {
   return quad_normal(t, kWhiteStream, g, k0, k1);
 }
-__device__ __attribute__((noinline)) double ecorr_one(uint64_t b, uint64_t g, uint32_t k0, uint32_t k1) {
-  return quad_normal(b, kEcorrStream, g, k0, k1);
-}
 __device__ __forceinline__ void white_quad(int64_t t, int64_t g, uint32_t k0, uint32_t k1, double (&z)[4]) {
   if (((t | g) & 1) == 0) {
     quad4((uint64_t)t, kWhiteStream, (uint64_t)g, k0, k1, z);
@@ -451,47 +448,6 @@ __device__ __forceinline__ void interp_white(const SynthArgs& a, const InterpTil
   // epoch 0 against es = 0.
   const bool ecorr = a.w_block_of != nullptr;
   const int64_t e0 = ep[0] >= 0 ? ep[0] : 0, e1 = ep[1] >= 0 ? ep[1] : 0;
-  if (ecorr && !a.w_zb) {
-    // ECORR epoch normals made here from their counters (oracle quad_normals on the ECORR stream: the words of
-    // k_epoch_normals) instead of read back from a [R][n_epochs] block: one Philox call gives epochs (2 i, 2 i + 1) x
-    // realizations (g, g + 1), so a TOA pair whose epochs share a pair takes one call per realization pair
-#pragma unroll
-    for (int m = 0; m < NP; ++m) {
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int rl = t.r0 + 32 * m + 2 * (lg + 4 * g);
-        const int64_t gg = a.real0 + rl;
-        double ze[2][2];  // [TOA parity][realization h]
-        if ((gg & 1) == 0) {
-          double z[4];
-          quad4((uint64_t)(e0 & ~(int64_t)1), kEcorrStream, (uint64_t)gg, a.k0, a.k1, z);
-          ze[0][0] = z[2 * (e0 & 1)];
-          ze[0][1] = z[2 * (e0 & 1) + 1];
-          if ((e1 >> 1) != (e0 >> 1)) quad4((uint64_t)(e1 & ~(int64_t)1), kEcorrStream, (uint64_t)gg, a.k0, a.k1, z);
-          ze[1][0] = z[2 * (e1 & 1)];
-          ze[1][1] = z[2 * (e1 & 1) + 1];
-        } else {
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-            ze[i >> 1][i & 1] = ecorr_one((uint64_t)((i >> 1) ? e1 : e0), (uint64_t)(gg + (i & 1)), a.k0, a.k1);
-        }
-        if (a.w_sigma) {
-          double z[4];
-          white_quad(tg, gg, a.k0, a.k1, z);
-#pragma unroll
-          for (int e = 0; e < 2; ++e)
-#pragma unroll
-            for (int h = 0; h < 2; ++h) acc[e][2 * m + h][g] = fma(sg[e], z[2 * e + h], acc[e][2 * m + h][g]);
-        }
-#pragma unroll
-        for (int e = 0; e < 2; ++e)
-#pragma unroll
-          for (int h = 0; h < 2; ++h) acc[e][2 * m + h][g] = fma(es[e], ze[e][h], acc[e][2 * m + h][g]);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-    return;
-  }
   auto zb_load = [&](int mg, double (&z)[2][2]) {
     const int rl = t.r0 + 32 * (mg >> 2) + 2 * (lg + 4 * (mg & 3));
 #pragma unroll
@@ -1370,6 +1326,154 @@ hipError_t launch_grid_interp_st(hipStream_t st, const SynthArgs& a, const GridB
                        : (a.part ? k_grid_interp_st<false, true> : k_grid_interp_st<false, false>);
   hipLaunchKernelGGL(kernel, dim3((unsigned)grid), dim3(512), 0, st, a, band, (int32_t)tiles, (int32_t)n_units, R_pad,
                      a.out);
+  return hipGetLastError();
+}
+
+// ----------------------------------------------------------------------------- k_grid_interp_u
+// Interpolation with union rows and weights made on the fly. Its time follows the vector-memory traffic beside the
+// residual stores (profiles/round4/R4j_c2_storer_load_volume_diag.txt: 0.32 ms without stores, 0.34 ms without operand
+// loads, 0.53 ms with both; ~0.13 ms per byte loaded per byte stored), and the per-chunk kernels load ~1.2 bytes per
+// byte stored: each chunk's band (V rows x realizations; a grid row sits in the bands of ~4.5 chunks) plus its weight
+// rows. Here a workgroup takes a group of <= kUnionGroup consecutive chunks of one pulsar (host plan, GridUnion) and
+// 128 realizations:
+//  1. the union of the group's bands (U <= kUnionRowsMax rows, all signals) is loaded once into LDS (one 1 KB
+//     direct-to-LDS load per row), ~0.42 bytes per byte stored on C2 instead of ~1.1;
+//  2. wave w interpolates chunk w of the group with the MFMA steps of k_grid_interp_mfma (even / odd TOA B-tiles,
+//     realization tile pairs), A from LDS (band row v of signal s sits at union slot v + base_s) and B = the weights
+//     es_weight(d, v - row, hw_s, beta_s, ch) of the lane's two TOAs made on the fly (the k_grid_weights expression:
+//     the same doubles as the weight tables), so it issues no global load;
+//  3. it stores the tile (and the partial checksums).
+// Two workgroups per CU (<= 79 KB of LDS each) alternate: one's MFMA steps run while the other loads its next union.
+#ifndef FPTA_U_DIAG
+#define FPTA_U_DIAG 0
+#endif
+template <bool PART>
+__global__ __launch_bounds__(256, 2) void k_grid_interp_u(SynthArgs a, GridBand band, GridUnion un, int32_t n_tiles,
+                                                          int32_t R_pad, double* __restrict__ out) {
+  constexpr int RW = 8, NP = RW / 2;
+  static_assert(kGridTT == 32 && kUnionSigMax == 2, "two 16-TOA B-tiles per chunk; two grid signals");
+  extern __shared__ __attribute__((aligned(16))) double Gs[];  // [U][kUnionPitch]
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int lr = lane & 15, lg = lane >> 4;
+  const int per = (n_tiles + 7) >> 3;
+  const int x = blockIdx.x & 7;
+  const int stride = gridDim.x >> 3;
+  const int end = min(n_tiles, (x + 1) * per);
+  const int n_rb = R_pad >> 7;
+  const int ns = un.n_sig;
+  d4 acc[2][RW];
+  auto mfma = [&](const dbl2(&av)[NP], const dbl2& bv) {
+#pragma unroll
+    for (int m = 0; m < NP; ++m) {
+      acc[0][2 * m] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m].x, bv.x, acc[0][2 * m], 0, 0, 0);
+      acc[0][2 * m + 1] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m].y, bv.x, acc[0][2 * m + 1], 0, 0, 0);
+      acc[1][2 * m] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m].x, bv.y, acc[1][2 * m], 0, 0, 0);
+      acc[1][2 * m + 1] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m].y, bv.y, acc[1][2 * m + 1], 0, 0, 0);
+    }
+  };
+  for (int tile = x * per + (int)(blockIdx.x >> 3); tile < end; tile += stride) {
+    const int g = __builtin_amdgcn_readfirstlane(tile / n_rb);
+    const int r0 = (tile - g * n_rb) * 128;
+    const int4 gi = ld_uniform4(un.groups + g);  // {first chunk, chunks, U, union row offset}
+    // 1. union rows -> LDS
+    for (int u = wave; u < gi.z; u += 4) {
+      const int row = __builtin_amdgcn_readfirstlane(ld_uniform(un.urows + gi.w + u));
+      FPTA_DCHECK(row >= 0 && row < band.grid_rows, "k_grid_interp_u grid row", row, band.grid_rows);
+      __builtin_amdgcn_global_load_lds((const void*)(band.g + (int64_t)row * R_pad + r0 + 2 * lane),
+                                       (__attribute__((address_space(3))) void*)(Gs + u * kUnionPitch), 16, 0, 0);
+    }
+    ws_wait_vm<0>();
+    ws_barrier();
+    // 2. chunk gi.x + wave
+    if (wave < gi.y) {
+      InterpTile<RW> t;
+      t.c = gi.x + wave;
+      const int4 ci = ld_uniform4(band.chunks + t.c);
+      t.p = __builtin_amdgcn_readfirstlane(ci.x);
+      t.y = __builtin_amdgcn_readfirstlane(ci.y);
+      t.cnt = __builtin_amdgcn_readfirstlane(ci.z);
+      t.nq = __builtin_amdgcn_readfirstlane(ci.w) >> 2;
+      t.r0 = r0;
+      const int4 cb = ld_uniform4(un.cbase + 4 * t.c);  // {voff_0, voff_1, base_0, base_1}
+      // the lane's TOAs 2 lr (e = 0) and 2 lr + 1 (e = 1): window start row and {d, ch} per signal
+      double dd[2][2], cc[2][2];
+      int wr[2][2];
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const int64_t k = ((int64_t)t.c * ns + min(s, ns - 1)) * kGridTT + 2 * lr + e;
+          const dbl2 v = *(const dbl2*)(un.dch + 2 * k);
+          dd[s][e] = v.x;
+          cc[s][e] = v.y;
+          wr[s][e] = s < ns ? un.wrow[k] : -(1 << 20);
+        }
+      // operands of step q: A = union slots of band rows 4 q + lg (LDS), B = this lane's two weights of that row
+      auto ops = [&](int q, dbl2(&av)[NP], dbl2& bv) {
+        const int v = 4 * q + lg;
+        const bool s1 = v >= cb.y;
+        const int slot = min(max(v + (s1 ? cb.w : cb.z), 0), gi.z - 1);  // pad rows: any valid slot (weight 0)
+        const double* __restrict__ src = Gs + slot * kUnionPitch + 2 * lr;
+#pragma unroll
+        for (int m = 0; m < NP; ++m) av[m] = *(const dbl2*)(src + 32 * m);
+        const int w = s1 ? un.w[1] : un.w[0];
+        const double hw = s1 ? un.hw[1] : un.hw[0], be = s1 ? un.beta[1] : un.beta[0];
+        const int i0 = v - (s1 ? wr[1][0] : wr[0][0]), i1 = v - (s1 ? wr[1][1] : wr[0][1]);
+        const double w0 = es_weight(s1 ? dd[1][0] : dd[0][0], i0, hw, be, s1 ? cc[1][0] : cc[0][0]);
+        const double w1 = es_weight(s1 ? dd[1][1] : dd[0][1], i1, hw, be, s1 ? cc[1][1] : cc[0][1]);
+        bv.x = (i0 >= 0 && i0 < w) ? w0 : 0.0;
+        bv.y = (i1 >= 0 && i1 < w) ? w1 : 0.0;
+#if FPTA_U_DIAG == 1  // diagnostic build only: weights from the table (global loads)
+        bv = *(const dbl2*)(band.wd + ((int64_t)t.c * band.vmax + v) * kGridTT + 2 * lr);
+#elif FPTA_U_DIAG == 2  // diagnostic build only: no weight arithmetic
+        bv = dbl2{1e-3 * i0, 1e-3 * i1};
+#endif
+      };
+#pragma unroll
+      for (int e = 0; e < 2; ++e)
+#pragma unroll
+        for (int i = 0; i < RW; ++i) acc[e][i] = d4{0.0, 0.0, 0.0, 0.0};
+      dbl2 a0[NP], a1[NP], b0, b1;
+      ops(0, a0, b0);
+      for (int q = 0; q < t.nq; q += 2) {
+        ops(min(q + 1, t.nq - 1), a1, b1);
+        mfma(a0, b0);
+        if (q + 1 < t.nq) {
+          ops(min(q + 2, t.nq - 1), a0, b0);
+          mfma(a1, b1);
+        }
+      }
+      interp_store<PART, RW>(a, out, t, acc);
+    }
+    // 3. every wave's LDS reads are done (consumed by its MFMAs): the union buffer may be refilled. A plain s_barrier:
+    // __syncthreads would also wait for this tile's stores
+    ws_barrier();
+  }
+}
+
+hipError_t launch_grid_interp_u(hipStream_t st, const SynthArgs& a, const GridBand& band, const GridUnion& un,
+                                int32_t R_pad) {
+  if (band.n_chunks <= 0 || un.n_groups <= 0 || un.n_sig < 1 || un.n_sig > kUnionSigMax || R_pad % 128 != 0 ||
+      R_pad <= 0 || a.w_on || a.accumulate)
+    return hipErrorInvalidValue;
+  const int64_t tiles = (int64_t)un.n_groups * (R_pad / 128);
+  if (tiles > 0x7FFFFFFF) return hipErrorInvalidValue;
+  static int n_cu = 0;
+  if (!n_cu) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0)
+      n_cu = 256;
+  }
+  const size_t lds = sizeof(double) * kUnionRowsMax * kUnionPitch;  // 79 KB: two workgroups per CU
+  const int64_t grid = std::min<int64_t>((tiles + 7) / 8 * 8, (2 * (int64_t)n_cu + 7) / 8 * 8);
+  if (a.part)
+    hipLaunchKernelGGL(k_grid_interp_u<true>, dim3((unsigned)grid), dim3(256), lds, st, a, band, un, (int32_t)tiles,
+                       R_pad, a.out);
+  else
+    hipLaunchKernelGGL(k_grid_interp_u<false>, dim3((unsigned)grid), dim3(256), lds, st, a, band, un, (int32_t)tiles,
+                       R_pad, a.out);
   return hipGetLastError();
 }
 

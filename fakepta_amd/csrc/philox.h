@@ -163,7 +163,10 @@ namespace fpta {
 __device__ __forceinline__ double quad_normal(uint64_t i, uint32_t stream, uint64_t g, uint32_t k0, uint32_t k1) {
   double z[4];
   normals4(philox4x32_10({(uint32_t)(i >> 1), kWhitePsrWord, stream, (uint32_t)(g >> 1)}, k0, k1), z);
-  return z[2 * (i & 1) + (g & 1)];
+  // a select, not z[k]: a lane-dependent index into a private array is a scratch (stack) object, and each inlined
+  // copy would get its own
+  const double lo = (g & 1) ? z[1] : z[0], hi = (g & 1) ? z[3] : z[2];
+  return (i & 1) ? hi : lo;
 }
 __device__ __forceinline__ void quad4(uint64_t i_even, uint32_t stream, uint64_t g_even, uint32_t k0, uint32_t k1,
                                       double (&z)[4]) {

@@ -337,10 +337,6 @@ int fpta_comm_gather(fpta_comm* comm, const double* send, int64_t count, double*
 #define FPTA_OPT_ASYNC_SUMS 19    /* streamed jobs (fpta_batch_synth_checksums, fpta_multi_synth): 1 a block's partial
                                      checksums are reduced on a stream of their own, beside the next block, into one
                                      of two partials buffers; 0 (default) on the context stream. Identical results. */
-#define FPTA_OPT_ECORR_INLINE 20  /* gridded path with fused white noise: 1 the interpolation's epilogue makes each ECORR
-                                     epoch normal from its Philox counter (the k_epoch_normals words) instead of
-                                     reading a [R][n_epochs] block written before the interpolation; 0 (default) the
-                                     block. Results are identical. */
 int fpta_set_option(fpta_ctx* ctx, int32_t key, int64_t value);
 /* Current value of option `key` (same keys as fpta_set_option). */
 int fpta_get_option(fpta_ctx* ctx, int32_t key, int64_t* value);

@@ -503,12 +503,11 @@ def test_partial_realization_blocks_write_every_sample(ctx, capi, shipped, ws, R
 @pytest.mark.parametrize("R,real0", [(128, 5), (256, 8), (333, 5), (1100, 8)])
 def test_storer_interpolation_white_ecorr_is_bitwise_identical(ctx, capi, shipped, fuse, R, real0):
     """FPTA_OPT_INTERP_WS 4 (k_grid_interp_st: compute waves hand their sums to storer waves through LDS; the storers
-    add white noise and ECORR, store, and reduce the partial checksums) and FPTA_OPT_ECORR_INLINE 1 (the epilogue
-    makes the ECORR epoch normals from their Philox counters instead of reading k_epoch_normals' block) return the
-    register kernel's block and checksums bit for bit with the white / ECORR epilogue, on a ragged layout whose
-    pulsars start at odd TOA offsets (the misaligned white-noise words), at odd and even first realizations (the
-    one-normal-per-call path), for realization counts whose last tile holds fewer than four units; and the block
-    matches the oracle (/root/reference/fakepta/fake_pta.py:201-230)."""
+    add white noise and ECORR, store, and reduce the partial checksums) returns the register kernel's block and
+    checksums bit for bit with the white / ECORR epilogue, on a ragged layout whose pulsars start at odd TOA offsets
+    (the misaligned white-noise words), at odd and even first realizations (the one-normal-per-call path), for
+    realization counts whose last tile holds fewer than four units; and the block matches the oracle
+    (/root/reference/fakepta/fake_pta.py:201-230)."""
     rng = np.random.default_rng(59)
     offs, toas, nu = random_layout(rng, 9, (31, 180))
     ctx.batch_set_toas(offs, toas, nu)
@@ -524,24 +523,65 @@ def test_storer_interpolation_white_ecorr_is_bitwise_identical(ctx, capi, shippe
         ctx.set_option(capi.OPT_SYNTH_PATH, 4)
         ctx.set_option(capi.OPT_FUSE_CHECKSUMS, fuse)
         res = {}
-        for ws, inline in ((0, 0), (4, 0), (0, 1), (4, 1)):
+        for ws in (0, 4):
             ctx.set_option(capi.OPT_INTERP_WS, ws)
-            ctx.set_option(capi.OPT_ECORR_INLINE, inline)
             ctx.batch_synth(13, 0, R, to_host=False)
             ctx.debug_fill_out(np.nan)
-            res[ws, inline] = (ctx.batch_synth(13, real0, R), ctx.batch_checksums())
-        for key in ((4, 0), (0, 1), (4, 1)):
+            res[ws] = (ctx.batch_synth(13, real0, R), ctx.batch_checksums())
+        for key in (4,):
             assert np.all(np.isfinite(res[key][0]))
-            np.testing.assert_array_equal(res[0, 0][0], res[key][0])
-            np.testing.assert_array_equal(res[0, 0][1], res[key][1])
+            np.testing.assert_array_equal(res[0][0], res[key][0])
+            np.testing.assert_array_equal(res[0][1], res[key][1])
         block_of = -np.ones(offs[-1], dtype=np.int64)
         for b, q in enumerate(blocks):
             block_of[q] = b
         segs = [O.Segment(0, 2 * np.pi * f, a, 0.0), O.Segment(0, 2 * np.pi * f2, a2, 2.0)]
         want = O.batch_synth(offs, toas, nu, segs, 13, real0, R, sigma=sigma, block_of=block_of, ecorr_sigma=es)
-        assert_parity(res[4, 1][0], want, TOL)
+        assert_parity(res[4][0], want, TOL)
     finally:
         ctx.batch_set_white()
+        ctx.set_options(shipped)
+
+
+@pytest.mark.parametrize("fuse", [0, 1])
+@pytest.mark.parametrize("layout,R", [("two", 333), ("two", 1024), ("one", 1100), ("shared", 256)])
+def test_union_interpolation_is_bitwise_identical(ctx, capi, shipped, fuse, layout, R):
+    """FPTA_OPT_INTERP_WS 5 (k_grid_interp_u: the union of 4 consecutive chunks' band rows staged once in LDS, weights
+    made on the fly by the weight tables' own expression) returns the register kernel's block and checksums bit for
+    bit: two grid signals (red noise + DM at several radio frequencies, one pulsar with unsorted TOAs), one signal
+    (a common GWB, C3-like, ragged pulsars: partial chunks and groups), and the coalesced C2-like layout; realization
+    counts off the 512 tile; every sample written (NaN-poisoned block). The kernel must be the one that ran."""
+    rng = np.random.default_rng(67)
+    if layout == "shared":
+        _shared_span_layout(ctx, rng, nu_const=False)
+    else:
+        offs, toas, nu = random_layout(rng, 11, (31, 400))
+        if layout == "two":
+            perm = rng.permutation(offs[1] - offs[0])
+            toas[offs[0]:offs[1]] = toas[offs[0]:offs[1]][perm]
+        ctx.batch_set_toas(offs, toas, nu)
+        if layout == "two":
+            for nm, idx in ((30, 0.0), (100, 2.0)):
+                f, a = per_psr_signal(rng, offs, toas, nm)
+                ctx.batch_add_signal(0, f, a, idx=idx)
+        else:
+            f, a, L, _ = common_signal(rng, offs, toas, 30)
+            ctx.batch_add_signal(1, f, a, L=L)
+    try:
+        ctx.set_option(capi.OPT_SYNTH_PATH, 4)
+        ctx.set_option(capi.OPT_FUSE_CHECKSUMS, fuse)
+        res = {}
+        for ws in (0, 5):
+            ctx.set_option(capi.OPT_INTERP_WS, ws)
+            ctx.batch_synth(7, 0, R, to_host=False)
+            ctx.debug_fill_out(np.nan)
+            res[ws] = (ctx.batch_synth(7, 64, R), ctx.batch_checksums())
+            if ws == 5:
+                assert ctx.batch_grid_info()["interp_kernel"] == f"k_grid_interp_u<{'true' if fuse else 'false'}>"
+        assert np.all(np.isfinite(res[5][0]))
+        np.testing.assert_array_equal(res[0][0], res[5][0])
+        np.testing.assert_array_equal(res[0][1], res[5][1])
+    finally:
         ctx.set_options(shipped)
 
 
