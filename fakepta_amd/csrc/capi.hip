@@ -1078,10 +1078,14 @@ int grid_build(fpta_ctx* c, Layout& L) {
   G.lds_ok = lds_ok && !groups.empty();
   G.n_groups = (int32_t)groups.size();
   G.lds_rows = umax;
-  // k_grid_interp_u plan: the same grouping under the tighter LDS budget of two workgroups per CU
+  // k_grid_interp_u plan (diagnostic builds): the same grouping under the tighter LDS budget of two workgroups per CU
   std::vector<int4> ug;
   std::vector<int32_t> uur, ucb, uwr;
+#ifdef FPTA_DIAG_KERNELS
   bool u_ok = n_seg <= kUnionSigMax;
+#else
+  bool u_ok = false;
+#endif
   for (int32_t ci = 0; ci < n_chunks && u_ok;) {
     const int32_t p = chunks[ci].x;
     auto span = [&](int32_t s, int32_t n, int64_t& lo, int64_t& end) {
@@ -1403,7 +1407,9 @@ int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad, bool pipe = fa
   // 6.8-7.4 vs 8.4 ms/step, profiles/r04a_c4_ws2.txt)
   const bool ws2_fits = c->interp_ws == 1 && (R_pad + 255) / 256 * 256 - R_pad < (R_pad + 511) / 512 * 512 - R_pad;
   int kind;  // the interpolation kernel (fpta_batch_grid_info_n slot 15)
-  if (c->interp_ws == 5 && !c->interp_lds && G.u_ok && !a.w_on) {
+  if (false) {
+#ifdef FPTA_DIAG_KERNELS
+  } else if (c->interp_ws == 5 && !c->interp_lds && G.u_ok && !a.w_on) {
     kind = 5;
     GridUnion un{G.ugroups.as<int4>(), G.uurows.as<int32_t>(), G.ucbase.as<int32_t>(), G.udch.as<double>(),
                  G.uwrow.as<int32_t>(), G.u_groups, G.u_sig, {G.u_w[0], G.u_w[1]}, {G.u_hw[0], G.u_hw[1]},
@@ -1412,6 +1418,7 @@ int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad, bool pipe = fa
   } else if (c->interp_ws == 4 && !c->interp_lds) {
     kind = 4;
     HIPCHK(c, launch_grid_interp_st(c->stream, a, band, R_pad), "k_grid_interp_st launch");
+#endif
   } else if ((c->interp_ws == 3 || ws2_fits) && !c->interp_lds && !a.w_on && !a.accumulate && !a.part) {
     kind = 2;
     HIPCHK(c, launch_grid_interp_ws(c->stream, a, band, R_pad, true), "k_grid_interp_ws2 launch");
@@ -1840,6 +1847,10 @@ int fpta_set_option(fpta_ctx* c, int32_t key, int64_t value) {
       return FPTA_OK;
     case FPTA_OPT_INTERP_WS:
       if (value < 0 || value > 5) return fail(c, FPTA_EINVAL, "interp_ws must be 0 .. 5");
+#ifndef FPTA_DIAG_KERNELS
+      if (value > 3)
+        return fail(c, FPTA_EINVAL, "interp_ws 4 / 5: k_grid_interp_st / _u are diagnostic kernels, not in this build");
+#endif
       c->interp_ws = (int)value;
       return FPTA_OK;
     case FPTA_OPT_SIDE_SPLIT:

@@ -1089,394 +1089,6 @@ __global__ __launch_bounds__(512, 2) void k_grid_interp_ws2(SynthArgs a, GridBan
   }
 }
 
-// ----------------------------------------------------------------------------- k_grid_interp_st
-// The interpolation with storer waves. In k_grid_interp_mfma / _ws the wave that runs a tile's MFMA steps also issues
-// its 32 stores (32 KB): when the write path is full a store waits at issue, and with one MFMA wave per SIMD the
-// matrix pipe idles until the queue drains, so the MFMA stream (~0.30 ms on C2) and the store stream (~0.29 ms) add
-// up instead of overlapping. Here a workgroup (one per CU) has 4 compute waves and 4 storer waves:
-//  * compute wave w runs the band steps (operands loaded kStLead steps ahead straight into VGPRs, one continuous
-//    stream across units) on its own unit = (chunk, 128 realizations), then hands the finished
-//    sums to storer w through a 32 KB LDS slot (32 ds_write_b128, the D-fragment layout as is) and starts its next unit.
-//    Its only global memory instructions are operand loads, so it never waits for a store;
-//  * storer w copies the slot into its registers, frees it, and runs the epilogue: white noise / ECORR (Philox VALU
-//    work, which now overlaps the compute wave's MFMA steps), the stores, and the partial checksums. Its stores may
-//    wait at issue as long as the memory system needs: only the storer stalls.
-// The pair synchronises through two LDS sequence counters per slot (full, empty), polled with s_sleep; no workgroup
-// barrier after the first. Units run chunk-major over 128-realization blocks (unit u: chunk u / (R_pad / 128), block
-// u % (R_pad / 128)); workgroup tile T = units 4 T .. 4 T + 3 (wave w: 4 T + w), so every R_pad that is a multiple
-// of 128 keeps all compute waves busy (C4's R = 256: two chunks per tile). A wave's valid units are a prefix of its
-// tiles (4 T + w < n_units), and the compute wave and its storer walk the same ones.
-#ifndef FPTA_ST_LEAD
-#define FPTA_ST_LEAD 3
-#endif
-#ifndef FPTA_ST_DIAG
-#define FPTA_ST_DIAG 0
-#endif
-#ifndef FPTA_ST_PACE
-#define FPTA_ST_PACE 4
-#endif
-constexpr int kStPace = FPTA_ST_PACE;  // storer: s_sleep units after each store (interp_store_rows)
-constexpr int kStLead = FPTA_ST_LEAD;  // steps a compute wave's operand loads run ahead
-constexpr int kStSets = kStLead + 1;   // operand register sets (ring)
-static_assert(kStLead >= 2 && 4 * (kStLead + 1) <= kGridMinV, "k_grid_interp_st lookahead");
-
-// sequence counters in LDS (an explicit LDS pointer: a generic one compiles to flat accesses, which count in vmcnt and
-// would make the compute wave wait for its operand loads)
-typedef volatile __attribute__((address_space(3))) int lds_int;
-__device__ __forceinline__ void st_signal(lds_int* f, int v) {
-  ws_wait_lgkm0();                   // the slot's ds_write / ds_read instructions have completed
-  asm volatile("" ::: "memory");     // and the compiler keeps them ahead of the flag
-  *f = v;
-}
-__device__ __forceinline__ void st_wait(lds_int* f, int v) {  // until *f >= v (a wave-uniform loop)
-  while (__builtin_amdgcn_readfirstlane(*f) < v) __builtin_amdgcn_s_sleep(1);
-  asm volatile("" ::: "memory");
-}
-
-template <bool WHITE, bool PART>
-__global__ __launch_bounds__(512, 1) void k_grid_interp_st(SynthArgs a, GridBand band, int32_t n_tiles,
-                                                           int32_t n_units, int32_t R_pad, double* __restrict__ out) {
-  constexpr int RW = 8, NP = RW / 2;
-  static_assert(kGridTT == 32, "two 16-TOA B-tiles per chunk");
-  __shared__ __attribute__((aligned(16))) dbl2 slots[4][4 * RW * 64];  // [wave][i * 4 + g][lane]: 4 x 32 KB
-  __shared__ int seqs[8];                                              // full[4], empty[4]
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  const int lr = lane & 15, lg = lane >> 4;
-  const int w = wave & 3;
-  const bool storer = wave >= 4;
-  if (threadIdx.x < 8) seqs[threadIdx.x] = 0;
-  __syncthreads();
-  const int per = (n_tiles + 7) >> 3;
-  const int x = blockIdx.x & 7;
-  const int stride = gridDim.x >> 3;
-  const int end = min(n_tiles, (x + 1) * per);
-  const int n_rb = R_pad >> 7;
-  lds_int* full = (lds_int*)(seqs + w);
-  lds_int* empty = (lds_int*)(seqs + 4 + w);
-  dbl2* __restrict__ slot = &slots[w][lane];
-  auto valid = [&](int tile) { return tile < end && 4 * tile + w < n_units; };
-  // unit of `tile` for this wave: chunk, realization base, chunk geometry (wave-uniform, scalar loads)
-  auto unit = [&](int tile, InterpTile<RW>& t) {
-    const int u = 4 * tile + w;
-    t.c = __builtin_amdgcn_readfirstlane(u / n_rb);
-    t.r0 = (u - t.c * n_rb) * 128;
-    const int4 ci = ld_uniform4(band.chunks + t.c);
-    t.p = __builtin_amdgcn_readfirstlane(ci.x);
-    t.y = __builtin_amdgcn_readfirstlane(ci.y);
-    t.cnt = __builtin_amdgcn_readfirstlane(ci.z);
-    t.nq = __builtin_amdgcn_readfirstlane(ci.w) >> 2;
-  };
-  int tile = x * per + (int)(blockIdx.x >> 3);
-
-  if (storer) {
-    int seq = 0;
-    for (; valid(tile); tile += stride, ++seq) {
-      InterpTile<RW> t;
-      unit(tile, t);
-      d4 acc[2][RW];
-      st_wait(full, seq + 1);
-#pragma unroll
-      for (int i = 0; i < RW; ++i)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const dbl2 v = slot[(i * 4 + g) * 64];
-          acc[0][i][g] = v.x;
-          acc[1][i][g] = v.y;
-        }
-      st_signal(empty, seq + 1);
-#if FPTA_ST_DIAG == 1  // diagnostic build only: no stores
-      continue;
-#endif
-      if constexpr (WHITE) interp_white<RW>(a, t, acc);
-      interp_store<PART, RW, kStPace>(a, out, t, acc);
-    }
-    return;
-  }
-
-  // compute wave: one continuous stream of band steps over its units. Step S's operands sit in register set S % kStSets
-  // and are loaded kStLead steps ahead, right after the first MFMAs of step S - kStLead + ... (the set of step S - 1,
-  // whose MFMAs have issued); a load past the unit's last step takes the next unit's step, so no tile boundary drains
-  // the pipeline. Every load is unconditional (clamped indices): with loads under a branch the compiler must wait
-  // for all of them (vmcnt(0)) where the stream needs only the oldest. The 4 rows of a step come from one scalar
-  // load issued a step ahead (no LDS lookup on the load's critical path). Every chunk has at least kStLead + 1 steps
-  // (grid_build pads V to 4 (kStLead + 1) rows), so a lookahead never passes the next unit.
-  struct StUnit {
-    int c, nq;
-    const int32_t* rowp;  // band.rows of the chunk
-    const double* G0;     // band.g + r0
-    const double* W0;     // band.wd of the chunk
-  };
-  auto setup = [&](int tl, StUnit& t) {
-    const int u = 4 * tl + w;
-    t.c = __builtin_amdgcn_readfirstlane(u / n_rb);
-    const int r0 = (u - t.c * n_rb) * 128;
-    t.nq = __builtin_amdgcn_readfirstlane(ld_uniform4(band.chunks + t.c).w) >> 2;
-    FPTA_DCHECK(4 * t.nq <= band.vmax && t.nq > kStLead, "k_grid_interp_st band rows", 4 * t.nq, band.vmax + 1);
-    t.rowp = band.rows + (int64_t)t.c * band.vmax;
-    t.G0 = band.g + r0;
-    t.W0 = band.wd + (int64_t)t.c * band.vmax * kGridTT;
-  };
-  // this lane's row of a step's four: a branch-free pick (a select chain on lg compiles to divergent branches)
-  const int e1 = lg == 1, e2 = lg == 2, e3 = lg == 3, e0 = lg == 0;
-  auto load = [&](const double* G0, const double* W0, int qq, int4 r4, dbl2(&av)[NP], dbl2& bv) {
-    const int row = e0 * r4.x + e1 * r4.y + e2 * r4.z + e3 * r4.w;
-    FPTA_DCHECK(row >= 0 && row < band.grid_rows, "k_grid_interp_st grid row", row, band.grid_rows);
-    const double* __restrict__ gr = G0 + (int64_t)row * R_pad + 2 * lr;
-#pragma unroll
-    for (int m = 0; m < NP; ++m) av[m] = *(const dbl2*)(gr + 32 * m);
-    bv = *(const dbl2*)(W0 + (int64_t)(4 * qq + lg) * kGridTT + 2 * lr);
-  };
-  d4 acc[2][RW];  // [TOA parity][realization tile]
-  // MFMAs of realization-tile pair m
-  auto mfma = [&](const dbl2(&av)[NP], const dbl2& bv, int m) {
-    acc[0][2 * m] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m].x, bv.x, acc[0][2 * m], 0, 0, 0);
-    acc[0][2 * m + 1] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m].y, bv.x, acc[0][2 * m + 1], 0, 0, 0);
-    acc[1][2 * m] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m].x, bv.y, acc[1][2 * m], 0, 0, 0);
-    acc[1][2 * m + 1] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m].y, bv.y, acc[1][2 * m + 1], 0, 0, 0);
-  };
-  auto zero = [&]() {
-#pragma unroll
-    for (int e = 0; e < 2; ++e)
-#pragma unroll
-      for (int i = 0; i < RW; ++i) acc[e][i] = d4{0.0, 0.0, 0.0, 0.0};
-  };
-  if (!valid(tile)) return;
-  FPTA_DCHECK(R_pad % 128 == 0, "k_grid_interp_st realization padding", R_pad % 128, 1);
-  StUnit cur, nxt;
-  setup(tile, cur);
-  int ntile = tile + stride;
-  bool more = valid(ntile);
-  if (more) setup(ntile, nxt);
-  else nxt = cur;
-  zero();
-  dbl2 av[kStSets][NP], bv[kStSets];
-#pragma unroll
-  for (int k = 0; k < kStLead; ++k) load(cur.G0, cur.W0, k, ld_uniform4(cur.rowp + 4 * k), av[k], bv[k]);
-  int4 rn = ld_uniform4(cur.rowp + 4 * kStLead);  // rows of the next step to load
-  int q = 0, seq = 0;
-  bool done = false;
-  // the loop exits only at its latch (an exit inside the unrolled body makes the compiler's structurised CFG merge an
-  // exit path into the loop header, and its conservative vmcnt(0) there drains the operand stream every 4 steps);
-  // after the last unit the remaining steps of the body run on a unit that never completes, their results unused
-  while (!done) {
-#pragma unroll
-    for (int k = 0; k < kStSets; ++k) {
-      // step q of cur in set k; its loads for step q + kStLead go to set (k + kStLead) % kStSets (step q - 1's)
-      __builtin_amdgcn_sched_barrier(0);
-      mfma(av[k], bv[k], 0);
-      __builtin_amdgcn_sched_barrier(0);
-      {
-        const int s = q + kStLead, s1 = s + 1;
-        const bool in = s < cur.nq, in1 = s1 < cur.nq;
-        const int kn = (k + kStLead) % kStSets;
-#if FPTA_ST_DIAG == 3  // diagnostic build only: operands loaded for every other step (half the load instructions)
-        if ((k & 1) == 0)
-#elif FPTA_ST_DIAG == 4  // diagnostic build only: no operand loads after the prefetch (stale operands)
-        if (false)
-#endif
-        load(in ? cur.G0 : nxt.G0, in ? cur.W0 : nxt.W0, in ? s : s - cur.nq, rn, av[kn], bv[kn]);
-        rn = ld_uniform4((in1 ? cur.rowp : nxt.rowp) + 4 * (in1 ? s1 : min(s1 - cur.nq, nxt.nq - 1)));
-      }
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int m = 1; m < NP; ++m) mfma(av[k], bv[k], m);
-      __builtin_amdgcn_sched_barrier(0);
-      if (++q == cur.nq) {  // unit done: hand its sums to the storer (LDS only: no memory-counter traffic here)
-        st_wait(empty, seq);  // the storer has copied out the previous unit
-#pragma unroll
-        for (int i = 0; i < RW; ++i)
-#pragma unroll
-          for (int g = 0; g < 4; ++g) slot[(i * 4 + g) * 64] = dbl2{acc[0][i][g], acc[1][i][g]};
-        st_signal(full, ++seq);
-        if (!more) {
-          done = true;
-          cur.nq = 0x40000000;
-          continue;
-        }
-        zero();
-        cur = nxt;
-        q = 0;
-        ntile += stride;
-        more = valid(ntile);
-        if (more) setup(ntile, nxt);
-        else nxt = cur;
-      }
-    }
-  }
-}
-
-hipError_t launch_grid_interp_st(hipStream_t st, const SynthArgs& a, const GridBand& band, int32_t R_pad) {
-  if (band.n_chunks <= 0 || band.vmax < 4 || band.vmax % 4 != 0 || band.vmax > kGridVMax || R_pad % 128 != 0 ||
-      R_pad <= 0)
-    return hipErrorInvalidValue;
-  const int64_t n_units = (int64_t)band.n_chunks * (R_pad / 128);
-  const int64_t tiles = (n_units + 3) / 4;
-  if (n_units > 0x7FFFFFFF) return hipErrorInvalidValue;
-  static int n_cu = 0;
-  if (!n_cu) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0)
-      n_cu = 256;
-  }
-  // persistent: one workgroup per CU (128 KB of LDS slots)
-  const int64_t grid = std::min<int64_t>((tiles + 7) / 8 * 8, ((int64_t)n_cu + 7) / 8 * 8);
-  auto kernel = a.w_on ? (a.part ? k_grid_interp_st<true, true> : k_grid_interp_st<true, false>)
-                       : (a.part ? k_grid_interp_st<false, true> : k_grid_interp_st<false, false>);
-  hipLaunchKernelGGL(kernel, dim3((unsigned)grid), dim3(512), 0, st, a, band, (int32_t)tiles, (int32_t)n_units, R_pad,
-                     a.out);
-  return hipGetLastError();
-}
-
-// ----------------------------------------------------------------------------- k_grid_interp_u
-// Interpolation with union rows and weights made on the fly. Its time follows the vector-memory traffic beside the
-// residual stores (profiles/round4/R4j_c2_storer_load_volume_diag.txt: 0.32 ms without stores, 0.34 ms without operand
-// loads, 0.53 ms with both; ~0.13 ms per byte loaded per byte stored), and the per-chunk kernels load ~1.2 bytes per
-// byte stored: each chunk's band (V rows x realizations; a grid row sits in the bands of ~4.5 chunks) plus its weight
-// rows. Here a workgroup takes a group of <= kUnionGroup consecutive chunks of one pulsar (host plan, GridUnion) and
-// 128 realizations:
-//  1. the union of the group's bands (U <= kUnionRowsMax rows, all signals) is loaded once into LDS (one 1 KB
-//     direct-to-LDS load per row), ~0.42 bytes per byte stored on C2 instead of ~1.1;
-//  2. wave w interpolates chunk w of the group with the MFMA steps of k_grid_interp_mfma (even / odd TOA B-tiles,
-//     realization tile pairs), A from LDS (band row v of signal s sits at union slot v + base_s) and B = the weights
-//     es_weight(d, v - row, hw_s, beta_s, ch) of the lane's two TOAs made on the fly (the k_grid_weights expression:
-//     the same doubles as the weight tables), so it issues no global load;
-//  3. it stores the tile (and the partial checksums).
-// Two workgroups per CU (<= 79 KB of LDS each) alternate: one's MFMA steps run while the other loads its next union.
-#ifndef FPTA_U_DIAG
-#define FPTA_U_DIAG 0
-#endif
-template <bool PART>
-__global__ __launch_bounds__(256, 2) void k_grid_interp_u(SynthArgs a, GridBand band, GridUnion un, int32_t n_tiles,
-                                                          int32_t R_pad, double* __restrict__ out) {
-  constexpr int RW = 8, NP = RW / 2;
-  static_assert(kGridTT == 32 && kUnionSigMax == 2, "two 16-TOA B-tiles per chunk; two grid signals");
-  extern __shared__ __attribute__((aligned(16))) double Gs[];  // [U][kUnionPitch]
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  const int lr = lane & 15, lg = lane >> 4;
-  const int per = (n_tiles + 7) >> 3;
-  const int x = blockIdx.x & 7;
-  const int stride = gridDim.x >> 3;
-  const int end = min(n_tiles, (x + 1) * per);
-  const int n_rb = R_pad >> 7;
-  const int ns = un.n_sig;
-  d4 acc[2][RW];
-  auto mfma = [&](const dbl2(&av)[NP], const dbl2& bv) {
-#pragma unroll
-    for (int m = 0; m < NP; ++m) {
-      acc[0][2 * m] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m].x, bv.x, acc[0][2 * m], 0, 0, 0);
-      acc[0][2 * m + 1] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m].y, bv.x, acc[0][2 * m + 1], 0, 0, 0);
-      acc[1][2 * m] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m].x, bv.y, acc[1][2 * m], 0, 0, 0);
-      acc[1][2 * m + 1] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m].y, bv.y, acc[1][2 * m + 1], 0, 0, 0);
-    }
-  };
-  for (int tile = x * per + (int)(blockIdx.x >> 3); tile < end; tile += stride) {
-    const int g = __builtin_amdgcn_readfirstlane(tile / n_rb);
-    const int r0 = (tile - g * n_rb) * 128;
-    const int4 gi = ld_uniform4(un.groups + g);  // {first chunk, chunks, U, union row offset}
-    // 1. union rows -> LDS
-    for (int u = wave; u < gi.z; u += 4) {
-      const int row = __builtin_amdgcn_readfirstlane(ld_uniform(un.urows + gi.w + u));
-      FPTA_DCHECK(row >= 0 && row < band.grid_rows, "k_grid_interp_u grid row", row, band.grid_rows);
-      __builtin_amdgcn_global_load_lds((const void*)(band.g + (int64_t)row * R_pad + r0 + 2 * lane),
-                                       (__attribute__((address_space(3))) void*)(Gs + u * kUnionPitch), 16, 0, 0);
-    }
-    ws_wait_vm<0>();
-    ws_barrier();
-    // 2. chunk gi.x + wave
-    if (wave < gi.y) {
-      InterpTile<RW> t;
-      t.c = gi.x + wave;
-      const int4 ci = ld_uniform4(band.chunks + t.c);
-      t.p = __builtin_amdgcn_readfirstlane(ci.x);
-      t.y = __builtin_amdgcn_readfirstlane(ci.y);
-      t.cnt = __builtin_amdgcn_readfirstlane(ci.z);
-      t.nq = __builtin_amdgcn_readfirstlane(ci.w) >> 2;
-      t.r0 = r0;
-      const int4 cb = ld_uniform4(un.cbase + 4 * t.c);  // {voff_0, voff_1, base_0, base_1}
-      // the lane's TOAs 2 lr (e = 0) and 2 lr + 1 (e = 1): window start row and {d, ch} per signal
-      double dd[2][2], cc[2][2];
-      int wr[2][2];
-#pragma unroll
-      for (int s = 0; s < 2; ++s)
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-          const int64_t k = ((int64_t)t.c * ns + min(s, ns - 1)) * kGridTT + 2 * lr + e;
-          const dbl2 v = *(const dbl2*)(un.dch + 2 * k);
-          dd[s][e] = v.x;
-          cc[s][e] = v.y;
-          wr[s][e] = s < ns ? un.wrow[k] : -(1 << 20);
-        }
-      // operands of step q: A = union slots of band rows 4 q + lg (LDS), B = this lane's two weights of that row
-      auto ops = [&](int q, dbl2(&av)[NP], dbl2& bv) {
-        const int v = 4 * q + lg;
-        const bool s1 = v >= cb.y;
-        const int slot = min(max(v + (s1 ? cb.w : cb.z), 0), gi.z - 1);  // pad rows: any valid slot (weight 0)
-        const double* __restrict__ src = Gs + slot * kUnionPitch + 2 * lr;
-#pragma unroll
-        for (int m = 0; m < NP; ++m) av[m] = *(const dbl2*)(src + 32 * m);
-        const int w = s1 ? un.w[1] : un.w[0];
-        const double hw = s1 ? un.hw[1] : un.hw[0], be = s1 ? un.beta[1] : un.beta[0];
-        const int i0 = v - (s1 ? wr[1][0] : wr[0][0]), i1 = v - (s1 ? wr[1][1] : wr[0][1]);
-        const double w0 = es_weight(s1 ? dd[1][0] : dd[0][0], i0, hw, be, s1 ? cc[1][0] : cc[0][0]);
-        const double w1 = es_weight(s1 ? dd[1][1] : dd[0][1], i1, hw, be, s1 ? cc[1][1] : cc[0][1]);
-        bv.x = (i0 >= 0 && i0 < w) ? w0 : 0.0;
-        bv.y = (i1 >= 0 && i1 < w) ? w1 : 0.0;
-#if FPTA_U_DIAG == 1  // diagnostic build only: weights from the table (global loads)
-        bv = *(const dbl2*)(band.wd + ((int64_t)t.c * band.vmax + v) * kGridTT + 2 * lr);
-#elif FPTA_U_DIAG == 2  // diagnostic build only: no weight arithmetic
-        bv = dbl2{1e-3 * i0, 1e-3 * i1};
-#endif
-      };
-#pragma unroll
-      for (int e = 0; e < 2; ++e)
-#pragma unroll
-        for (int i = 0; i < RW; ++i) acc[e][i] = d4{0.0, 0.0, 0.0, 0.0};
-      dbl2 a0[NP], a1[NP], b0, b1;
-      ops(0, a0, b0);
-      for (int q = 0; q < t.nq; q += 2) {
-        ops(min(q + 1, t.nq - 1), a1, b1);
-        mfma(a0, b0);
-        if (q + 1 < t.nq) {
-          ops(min(q + 2, t.nq - 1), a0, b0);
-          mfma(a1, b1);
-        }
-      }
-      interp_store<PART, RW>(a, out, t, acc);
-    }
-    // 3. every wave's LDS reads are done (consumed by its MFMAs): the union buffer may be refilled. A plain s_barrier:
-    // __syncthreads would also wait for this tile's stores
-    ws_barrier();
-  }
-}
-
-hipError_t launch_grid_interp_u(hipStream_t st, const SynthArgs& a, const GridBand& band, const GridUnion& un,
-                                int32_t R_pad) {
-  if (band.n_chunks <= 0 || un.n_groups <= 0 || un.n_sig < 1 || un.n_sig > kUnionSigMax || R_pad % 128 != 0 ||
-      R_pad <= 0 || a.w_on || a.accumulate)
-    return hipErrorInvalidValue;
-  const int64_t tiles = (int64_t)un.n_groups * (R_pad / 128);
-  if (tiles > 0x7FFFFFFF) return hipErrorInvalidValue;
-  static int n_cu = 0;
-  if (!n_cu) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0)
-      n_cu = 256;
-  }
-  const size_t lds = sizeof(double) * kUnionRowsMax * kUnionPitch;  // 79 KB: two workgroups per CU
-  const int64_t grid = std::min<int64_t>((tiles + 7) / 8 * 8, (2 * (int64_t)n_cu + 7) / 8 * 8);
-  if (a.part)
-    hipLaunchKernelGGL(k_grid_interp_u<true>, dim3((unsigned)grid), dim3(256), lds, st, a, band, un, (int32_t)tiles,
-                       R_pad, a.out);
-  else
-    hipLaunchKernelGGL(k_grid_interp_u<false>, dim3((unsigned)grid), dim3(256), lds, st, a, band, un, (int32_t)tiles,
-                       R_pad, a.out);
-  return hipGetLastError();
-}
-
 hipError_t launch_grid_interp_ws(hipStream_t st, const SynthArgs& a, const GridBand& band, int32_t R_pad, bool ws2) {
   if (band.n_chunks <= 0 || band.vmax < 4 || band.vmax % 4 != 0 || band.vmax > kGridVMax || R_pad % 128 != 0 ||
       a.w_on || a.accumulate)
@@ -1850,6 +1462,8 @@ hipError_t launch_part_checksums(hipStream_t st, const double* part, int32_t n_c
 
 #ifdef FPTA_DIAG_KERNELS
 #include "diag/interp_lds.inc"
+#include "diag/interp_st.inc"
+#include "diag/interp_u.inc"
 #endif
 
 }  // namespace fpta
