@@ -249,8 +249,11 @@ def cpu_baseline(sim, psrs, n_sample, seed):
 def pmc_traffic(kernel, info, R, path_arg, layout=None):
     """HBM bytes per launch from the matching profiles/*traffic.json PMC record (same kernel, shape and, for the
     gridded path, plan layout)."""
-    # newest round first (profiles/rNN<letter>_*: a later tag sorts after an earlier one)
-    candidates = ([path_arg] if path_arg else sorted(glob.glob(os.path.join(ROOT, "profiles", "*traffic.json")), reverse=True))
+    # newest round first: profiles/roundN/ (N descending), then the earlier rounds' profiles/rNN<letter>_* (a later tag
+    # sorts after an earlier one)
+    rounds = sorted(glob.glob(os.path.join(ROOT, "profiles", "round*", "*traffic.json")), reverse=True)
+    candidates = ([path_arg] if path_arg else
+                  rounds + sorted(glob.glob(os.path.join(ROOT, "profiles", "*traffic.json")), reverse=True))
     for cand in candidates:
         try:
             with open(cand) as fh:

@@ -61,6 +61,7 @@ _SIGS = [
     ("fpta_reset_stats", _c_int, [_ctx_p]),
     ("fpta_synchronize", _c_int, [_ctx_p]),
     ("fpta_debug_philox", _c_int, [_ctx_p, _i64, _vp, _vp, _vp]),
+    ("fpta_debug_normals", _c_int, [_ctx_p, _i64, _vp, _vp]),
     ("fpta_debug_fill_out", _c_int, [_ctx_p, _dbl]),
     ("fpta_get_option", _c_int, [_ctx_p, _i32, ctypes.POINTER(_i64)]),
     ("fpta_build_flags", _c_int, []),
@@ -429,6 +430,13 @@ class Context:
         key = np.ascontiguousarray(key, dtype=np.uint32)
         out = np.empty_like(ctr)
         self._check(_lib.fpta_debug_philox(self._h, len(ctr), _ptr(ctr), _ptr(key), _ptr(out)), "fpta_debug_philox")
+        return out
+
+    def debug_normals(self, words):
+        """philox.h normals4 on the device for uint32 words [n, 4] -> float64 [n, 4] (oracle normals4)."""
+        words = np.ascontiguousarray(words, dtype=np.uint32).reshape(-1, 4)
+        out = np.empty(words.shape, dtype=np.float64)
+        self._check(_lib.fpta_debug_normals(self._h, len(words), _ptr(words), _ptr(out)), "fpta_debug_normals")
         return out
 
 

@@ -2496,6 +2496,19 @@ int fpta_debug_philox(fpta_ctx* c, int64_t n, const uint32_t* ctr, const uint32_
   return FPTA_OK;
 }
 
+int fpta_debug_normals(fpta_ctx* c, int64_t n, const uint32_t* words, double* out) {
+  if (!c || n <= 0 || !words || !out) return fail(c, FPTA_EINVAL, "debug_normals: bad arguments");
+  HIPCHK(c, hipSetDevice(c->device), "hipSetDevice");
+  int rc = upload(c, c->dbg_a, words, sizeof(uint32_t) * 4 * n, "normals words");
+  if (rc) return rc;
+  HIPCHK(c, c->dbg_b.ensure(sizeof(double) * 4 * n), "normals out");
+  HIPCHK(c, launch_normals4(c->stream, n, c->dbg_a.as<uint32_t>(), c->dbg_b.as<double>()), "k_normals4 launch");
+  HIPCHK(c, hipMemcpyAsync(out, c->dbg_b.p, sizeof(double) * 4 * n, hipMemcpyDeviceToHost, c->stream),
+         "normals download");
+  HIPCHK(c, hipStreamSynchronize(c->stream), "normals sync");
+  return FPTA_OK;
+}
+
 
 // ------------------------------------------------------------------------------------ multi-device
 // One process driving several devices (SURVEY.md §8(b) fpta_multi_*, §8(e)): one context per listed

@@ -239,6 +239,7 @@ hipError_t launch_correlations(hipStream_t st, const double* out, int64_t ldo, i
                                int32_t mode, double* autos, double* parts, int32_t nparts, double* dst);
 hipError_t launch_philox(hipStream_t st, int64_t n, const uint32_t* ctr, uint32_t k0, uint32_t k1,
                          uint32_t* out);
+hipError_t launch_normals4(hipStream_t st, int64_t n, const uint32_t* words, double* out);
 
 // dense-covariance path (dense.hip)
 hipError_t launch_cov_basis(hipStream_t st, const double* toas, const double* nu, int64_t n, const double* f,

@@ -854,6 +854,18 @@ __global__ void k_philox(int64_t n, const uint32_t* __restrict__ ctr, uint32_t k
   out[4 * i + 3] = v.w;
 }
 
+// k_normals4: the build's uniform -> normal map on given Philox words (fpta_debug_normals): out[4 i .. 4 i + 3] =
+// normals4(words[4 i .. 4 i + 3]), the map every device draw uses
+__global__ void k_normals4(int64_t n, const uint32_t* __restrict__ words, double* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const u32x4 v = {words[4 * i], words[4 * i + 1], words[4 * i + 2], words[4 * i + 3]};
+  double z[4];
+  normals4(v, z);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) out[4 * i + k] = z[k];
+}
+
 // ----------------------------------------------------------------------------- launchers
 
 hipError_t launch_gen(hipStream_t st, const SegDesc& sd, int32_t seg_id, int32_t P, int32_t n_real,
@@ -1003,6 +1015,12 @@ hipError_t launch_checksums(hipStream_t st, const double* out, int64_t ldo, int6
 hipError_t launch_philox(hipStream_t st, int64_t n, const uint32_t* ctr, uint32_t k0, uint32_t k1,
                          uint32_t* out) {
   hipLaunchKernelGGL(k_philox, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, n, ctr, k0, k1, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_normals4(hipStream_t st, int64_t n, const uint32_t* words, double* out) {
+  if (n <= 0 || (n + 255) / 256 > 0x7FFFFFFF) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_normals4, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, n, words, out);
   return hipGetLastError();
 }
 

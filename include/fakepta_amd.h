@@ -363,6 +363,9 @@ int fpta_synchronize(fpta_ctx* ctx);
 /* Philox4x32-10 on device: ctr [n][4], key [2] -> out [n][4]. */
 int fpta_debug_philox(fpta_ctx* ctx, int64_t n, const uint32_t* ctr, const uint32_t* key,
                       uint32_t* out);
+/* The uniform -> normal map of every device draw (philox.h normals4) on n given Philox outputs: out[4 i + k] for the
+ * words words[4 i .. 4 i + 3] (validation of the map on chosen words, e.g. its end points; oracle normals4). */
+int fpta_debug_normals(fpta_ctx* ctx, int64_t n, const uint32_t* words, double* out);
 /* Fill the last synthesized device block with `value` (tests: a later batch must overwrite every sample). */
 int fpta_debug_fill_out(fpta_ctx* ctx, double value);
 

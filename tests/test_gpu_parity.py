@@ -62,6 +62,31 @@ def test_device_normals_match_oracle(ctx):
             np.testing.assert_allclose(co[p], want, rtol=1e-13, atol=1e-13 * np.abs(want).max())
 
 
+def test_device_normals4_edge_words(ctx):
+    """The device normal map on chosen words (fpta_debug_normals), not only on Philox outputs: the logarithm word at
+    its ends (0: the largest radius; 0xFFFFFFFF: u1 = 1, radius exactly 0 through bm_sqrt's x > 0 select) and around
+    2^31; the angle word at every quarter turn (q = 4 wraps to quadrant 0), one below and above, and the rint ties
+    between quarter turns; plus 200k random words. Within a few ulp of the oracle's IEEE division / square root (the
+    device uses v_rcp_f64 / v_rsq_f64 refinements)."""
+    edge_a = np.array([0, 1, 2, 0x7FFFFFFE, 0x7FFFFFFF, 0x80000000, 0x80000001, 0xFFFFFFFD, 0xFFFFFFFE, 0xFFFFFFFF],
+                      dtype=np.uint64)
+    qb = [k << 30 for k in range(4)] + [(2 * k + 1) << 29 for k in range(4)]
+    edge_b = np.unique(np.clip(np.array([b + d for b in qb for d in (-2, -1, 0, 1, 2)] + [0xFFFFFFFF],
+                                        dtype=np.int64), 0, 0xFFFFFFFF)).astype(np.uint64)
+    a, b = np.meshgrid(edge_a, edge_b, indexing="ij")
+    a, b = a.ravel(), b.ravel()
+    edges = np.stack([a, b, b[::-1], a[::-1]], 1).astype(np.uint32)
+    rng = np.random.default_rng(11)
+    words = np.concatenate([edges, rng.integers(0, 2 ** 32, size=(200000, 4), dtype=np.uint64).astype(np.uint32)])
+    got = ctx.debug_normals(words)
+    want = O.normals4(words)
+    assert np.all(np.isfinite(got))
+    radius = np.repeat(np.hypot(want[:, 0::2], want[:, 1::2]), 2, axis=1)
+    np.testing.assert_allclose(got, want, rtol=4e-15, atol=4e-15 * np.maximum(radius, 1e-300))
+    zero_r = words[:, 0] == 0xFFFFFFFF
+    assert np.all(got[zero_r, :2] == 0.0)
+
+
 # ----------------------------------------------------------------------------- drop-in kernels vs fixtures
 @pytest.mark.parametrize("lab", ["rn", "dm", "sv"])
 def test_gp_accumulate_vs_reference(ctx, golden, lab):

@@ -214,7 +214,7 @@ def c4(steps=5):
     return dict(config="c4", K=2 * N, n_toa=P * n_p, realizations=R, ms_per_step=dt / steps * 1e3,
                 samples_per_s=P * n_p * R * steps / dt, isolated_kernels_ms_per_step=kt1,
                 interp=_interp_entry(gi, P * n_p, R, kt1["synth"]),
-                path=ctx.batch_grid_info()["last_path"],
+                path=gi["last_path"],
                 synth_direct_equiv_tflops=flops / ((kt1["synth"] + kt1["grid"]) / 1e3) / 1e12,
                 mix_factor="cholesky" if np.all(np.triu(L, 1) == 0) else "svd",
                 mix_ms_isolated=kt1["mix"],
