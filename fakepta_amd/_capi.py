@@ -10,7 +10,8 @@ import threading
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("FAKEPTA_AMD_LIB", os.path.join(_HERE, "lib", "libfakepta_amd.so"))
+_DEFAULT_LIB = os.path.join(_HERE, "lib", "libfakepta_amd.so")
+LIB_PATH = os.environ.get("FAKEPTA_AMD_LIB", _DEFAULT_LIB)
 
 if not os.path.exists(LIB_PATH):
     raise ImportError(
@@ -86,8 +87,16 @@ _SIGS = [
     ("fpta_comm_max", _c_int, [_vp, ctypes.POINTER(_dbl)]),
     ("fpta_comm_gather", _c_int, [_vp, _vp, _i64, _vp]),
 ]
+# entry points newer than an older library a same-box A/B may load through FAKEPTA_AMD_LIB (tools/gpu_ab_cfg.sh LIB=):
+# bound when present (the product library exports every one: tests/test_capi_symbols.py)
+_OPTIONAL = {"fpta_debug_normals"}
 for _name, _res, _args in _SIGS:
-    _fn = getattr(_lib, _name)
+    try:
+        _fn = getattr(_lib, _name)
+    except AttributeError:
+        if _name in _OPTIONAL and LIB_PATH != _DEFAULT_LIB:
+            continue
+        raise
     _fn.restype = _res
     _fn.argtypes = _args
 
