@@ -210,9 +210,6 @@ __device__ __forceinline__ double opaque(double x) {
   return x;
 }
 
-#ifndef FPTA_DFT_DIAG
-#define FPTA_DFT_DIAG 0
-#endif
 constexpr int kDftGenMaxModes = 512;  // LDS: [modes][16 realizations][cos, sin] = 256 B per mode (128 KB at most)
 
 __global__ __launch_bounds__(256, 2) void k_grid_dft_gen(DftGenArgs d) {
@@ -295,13 +292,8 @@ __global__ __launch_bounds__(256, 2) void k_grid_dft_gen(DftGenArgs d) {
       dbl2 ac[3], as[3], bb[3];
       auto fetch = [&](int q, int k) {
         const int qq = min(q, nq - 1);
-#if FPTA_DFT_DIAG == 1  // diagnostic build only: no table loads (wrong values; the table traffic's share of the time)
-        ac[k] = dbl2{1e-3 * qq + lr, 2e-3 * qq + lg};
-        as[k] = dbl2{3e-3 * qq + lr, 4e-3 * qq + lg};
-#else
         ac[k] = *(const dbl2*)(tc + (int64_t)(4 * qq) * gs.ldq);
         as[k] = *(const dbl2*)(ts + (int64_t)(4 * qq) * gs.ldq);
-#endif
         bb[k] = *(const dbl2*)(Bs + 2 * ((2 * (4 * qq + lg) + par) * 16 + lr));
       };
       if (nq > 0) {
