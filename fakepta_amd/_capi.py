@@ -105,11 +105,11 @@ EXPORTED = [s[0] for s in _SIGS]
 OPT_SYNTH_PATH, OPT_MFMA_MIN_REAL, OPT_PROFILE, OPT_ANCHOR, OPT_VALU_VARIANT, OPT_FUSE_WHITE = 1, 2, 3, 4, 5, 6
 OPT_GRID_WIDTH, OPT_GRID_SIGMA, OPT_GRID_MFMA, OPT_FUSE_CHECKSUMS = 7, 8, 9, 10
 OPT_MIX_MFMA, OPT_OVERLAP, OPT_INTERP_LDS, OPT_GRID_COALESCE, OPT_INTERP_WS, OPT_SIDE_SPLIT = 11, 12, 13, 14, 15, 16
-OPT_DFT_GEN, OPT_GEN_MIX, OPT_ASYNC_SUMS = 17, 18, 19
+OPT_DFT_GEN, OPT_GEN_MIX, OPT_ASYNC_SUMS, OPT_PART_GROUP = 17, 18, 19, 20
 OPTIONS = (OPT_SYNTH_PATH, OPT_MFMA_MIN_REAL, OPT_PROFILE, OPT_ANCHOR, OPT_VALU_VARIANT, OPT_FUSE_WHITE,
            OPT_GRID_WIDTH, OPT_GRID_SIGMA, OPT_GRID_MFMA, OPT_FUSE_CHECKSUMS, OPT_MIX_MFMA, OPT_OVERLAP,
            OPT_INTERP_LDS, OPT_GRID_COALESCE, OPT_INTERP_WS, OPT_SIDE_SPLIT, OPT_DFT_GEN, OPT_GEN_MIX,
-           OPT_ASYNC_SUMS)
+           OPT_ASYNC_SUMS, OPT_PART_GROUP)
 K_GEN, K_MIX, K_SYNTH, K_WHITE, K_DENSE, K_GRID = 0, 1, 2, 3, 4, 5
 
 

@@ -201,6 +201,7 @@ struct fpta_ctx {
   int interp_ws = 1;      // gridded interpolation on the warp-specialised kernel (FPTA_OPT_INTERP_WS)
   int last_interp = 0;    // interpolation kernel of the last gridded block: 1 + 4 kind + 2 white + part (0: none)
   int grid_coalesce = 1;  // gridded path: signals sharing w0 and the chromatic weight share one grid (FPTA_OPT_GRID_COALESCE)
+  int part_group = kPartGroup;  // fused partial checksums: consecutive chunks per partial row (FPTA_OPT_PART_GROUP)
   int async_sums = 0;    // streamed jobs: partial-checksum reductions on their own stream (FPTA_OPT_ASYNC_SUMS; measured
                          // no faster on C3, profiles/r03h_ab_c3_async_sums.txt: the reductions then compete with the interpolation)
   int gen_mix = 2;       // common signals of 64..256 pulsars: draws and ORF mixing in one kernel (k_gen_mix,
@@ -1392,6 +1393,7 @@ int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad, bool pipe = fa
     // the reduction of the block that last wrote this buffer (on the red stream) must have read it
     if (c->pfree_set[pi]) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_pfree[pi], 0), "partials buffer wait");
     a.part = pb.as<double>();
+    a.part_group = c->part_group;  // the diagnostic kernels below write one row per chunk
     c->part_cur = pi;
     c->part_next = pi ^ 1;
   }
@@ -1411,12 +1413,14 @@ int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad, bool pipe = fa
 #ifdef FPTA_DIAG_KERNELS
   } else if (c->interp_ws == 5 && !c->interp_lds && G.u_ok && !a.w_on) {
     kind = 5;
+    a.part_group = 1;
     GridUnion un{G.ugroups.as<int4>(), G.uurows.as<int32_t>(), G.ucbase.as<int32_t>(), G.udch.as<double>(),
                  G.uwrow.as<int32_t>(), G.u_groups, G.u_sig, {G.u_w[0], G.u_w[1]}, {G.u_hw[0], G.u_hw[1]},
                  {G.u_beta[0], G.u_beta[1]}};
     HIPCHK(c, launch_grid_interp_u(c->stream, a, band, un, R_pad), "k_grid_interp_u launch");
   } else if (c->interp_ws == 4 && !c->interp_lds) {
     kind = 4;
+    a.part_group = 1;
     HIPCHK(c, launch_grid_interp_st(c->stream, a, band, R_pad), "k_grid_interp_st launch");
 #endif
   } else if ((c->interp_ws == 3 || ws2_fits) && !c->interp_lds && !a.w_on && !a.accumulate && !a.part) {
@@ -1428,6 +1432,7 @@ int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad, bool pipe = fa
 #ifdef FPTA_DIAG_KERNELS
   } else if (c->interp_lds && G.lds_ok && !a.w_on) {
     kind = 3;
+    a.part_group = 1;
     GridLds lds{G.groups.as<int4>(), G.urows.as<int32_t>(), G.lrows.as<int32_t>(), G.n_groups, G.lds_rows};
     HIPCHK(c, launch_grid_interp_lds(c->stream, a, band, lds, R_pad), "k_grid_interp_lds launch");
 #endif
@@ -1443,7 +1448,7 @@ int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad, bool pipe = fa
   }
   if (a.part) {
     c->part_ready = true;
-    c->part_chunks = G.n_chunks;
+    c->part_chunks = (G.n_chunks + a.part_group - 1) / a.part_group;  // partial rows
     c->part_rpad = R_pad;
   }
   return FPTA_OK;
@@ -1841,6 +1846,10 @@ int fpta_set_option(fpta_ctx* c, int32_t key, int64_t value) {
     case FPTA_OPT_ASYNC_SUMS:
       c->async_sums = value ? 1 : 0;
       return FPTA_OK;
+    case FPTA_OPT_PART_GROUP:
+      if (value < 1 || value > kPartGroupMax) return fail(c, FPTA_EINVAL, "part_group must be 1 .. 16");
+      c->part_group = (int)value;
+      return FPTA_OK;
     case FPTA_OPT_GRID_COALESCE:
       c->grid_coalesce = value ? 1 : 0;
       c->batch.grid.clear();
@@ -1896,6 +1905,7 @@ int fpta_get_option(fpta_ctx* c, int32_t key, int64_t* value) {
     case FPTA_OPT_DFT_GEN: *value = c->dft_gen; return FPTA_OK;
     case FPTA_OPT_GEN_MIX: *value = c->gen_mix; return FPTA_OK;
     case FPTA_OPT_ASYNC_SUMS: *value = c->async_sums; return FPTA_OK;
+    case FPTA_OPT_PART_GROUP: *value = c->part_group; return FPTA_OK;
   }
   return fail(c, FPTA_EINVAL, "get_option: unknown key");
 }

@@ -55,9 +55,10 @@ struct SynthArgs {
   // realization tile the tile table was built for (0 when the kernel takes no tile table)
   int64_t coef_len;
   int32_t tile_toa, tile_real;
-  // gridded interpolation: per-(chunk, realization) partial checksums {sum, sum of squares} [n_chunks][R_pad]
-  // of the stored block, or null (FPTA_OPT_FUSE_CHECKSUMS)
+  // gridded interpolation: partial checksums {sum, sum of squares} of the stored block per (group of part_group
+  // consecutive chunks, realization) [ceil(n_chunks / part_group)][R_pad], or null (FPTA_OPT_FUSE_CHECKSUMS)
   double* part;
+  int32_t part_group;
 };
 
 // MFMA tile geometry
@@ -196,10 +197,11 @@ struct GridUnion {
 };
 hipError_t launch_grid_interp_u(hipStream_t st, const SynthArgs& a, const GridBand& band, const GridUnion& un,
                                 int32_t R_pad);
-// checksums [n_real][2] from the interpolation's partials [n_chunks][R_pad][2], summed over chunks in a fixed
-// order (tmp: kPartSegs * R_pad * 2 doubles)
+// checksums [n_real][2] from the interpolation's partials [n_rows][R_pad][2] (one row per group of part_group
+// consecutive chunks), summed over rows in a fixed order (tmp: kPartSegs * R_pad * 2 doubles)
 constexpr int kPartSegs = 64;
-hipError_t launch_part_checksums(hipStream_t st, const double* part, int32_t n_chunks, int32_t R_pad, int32_t n_real,
+constexpr int kPartGroup = 4, kPartGroupMax = 16;
+hipError_t launch_part_checksums(hipStream_t st, const double* part, int32_t n_rows, int32_t R_pad, int32_t n_real,
                                  double* tmp, double* sums);
 
 hipError_t launch_seeds(hipStream_t st, const SegDesc* segs, int32_t n_seg, const int32_t* psr_of,

@@ -417,6 +417,9 @@ __device__ __forceinline__ void white_quad(int64_t t, int64_t g, uint32_t k0, ui
 template <int RW>
 struct InterpTile {
   int c, p, r0, nq, cnt, y;
+  // partial-checksum row of the tile's chunk group and the chunk's place in it (first: start the row's sums, last:
+  // store them); the diagnostic kernels take one chunk per row
+  int pg = -1, pfirst = 1, plast = 1;
   int rr[kGridVMax / 64];
   const double* G0;
   const double* Wp;
@@ -512,9 +515,12 @@ __device__ __forceinline__ void rs_step(double (&x)[2 * H], bool up) {
 }
 
 // Partial checksums of the tile's chunk, after its stores (the accumulators then die as the first
-// reduce-scatter step consumes them).
+// reduce-scatter step consumes them). A wave takes the chunks of a group (SynthArgs::part_group consecutive chunks)
+// one after another for the same realizations: their partials add up in ps, in chunk order, and the group's last
+// chunk stores the row (C3: a quarter of the per-chunk rows' 0.41 GB per batch written and read back).
 template <int RW>
-__device__ __forceinline__ void interp_partials(const SynthArgs& a, const InterpTile<RW>& t, const d4 (&acc)[2][RW]) {
+__device__ __forceinline__ void interp_partials(const SynthArgs& a, const InterpTile<RW>& t, const d4 (&acc)[2][RW],
+                                                double (&ps)[4]) {
   const int lane = threadIdx.x & 63;
   const int lr = lane & 15, lg = lane >> 4;
   const int tt = 2 * lr;
@@ -525,7 +531,7 @@ __device__ __forceinline__ void interp_partials(const SynthArgs& a, const Interp
     // register g); lane lr ends with k in [4 lr, 4 lr + 4): the realization pair of tiles (2m, 2m + 1) at
     // register g for m = lr >> 2, g = lr & 3, stored with two 16-byte stores (two store instructions per wave)
     static_assert(RW == 8, "16 lanes of a row = 4 realization pairs x 4 registers");
-    double* __restrict__ pp = a.part + ((int64_t)t.c * a.R_pad + t.r0) * 2;
+    double* __restrict__ pp = a.part + ((int64_t)(t.pg >= 0 ? t.pg : t.c) * a.R_pad + t.r0) * 2;
     const bool ok0 = tt < t.cnt, ok1 = tt + 1 < t.cnt;
     double x[32];
     {
@@ -552,12 +558,15 @@ __device__ __forceinline__ void interp_partials(const SynthArgs& a, const Interp
       double (&w)[8] = *reinterpret_cast<double(*)[8]>(&z[0]);
       rs_step<0xB1, 4>(w, (lr & 1) != 0);
     }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) ps[i] = t.pfirst ? x[i] : ps[i] + x[i];
+    if (!t.plast) return;
     const int mm = lr >> 2, gg = lr & 3;
     const int rl = 32 * mm + 2 * (lg + 4 * gg);  // realization of (tile 2mm, register gg); rl + 1: tile 2mm + 1
-    // non-temporal, as the block's own stores: the partials are read back by k_part_reduce from HBM (0.41 GB per
-    // C3 batch), and L2-allocating them would evict the grid rows the next chunks re-read
-    __builtin_nontemporal_store(dbl2{x[0], x[1]}, (dbl2*)(pp + 2 * rl));
-    __builtin_nontemporal_store(dbl2{x[2], x[3]}, (dbl2*)(pp + 2 * rl + 2));
+    // non-temporal, as the block's own stores: the partials are read back by k_part_reduce from HBM, and
+    // L2-allocating them would evict the grid rows the next chunks re-read
+    __builtin_nontemporal_store(dbl2{ps[0], ps[1]}, (dbl2*)(pp + 2 * rl));
+    __builtin_nontemporal_store(dbl2{ps[2], ps[3]}, (dbl2*)(pp + 2 * rl + 2));
   }
 }
 
@@ -629,10 +638,39 @@ __device__ __forceinline__ void interp_store_rows(const SynthArgs& a, double* __
 // The tile's epilogue: its block rows, then (FPTA_OPT_FUSE_CHECKSUMS) its partial checksums.
 template <bool PART, int RW, int PACE = 0>
 __device__ __forceinline__ void interp_store(const SynthArgs& a, double* __restrict__ out, const InterpTile<RW>& t,
-                                             const d4 (&acc)[2][RW]) {
+                                             const d4 (&acc)[2][RW], double (&ps)[4]) {
   interp_store_rows<RW, PACE>(a, out, t, acc);
-  if constexpr (PART) interp_partials<RW>(a, t, acc);
+  if constexpr (PART) interp_partials<RW>(a, t, acc, ps);
 }
+// one chunk per partial row (the diagnostic kernels)
+template <bool PART, int RW, int PACE = 0>
+__device__ __forceinline__ void interp_store(const SynthArgs& a, double* __restrict__ out, const InterpTile<RW>& t,
+                                             const d4 (&acc)[2][RW]) {
+  double ps[4];
+  interp_store<PART, RW, PACE>(a, out, t, acc, ps);
+}
+
+// Tile walk of the persistent interpolation kernels. Work item = (group of G consecutive chunks, realization block),
+// items chunk-group-major (the realization blocks of a group run side by side on one XCD and share its weights and
+// grid rows in L2); a wave takes its item's chunks in order. G = SynthArgs::part_group for fused partial checksums,
+// else 1 (item = chunk x realization block).
+struct TileWalk {
+  int item, k;
+  __device__ __forceinline__ int group(int n_rb) const { return item / n_rb; }
+  __device__ __forceinline__ int chunk(int n_rb, int G) const { return (item / n_rb) * G + k; }
+  // the current tile's chunk ends its group
+  __device__ __forceinline__ bool last(int n_rb, int G, int n_chunks) const {
+    return k + 1 == G || chunk(n_rb, G) + 1 == n_chunks;
+  }
+  __device__ __forceinline__ void next(int n_rb, int G, int n_chunks, int stride) {
+    if (last(n_rb, G, n_chunks)) {
+      item += stride;
+      k = 0;
+    } else {
+      ++k;
+    }
+  }
+};
 
 // Persistent launch: gridDim.x (a multiple of 8) workgroups, about as many as are co-resident; workgroup
 // b runs on XCD b % 8 and walks that XCD's contiguous range of tiles (consecutive chunks: their grid rows
@@ -646,6 +684,9 @@ __global__ __launch_bounds__(256, FPTA_INTERP_WPC) void k_grid_interp_mfma(Synth
   static_assert(RW % 2 == 0, "realization tiles come in pairs");
   static_assert(kGridTT == 32, "two 16-TOA B-tiles per chunk");
   constexpr int NP = RW / 2;
+  // n_tiles: work items (TileWalk), chunk groups x realization blocks
+  const int G = PART ? a.part_group : 1;
+  const int n_rb = (R_pad + 64 * RW - 1) / (64 * RW);
   const int per = (n_tiles + 7) >> 3;
   const int x = blockIdx.x & 7;
   const int stride = gridDim.x >> 3;
@@ -654,12 +695,15 @@ __global__ __launch_bounds__(256, FPTA_INTERP_WPC) void k_grid_interp_mfma(Synth
   const int lane = threadIdx.x & 63;
   const int lr = lane & 15, lg = lane >> 4;
 
-  auto setup = [&](int tile, InterpTile<RW>& t) {
-    // chunk-major tiles: the realization blocks of one chunk are consecutive tiles, so they run together on
+  auto setup = [&](const TileWalk& tw, InterpTile<RW>& t) {
+    // chunk-(group-)major tiles: the realization blocks of one chunk are consecutive tiles, so they run together on
     // one XCD and the chunk's weights are read from HBM once (realization-block-major read them once per block)
-    const int n_rb = (R_pad + 64 * RW - 1) / (64 * RW);
-    t.c = __builtin_amdgcn_readfirstlane(tile / n_rb);
-    const int rb = __builtin_amdgcn_readfirstlane(tile - t.c * n_rb);  // realization block of 64 RW
+    const int grp = __builtin_amdgcn_readfirstlane(tw.group(n_rb));
+    t.c = __builtin_amdgcn_readfirstlane(grp * G + tw.k);
+    const int rb = __builtin_amdgcn_readfirstlane(tw.item - grp * n_rb);  // realization block of 64 RW
+    t.pg = grp;
+    t.pfirst = tw.k == 0;
+    t.plast = tw.last(n_rb, G, band.n_chunks);
     t.r0 = (rb * 4 + wave) * 16 * RW;
     const int4 ci = band.chunks[t.c];
     t.p = __builtin_amdgcn_readfirstlane(ci.x);
@@ -688,6 +732,7 @@ __global__ __launch_bounds__(256, FPTA_INTERP_WPC) void k_grid_interp_mfma(Synth
     bv = *(const dbl2*)(t.Wp + 4 * kGridTT * qq);
   };
   d4 acc[2][RW];  // [TOA parity][realization tile]
+  double ps[4];   // partial checksums of the chunk group so far (PART)
   auto mfma = [&](const dbl2(&av)[NP], const dbl2& bv) {
 #pragma unroll
     for (int m = 0; m < NP; ++m) {
@@ -698,10 +743,10 @@ __global__ __launch_bounds__(256, FPTA_INTERP_WPC) void k_grid_interp_mfma(Synth
     }
   };
 
-  int tile = x * per + (int)(blockIdx.x >> 3);
-  if (tile >= end) return;
+  TileWalk tw{x * per + (int)(blockIdx.x >> 3), 0};
+  if (tw.item >= end) return;
   InterpTile<RW> cur;
-  setup(tile, cur);
+  setup(tw, cur);
   FPTA_DCHECK(R_pad % (16 * RW) == 0, "k_grid_interp_mfma realization padding", R_pad % (16 * RW), 1);
   // operand sets: step q's operands are loaded kInterpDepth steps ahead (FPTA_INTERP_DEPTH 2 or 3). After a tile's
   // epilogue the first load that waits (vmcnt) for its 32 stores is that of step kInterpDepth of the next tile.
@@ -749,23 +794,23 @@ __global__ __launch_bounds__(256, FPTA_INTERP_WPC) void k_grid_interp_mfma(Synth
       // together: this variant stores first, then starts the next tile
       if (cur.r0 < R_pad) {
         interp_white<RW>(a, cur, acc);
-        interp_store<PART, RW>(a, out, cur, acc);
+        interp_store<PART, RW>(a, out, cur, acc, ps);
       }
-      tile += stride;
-      if (tile >= end) break;
-      setup(tile, cur);
+      tw.next(n_rb, G, band.n_chunks, stride);
+      if (tw.item >= end) break;
+      setup(tw, cur);
       prefetch(cur);
     } else {
       // next tile: its first steps are in flight before this tile's stores enter the vmcnt queue
-      tile += stride;
-      const bool more = tile < end;
+      tw.next(n_rb, G, band.n_chunks, stride);
+      const bool more = tw.item < end;
       InterpTile<RW> nxt = cur;
       if (more) {
-        setup(tile, nxt);
+        setup(tw, nxt);
         prefetch(nxt);
       }
       __builtin_amdgcn_sched_barrier(0);
-      if (cur.r0 < R_pad) interp_store<PART, RW>(a, out, cur, acc);
+      if (cur.r0 < R_pad) interp_store<PART, RW>(a, out, cur, acc, ps);
       if (!more) break;
       cur = nxt;
     }
@@ -832,6 +877,7 @@ __global__ __launch_bounds__(512, 1) void k_grid_interp_ws(SynthArgs a, GridBand
   const int end = min(n_tiles, (x + 1) * per);
   const int first = x * per + (int)(blockIdx.x >> 3);
   const int n_rb = (R_pad + 511) / 512;
+  const int G = PART ? a.part_group : 1;  // n_tiles: work items (TileWalk)
   const bool producer = wave >= 4;
   const int w = wave & 3;  // compute wave w, or the producer serving it
   if (first >= end) return;  // no tile: every wave of the workgroup leaves (no barrier issued)
@@ -839,10 +885,12 @@ __global__ __launch_bounds__(512, 1) void k_grid_interp_ws(SynthArgs a, GridBand
   if (producer) {
     // cursor of the step the producer loads next: tile, step q of nq, chunk, realization base. Everything it
     // reads besides the operands is wave-uniform (scalar loads), so its vmcnt counts the ring loads alone.
-    int tile = first, q = 0, nq = 0, c = 0, r0 = 0;
+    TileWalk tw{first, 0};
+    int q = 0, nq = 0, c = 0, r0 = 0;
     auto setup = [&]() {
-      c = __builtin_amdgcn_readfirstlane(tile / n_rb);
-      const int rb = __builtin_amdgcn_readfirstlane(tile - c * n_rb);
+      const int grp = __builtin_amdgcn_readfirstlane(tw.group(n_rb));
+      c = __builtin_amdgcn_readfirstlane(grp * G + tw.k);
+      const int rb = __builtin_amdgcn_readfirstlane(tw.item - grp * n_rb);
       r0 = rb * 512 + w * 128;
       if (r0 >= R_pad) r0 = 0;  // a compute wave past R_pad: valid rows, its sums are never stored
       nq = __builtin_amdgcn_readfirstlane(ld_uniform4(band.chunks + c).w) >> 2;
@@ -868,8 +916,8 @@ __global__ __launch_bounds__(512, 1) void k_grid_interp_ws(SynthArgs a, GridBand
       ++issued;
       if (++q == nq) {
         q = 0;
-        tile += stride;
-        valid = tile < end;
+        tw.next(n_rb, G, band.n_chunks, stride);
+        valid = tw.item < end;
         if (valid) setup();
       }
     };
@@ -892,6 +940,7 @@ __global__ __launch_bounds__(512, 1) void k_grid_interp_ws(SynthArgs a, GridBand
 
   // compute wave
   d4 acc[2][RW];
+  double ps[4];  // partial checksums of the chunk group so far (PART)
 #pragma unroll
   for (int e = 0; e < 2; ++e)
 #pragma unroll
@@ -916,10 +965,14 @@ __global__ __launch_bounds__(512, 1) void k_grid_interp_ws(SynthArgs a, GridBand
   read(0, a0, b0);
   ws_wait_lgkm0();
   int S = 0;
-  for (int tile = first; tile < end; tile += stride) {
+  for (TileWalk tw{first, 0}; tw.item < end; tw.next(n_rb, G, band.n_chunks, stride)) {
     InterpTile<RW> t;
-    t.c = __builtin_amdgcn_readfirstlane(tile / n_rb);
-    const int rb = __builtin_amdgcn_readfirstlane(tile - t.c * n_rb);
+    const int grp = __builtin_amdgcn_readfirstlane(tw.group(n_rb));
+    t.c = __builtin_amdgcn_readfirstlane(grp * G + tw.k);
+    const int rb = __builtin_amdgcn_readfirstlane(tw.item - grp * n_rb);
+    t.pg = grp;
+    t.pfirst = tw.k == 0;
+    t.plast = tw.last(n_rb, G, band.n_chunks);
     t.r0 = rb * 512 + w * 128;
     const int4 ci = ld_uniform4(band.chunks + t.c);
     t.p = __builtin_amdgcn_readfirstlane(ci.x);
@@ -936,7 +989,7 @@ __global__ __launch_bounds__(512, 1) void k_grid_interp_ws(SynthArgs a, GridBand
       for (int m = 0; m < NP; ++m) a0[m] = a1[m];
       b0 = b1;
     }
-    if (t.r0 < R_pad) interp_store<PART, RW>(a, out, t, acc);
+    if (t.r0 < R_pad) interp_store<PART, RW>(a, out, t, acc, ps);
 #pragma unroll
     for (int e = 0; e < 2; ++e)
 #pragma unroll
@@ -1093,8 +1146,10 @@ hipError_t launch_grid_interp_ws(hipStream_t st, const SynthArgs& a, const GridB
   if (band.n_chunks <= 0 || band.vmax < 4 || band.vmax % 4 != 0 || band.vmax > kGridVMax || R_pad % 128 != 0 ||
       a.w_on || a.accumulate)
     return hipErrorInvalidValue;
+  if (a.part && (a.part_group < 1 || a.part_group > kPartGroupMax)) return hipErrorInvalidValue;
   const int32_t n_rb = (R_pad + 511) / 512;
-  const int64_t tiles = (int64_t)band.n_chunks * n_rb;
+  const int32_t G = a.part ? a.part_group : 1;
+  const int64_t tiles = (int64_t)((band.n_chunks + G - 1) / G) * n_rb;  // work items (TileWalk)
   if (tiles > 0x7FFFFFFF) return hipErrorInvalidValue;
   static int n_cu = 0;
   if (!n_cu) {
@@ -1147,8 +1202,10 @@ hipError_t launch_grid_interp_mfma(hipStream_t st, const SynthArgs& a, const Gri
   constexpr int RW = kInterpRW;
   if (band.n_chunks <= 0 || band.vmax < 4 || band.vmax % 4 != 0 || R_pad % (16 * RW) != 0)
     return hipErrorInvalidValue;
+  if (a.part && (a.part_group < 1 || a.part_group > kPartGroupMax)) return hipErrorInvalidValue;
   const int32_t n_rb = (R_pad + 64 * RW - 1) / (64 * RW);
-  const int64_t tiles = (int64_t)band.n_chunks * n_rb;
+  const int32_t G = a.part ? a.part_group : 1;
+  const int64_t tiles = (int64_t)((band.n_chunks + G - 1) / G) * n_rb;  // work items (TileWalk)
   if (tiles > 0x7FFFFFFF) return hipErrorInvalidValue;
   static int n_cu = 0;
   if (!n_cu) {
@@ -1416,16 +1473,17 @@ hipError_t launch_mix_mfma(hipStream_t st, const SegDesc& sd, int32_t P, int32_t
 }
 
 // ----------------------------------------------------------------------------- partial checksums
-// Two fixed-order passes over the interpolation's partials: segment s of kPartSegs sums chunks
+// Two fixed-order passes over the interpolation's partial rows: segment s of kPartSegs sums rows
 // [s L, (s + 1) L) per realization, then the segments are summed in order. Threads run over realizations, so
 // every pass reads consecutive 16-byte {sum, sumsq} pairs.
-__global__ __launch_bounds__(256) void k_part_reduce(const double* __restrict__ part, int32_t n_chunks, int32_t R_pad,
+__global__ __launch_bounds__(256) void k_part_reduce(const double* __restrict__ part, int32_t n_rows, int32_t R_pad,
                                                      int32_t L, double* __restrict__ tmp) {
   const int r = blockIdx.x * 256 + threadIdx.x;
   if (r >= R_pad) return;
   const int s = blockIdx.y;
-  const int c1 = min(n_chunks, (s + 1) * L);
+  const int c1 = min(n_rows, (s + 1) * L);
   double a = 0.0, b = 0.0;
+#pragma unroll 8
   for (int c = s * L; c < c1; ++c) {
     const dbl2 v = *(const dbl2*)(part + ((int64_t)c * R_pad + r) * 2);
     a += v.x;
@@ -1448,13 +1506,13 @@ __global__ __launch_bounds__(256) void k_part_final(const double* __restrict__ t
   sums[2 * r + 1] = b;
 }
 
-hipError_t launch_part_checksums(hipStream_t st, const double* part, int32_t n_chunks, int32_t R_pad, int32_t n_real,
+hipError_t launch_part_checksums(hipStream_t st, const double* part, int32_t n_rows, int32_t R_pad, int32_t n_real,
                                  double* tmp, double* sums) {
-  if (n_chunks <= 0 || n_real <= 0 || n_real > R_pad) return hipErrorInvalidValue;
-  const int32_t L = (n_chunks + kPartSegs - 1) / kPartSegs;
-  const int32_t n_seg = (n_chunks + L - 1) / L;
+  if (n_rows <= 0 || n_real <= 0 || n_real > R_pad) return hipErrorInvalidValue;
+  const int32_t L = (n_rows + kPartSegs - 1) / kPartSegs;
+  const int32_t n_seg = (n_rows + L - 1) / L;
   hipLaunchKernelGGL(k_part_reduce, dim3((unsigned)((R_pad + 255) / 256), (unsigned)n_seg), dim3(256), 0, st, part,
-                     n_chunks, R_pad, L, tmp);
+                     n_rows, R_pad, L, tmp);
   hipLaunchKernelGGL(k_part_final, dim3((unsigned)((n_real + 255) / 256)), dim3(256), 0, st, tmp, n_seg, R_pad, n_real,
                      sums);
   return hipGetLastError();

@@ -337,6 +337,11 @@ int fpta_comm_gather(fpta_comm* comm, const double* send, int64_t count, double*
 #define FPTA_OPT_ASYNC_SUMS 19    /* streamed jobs (fpta_batch_synth_checksums, fpta_multi_synth): 1 a block's partial
                                      checksums are reduced on a stream of their own, beside the next block, into one
                                      of two partials buffers; 0 (default) on the context stream. Identical results. */
+#define FPTA_OPT_PART_GROUP 20    /* fused partial checksums (FPTA_OPT_FUSE_CHECKSUMS): the interpolation sums the partials
+                                     of this many consecutive chunks (1 .. 16, default 4) in registers, in chunk order,
+                                     and writes one {sum, sum of squares} row per group; the reduction then sums the
+                                     groups in order. Deterministic and batch-split invariant for every value; the
+                                     value changes the order of the additions (checksums agree to rounding). */
 int fpta_set_option(fpta_ctx* ctx, int32_t key, int64_t value);
 /* Current value of option `key` (same keys as fpta_set_option). */
 int fpta_get_option(fpta_ctx* ctx, int32_t key, int64_t* value);

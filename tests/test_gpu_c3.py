@@ -83,11 +83,14 @@ def test_c3_multi_device_driver_matches(c3):
         m.close()
 
 
-def test_fused_checksums_match_full_pass(c3):
+@pytest.mark.parametrize("pgroup", [1, 4, 7, 16])
+def test_fused_checksums_match_full_pass(c3, pgroup):
     """FPTA_OPT_FUSE_CHECKSUMS: the interpolation's partial checksums, reduced in a fixed order, agree with a full
-    pass over the resident block (rounding only), including a ragged realization count and the white epilogue."""
+    pass over the resident block (rounding only), including a ragged realization count and the white epilogue, for
+    partial rows of 1, 4 (default), 7 and 16 chunks (FPTA_OPT_PART_GROUP; 7 and 16 leave a short last group)."""
     from fakepta_amd import _capi
     psrs, sim, ctx = c3
+    ctx.set_option(_capi.OPT_PART_GROUP, pgroup)
     try:
         for n, white in ((1808, False), (333, True)):
             if white:
@@ -104,6 +107,7 @@ def test_fused_checksums_match_full_pass(c3):
             assert not np.array_equal(fused, full) or n < 2  # the fused route ran (different summation order)
     finally:
         ctx.set_option(_capi.OPT_FUSE_CHECKSUMS, 0)
+        ctx.set_option(_capi.OPT_PART_GROUP, 4)
         ctx.batch_set_white(None, [], [])
 
 

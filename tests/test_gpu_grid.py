@@ -321,6 +321,7 @@ def test_lds_interpolation_is_bitwise_identical(ctx, capi, shipped, fuse):
     try:
         ctx.set_option(capi.OPT_SYNTH_PATH, 4)
         ctx.set_option(capi.OPT_FUSE_CHECKSUMS, fuse)
+        ctx.set_option(capi.OPT_PART_GROUP, 1)  # the diagnostic kernels write one partial row per chunk
         res = {}
         for lds in (0, 1):
             ctx.set_option(capi.OPT_INTERP_LDS, lds)
@@ -446,13 +447,14 @@ def test_pipelined_layout_switches_are_bitwise_identical(ctx, capi, shipped):
         ctx.set_options(shipped)
 
 
-@pytest.mark.parametrize("fuse", [0, 1])
+@pytest.mark.parametrize("fuse,pgroup", [(0, 4), (1, 1), (1, 3), (1, 4)])
 @pytest.mark.parametrize("R", [333, 1024, 1100])
-def test_warp_specialised_interpolation_is_bitwise_identical(ctx, capi, shipped, fuse, R):
+def test_warp_specialised_interpolation_is_bitwise_identical(ctx, capi, shipped, fuse, pgroup, R):
     """FPTA_OPT_INTERP_WS: the warp-specialised interpolation (producer waves fill an LDS ring, compute waves run the
     same MFMA steps and only store) returns the register-pipelined kernel's block and checksums bit for bit, on a
     ragged multi-signal layout with unsorted TOAs, for realization counts that leave compute waves idle (R_pad not a
-    multiple of 512)."""
+    multiple of 512), and with the fused partial checksums summed over groups of 1, 3 or 4 chunks
+    (FPTA_OPT_PART_GROUP: 23 pulsars' chunks leave a short last group)."""
     rng = np.random.default_rng(43)
     offs, toas, nu = random_layout(rng, 23, (31, 260))
     perm = rng.permutation(offs[1] - offs[0])
@@ -467,10 +469,11 @@ def test_warp_specialised_interpolation_is_bitwise_identical(ctx, capi, shipped,
     try:
         ctx.set_option(capi.OPT_SYNTH_PATH, 4)
         ctx.set_option(capi.OPT_FUSE_CHECKSUMS, fuse)
+        ctx.set_option(capi.OPT_PART_GROUP, pgroup)
         res = {}
         # 2: WS also for fused-checksum blocks; 3: k_grid_interp_ws2 (two workgroups per CU); 4: k_grid_interp_st
-        # (storer waves, diagnostic builds only)
-        variants = (1, 2, 3, 4) if _diag_build(capi) else (1, 2, 3)
+        # (storer waves, diagnostic builds only: one partial row per chunk)
+        variants = (1, 2, 3, 4) if _diag_build(capi) and (not fuse or pgroup == 1) else (1, 2, 3)
         for ws in (0,) + variants:
             ctx.set_option(capi.OPT_INTERP_WS, ws)
             res[ws] = (ctx.batch_synth(5, 300, R), ctx.batch_checksums())
@@ -541,6 +544,7 @@ def test_storer_interpolation_white_ecorr_is_bitwise_identical(ctx, capi, shippe
     try:
         ctx.set_option(capi.OPT_SYNTH_PATH, 4)
         ctx.set_option(capi.OPT_FUSE_CHECKSUMS, fuse)
+        ctx.set_option(capi.OPT_PART_GROUP, 1)  # the diagnostic kernels write one partial row per chunk
         res = {}
         for ws in (0, 4):
             ctx.set_option(capi.OPT_INTERP_WS, ws)
@@ -593,6 +597,7 @@ def test_union_interpolation_is_bitwise_identical(ctx, capi, shipped, fuse, layo
     try:
         ctx.set_option(capi.OPT_SYNTH_PATH, 4)
         ctx.set_option(capi.OPT_FUSE_CHECKSUMS, fuse)
+        ctx.set_option(capi.OPT_PART_GROUP, 1)  # the diagnostic kernels write one partial row per chunk
         res = {}
         for ws in (0, 5):
             ctx.set_option(capi.OPT_INTERP_WS, ws)
