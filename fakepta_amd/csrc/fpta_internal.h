@@ -200,7 +200,7 @@ hipError_t launch_grid_interp_u(hipStream_t st, const SynthArgs& a, const GridBa
 // checksums [n_real][2] from the interpolation's partials [n_rows][R_pad][2] (one row per group of part_group
 // consecutive chunks), summed over rows in a fixed order (tmp: kPartSegs * R_pad * 2 doubles)
 constexpr int kPartSegs = 64;
-constexpr int kPartGroup = 4, kPartGroupMax = 16;
+constexpr int kPartGroup = 16, kPartGroupMax = 16;
 hipError_t launch_part_checksums(hipStream_t st, const double* part, int32_t n_rows, int32_t R_pad, int32_t n_real,
                                  double* tmp, double* sums);
 

@@ -338,7 +338,7 @@ int fpta_comm_gather(fpta_comm* comm, const double* send, int64_t count, double*
                                      checksums are reduced on a stream of their own, beside the next block, into one
                                      of two partials buffers; 0 (default) on the context stream. Identical results. */
 #define FPTA_OPT_PART_GROUP 20    /* fused partial checksums (FPTA_OPT_FUSE_CHECKSUMS): the interpolation sums the partials
-                                     of this many consecutive chunks (1 .. 16, default 4) in registers, in chunk order,
+                                     of this many consecutive chunks (1 .. 16, default 16) in registers, in chunk order,
                                      and writes one {sum, sum of squares} row per group; the reduction then sums the
                                      groups in order. Deterministic and batch-split invariant for every value; the
                                      value changes the order of the additions (checksums agree to rounding). */

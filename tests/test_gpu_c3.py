@@ -87,7 +87,7 @@ def test_c3_multi_device_driver_matches(c3):
 def test_fused_checksums_match_full_pass(c3, pgroup):
     """FPTA_OPT_FUSE_CHECKSUMS: the interpolation's partial checksums, reduced in a fixed order, agree with a full
     pass over the resident block (rounding only), including a ragged realization count and the white epilogue, for
-    partial rows of 1, 4 (default), 7 and 16 chunks (FPTA_OPT_PART_GROUP; 7 and 16 leave a short last group)."""
+    partial rows of 1, 4, 7 and 16 (default) chunks (FPTA_OPT_PART_GROUP; 7 and 16 leave a short last group)."""
     from fakepta_amd import _capi
     psrs, sim, ctx = c3
     ctx.set_option(_capi.OPT_PART_GROUP, pgroup)
@@ -107,7 +107,7 @@ def test_fused_checksums_match_full_pass(c3, pgroup):
             assert not np.array_equal(fused, full) or n < 2  # the fused route ran (different summation order)
     finally:
         ctx.set_option(_capi.OPT_FUSE_CHECKSUMS, 0)
-        ctx.set_option(_capi.OPT_PART_GROUP, 4)
+        ctx.set_option(_capi.OPT_PART_GROUP, 16)
         ctx.batch_set_white(None, [], [])
 
 

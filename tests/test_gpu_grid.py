@@ -447,13 +447,13 @@ def test_pipelined_layout_switches_are_bitwise_identical(ctx, capi, shipped):
         ctx.set_options(shipped)
 
 
-@pytest.mark.parametrize("fuse,pgroup", [(0, 4), (1, 1), (1, 3), (1, 4)])
+@pytest.mark.parametrize("fuse,pgroup", [(0, 16), (1, 1), (1, 3), (1, 16)])
 @pytest.mark.parametrize("R", [333, 1024, 1100])
 def test_warp_specialised_interpolation_is_bitwise_identical(ctx, capi, shipped, fuse, pgroup, R):
     """FPTA_OPT_INTERP_WS: the warp-specialised interpolation (producer waves fill an LDS ring, compute waves run the
     same MFMA steps and only store) returns the register-pipelined kernel's block and checksums bit for bit, on a
     ragged multi-signal layout with unsorted TOAs, for realization counts that leave compute waves idle (R_pad not a
-    multiple of 512), and with the fused partial checksums summed over groups of 1, 3 or 4 chunks
+    multiple of 512), and with the fused partial checksums summed over groups of 1, 3 or 16 chunks
     (FPTA_OPT_PART_GROUP: 23 pulsars' chunks leave a short last group)."""
     rng = np.random.default_rng(43)
     offs, toas, nu = random_layout(rng, 23, (31, 260))

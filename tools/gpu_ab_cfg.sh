@@ -26,7 +26,7 @@ for rep in 1 2; do
     log=gpurun_out/${tag}_${cfg}_v${i}_r$rep.log
     case $cfg in
       c2) timeout -k 10 300 python -u bench.py --cpu-sample 0 --steps 30 --exact-launches 3 $flags > $log 2>&1 ;;
-      c3) timeout -k 10 300 python -u bench.py --cpu-sample 0 --config c3 --steps 2 --warmup 1 $flags > $log 2>&1 ;;
+      c3) timeout -k 10 300 python -u bench.py --cpu-sample 0 --config c3 --steps 4 --warmup 2 --sub-configs 0 $flags > $log 2>&1 ;;
       *) timeout -k 10 300 python -u tools/bench_configs.py $cfg $flags > $log 2>&1 ;;
     esac || { tail -20 $log; exit 1; }
     grep '^{' $log | python -c "
