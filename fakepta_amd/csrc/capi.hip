@@ -34,6 +34,10 @@ struct DevBuf {
     p = nullptr;
     cap = 0;
   }
+  void swap(DevBuf& o) {
+    std::swap(p, o.p);
+    std::swap(cap, o.cap);
+  }
   hipError_t ensure(size_t bytes) {
     if (bytes <= cap && p) return hipSuccess;
     release();
@@ -84,6 +88,12 @@ struct GridPlan {
   DevBuf rows;               // [n_chunks][vmax] int32 grid-buffer row of each band row (all signals back to back)
   DevBuf wd;                 // [n_chunks][vmax][kGridTT] interpolation weights (chromatic factor, mask folded in)
   DevBuf g, g2;              // [grid_rows][R_pad] grid values of the batch (two buffers when pipelined)
+  std::vector<int32_t> psr_chunk0;  // [P + 1] first chunk of each pulsar (chunks are pulsar-major)
+  // partial-checksum groups (FPTA_OPT_FUSE_CHECKSUMS): <= pg_size consecutive chunks of one pulsar each; pgfirst
+  // [n_pg + 1] the first chunk of each group, psr_pg [P + 1] the first group of each pulsar
+  int32_t pg_size = 0, n_pg = 0;
+  DevBuf pgfirst, psr_pg;
+  DevBuf psr_c0;  // device copy of psr_chunk0 (k_grid_interp_psr without partial checksums)
   // k_grid_interp_lds plan: groups int4 {first chunk, chunks, union rows U, offset into urows}; urows the grid-
   // buffer rows of each group's union; lrows [n_chunks][vmax] the union slot of each band row
   bool lds_ok = false;
@@ -125,6 +135,8 @@ struct GridPlan {
     u_groups = u_sig = 0;
     grid_rows = 0;
     g_rpad = 0;
+    psr_chunk0.clear();
+    pg_size = n_pg = 0;
     members.clear();
     anchor.clear();
     last.clear();
@@ -202,6 +214,13 @@ struct fpta_ctx {
   int last_interp = 0;    // interpolation kernel of the last gridded block: 1 + 4 kind + 2 white + part (0: none)
   int grid_coalesce = 1;  // gridded path: signals sharing w0 and the chromatic weight share one grid (FPTA_OPT_GRID_COALESCE)
   int part_group = kPartGroup;  // fused partial checksums: consecutive chunks per partial row (FPTA_OPT_PART_GROUP)
+  int interp_psr = 1;  // k_grid_interp_psr where the layout allows it (FPTA_OPT_INTERP_PSR)
+  // pipelined per-pulsar blocks read their coefficients in the interpolation (ctx stream): two coefficient buffers,
+  // coef2 the other one; coef_slot = the grid-buffer index whose block owns c->coef; prev_psr: the last pipelined
+  // block ran that way (its draws waited for the interpolation two blocks back, not for the whole ctx stream)
+  DevBuf coef2;
+  int coef_slot = 0;
+  bool prev_psr = false;
   int async_sums = 0;    // streamed jobs: partial-checksum reductions on their own stream (FPTA_OPT_ASYNC_SUMS; measured
                          // no faster on C3, profiles/r03h_ab_c3_async_sums.txt: the reductions then compete with the interpolation)
   int gen_mix = 2;       // common signals of 64..256 pulsars: draws and ORF mixing in one kernel (k_gen_mix,
@@ -551,6 +570,18 @@ bool grid_gen_fused(const fpta_ctx* c, const Layout& L, size_t g) {
   return false;
 }
 
+// The gridded plan of L runs on k_grid_interp_psr (FPTA_OPT_INTERP_PSR): one grid signal whose coefficients come
+// from the coefficient buffer through the MFMA DFT (the kernel reproduces k_grid_dft_mfma), one 32-row DFT block
+// (nf <= 124), bands of <= 32 rows, and no diagnostic interpolation kernel chosen.
+bool psr_layout(const fpta_ctx* c, const Layout& L) {
+  const GridPlan& G = L.grid;
+  if (!c->interp_psr || !G.built || !G.ok || G.segs.size() != 1 || grid_gen_fused(c, L, 0) || !(c->grid_mfma & 1) ||
+      c->interp_lds || c->interp_ws >= 4)
+    return false;
+  const GridSeg* gs = G.segs[0];
+  return gs->nf <= 124 && gs->nf % 4 == 0 && gs->ldq == kGridDftRows && G.vmax <= 32 && gs->rowoff == 0;
+}
+
 // merge: the gridded plan of L coalesces signals (GridPlan::members): after the last member of a grid signal is
 // drawn, k_coef_merge adds the other members' columns into the anchor's. coef_host (optional, with merge): the
 // per-signal coefficients [P][K][R] are downloaded before any merge and *coef_done is set.
@@ -566,6 +597,13 @@ int run_coefficients(fpta_ctx* c, Layout& L, uint64_t seed, int64_t real0, int32
   const bool last_side = c->coef_last_side;
   c->coef_last_side = false;
   if (!use_side) c->coef_free_set = false;  // coef is written on the ctx stream from here on
+  // a pipelined per-pulsar block draws into the coefficient buffer of its grid-buffer index (the interpolation of the
+  // previous block may still read the other one)
+  const bool psr = pipe && use_side && !zin && !x_out && !coef_host && psr_layout(c, L);
+  if (psr && c->coef_slot != c->gbuf) {
+    c->coef.swap(c->coef2);
+    c->coef_slot = c->gbuf;
+  }
   const size_t coef_bytes = sizeof(double) * (size_t)P * std::max(L.K, 1) * R_pad;
   if (c->side && c->coef.cap < coef_bytes) HIPCHK(c, hipStreamSynchronize(c->side), "side sync");  // before a regrow
   if (c->side2 && c->coef.cap < coef_bytes) HIPCHK(c, hipStreamSynchronize(c->side2), "side sync");
@@ -580,10 +618,13 @@ int run_coefficients(fpta_ctx* c, Layout& L, uint64_t seed, int64_t real0, int32
     // the previous block's last reader of coef (its DFT or download) comes first; without one recorded,
     // everything queued on the ctx stream. A pipelined block whose DFT (on this stream) was that reader needs no
     // wait, unless the draws read a ctx-stream upload (zin)
-    if (!(pipe && last_side && !c->coef_free_set && !zin)) {
+    // (a per-pulsar block after another: its buffer's last reader was the interpolation two blocks back)
+    if (!(pipe && last_side && !c->coef_free_set && !zin) && !(psr && c->prev_psr)) {
       if (!c->coef_free_set) HIPCHK(c, hipEventRecord(c->ev_begin, c->stream), "event record");
       HIPCHK(c, hipStreamWaitEvent(c->side, c->coef_free_set ? c->ev_coef_free : c->ev_begin, 0), "side wait");
     }
+    if (psr && c->gfree_set[c->gbuf])
+      HIPCHK(c, hipStreamWaitEvent(c->side, c->ev_gfree[c->gbuf], 0), "coefficient buffer wait");
     c->coef_free_set = false;
     // the previous split block's second side stream (its draws and DFT) comes first as well
     if (c->s2done_set) HIPCHK(c, hipStreamWaitEvent(c->side, c->ev_gready2, 0), "side wait");
@@ -724,6 +765,7 @@ int run_coefficients(fpta_ctx* c, Layout& L, uint64_t seed, int64_t real0, int32
       for (size_t i = 0; i < L.segs.size(); ++i) HIPCHK(c, hipEventRecord(c->ev_sig[i], st), "event record");
   }
   c->coef_side = st != c->stream && !pipe;  // pipelined: the DFT follows on the same stream, no per-signal events
+  c->prev_psr = psr;
   return FPTA_OK;
 }
 
@@ -978,6 +1020,13 @@ int grid_build(fpta_ctx* c, Layout& L) {
     return FPTA_OK;
   }
   G.n_chunks = (int32_t)chunks.size();
+  G.psr_chunk0.assign((size_t)L.P + 1, 0);
+  for (int32_t ci = (int32_t)chunks.size() - 1; ci >= 0; --ci) G.psr_chunk0[chunks[ci].x] = ci;
+  G.psr_chunk0[L.P] = G.n_chunks;
+  for (int32_t p = L.P - 1; p >= 0; --p)  // a pulsar without TOAs has no chunk: it starts where the next one does
+    if (L.h_offs[p + 1] == L.h_offs[p]) G.psr_chunk0[p] = G.psr_chunk0[p + 1];
+  if (int rc0 = upload(c, G.psr_c0, G.psr_chunk0.data(), sizeof(int32_t) * G.psr_chunk0.size(), "pulsar chunks"))
+    return rc0;
   const int32_t n_chunks = G.n_chunks;
   // band rows of a chunk: every signal's band back to back (virtual rows voff_s ..), padded to a multiple of
   // 4 once per chunk (k_grid_interp_mfma: 4 rows per MFMA step; pad rows re-read a valid row at weight 0), and to at
@@ -1246,6 +1295,26 @@ int grid_build(fpta_ctx* c, Layout& L) {
   return FPTA_OK;
 }
 
+// Partial-checksum groups of G: each pulsar's chunks cut into runs of <= size consecutive chunks (a group never spans
+// two pulsars, so a workgroup that owns a pulsar owns its groups), uploaded once per (plan, size).
+int grid_part_groups(fpta_ctx* c, GridPlan& G, int32_t P, int32_t size) {
+  if (G.pg_size == size) return FPTA_OK;
+  std::vector<int32_t> first, psr((size_t)P + 1);
+  for (int32_t p = 0; p < P; ++p) {
+    psr[p] = (int32_t)first.size();
+    for (int32_t ci = G.psr_chunk0[p]; ci < G.psr_chunk0[p + 1]; ci += size) first.push_back(ci);
+  }
+  psr[P] = (int32_t)first.size();
+  first.push_back(G.n_chunks);
+  int rc;
+  if ((rc = upload(c, G.pgfirst, first.data(), sizeof(int32_t) * first.size(), "partial groups")) ||
+      (rc = upload(c, G.psr_pg, psr.data(), sizeof(int32_t) * psr.size(), "partial groups of pulsars")))
+    return rc;
+  G.n_pg = (int32_t)first.size() - 1;
+  G.pg_size = size;
+  return FPTA_OK;
+}
+
 // Run the gridded synthesis: one DFT launch per grid signal, then one interpolation launch for all.
 // pipe (run_coefficients drew this block on the side stream in pipelined mode): the DFTs follow there, into grid
 // buffer c->gbuf, and the interpolation on the ctx stream waits only for them.
@@ -1264,13 +1333,34 @@ int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad, bool pipe = fa
   }
   const int gi = pipe ? c->gbuf : 0;
   double* const gbase = gi ? G.g2.as<double>() : G.g.as<double>();
+  // k_grid_interp_psr: no DFT launch, no grid buffer; in a pipelined block the coefficients drawn on the side stream
+  // into buffer gi are this block's (run_coefficients)
+  const bool psr = psr_layout(c, L) && !a.w_on && !a.accumulate && (!pipe || c->prev_psr);
   if (pipe) {
     for (hipEvent_t* e : {&c->ev_gready, &c->ev_gfree[0], &c->ev_gfree[1]})
       if (!*e) HIPCHK(c, hipEventCreateWithFlags(e, hipEventDisableTiming), "event create");
     // the DFT overwrites buffer gi: the interpolation that last read it (two blocks back) must be done
     if (c->gfree_set[gi]) HIPCHK(c, hipStreamWaitEvent(c->side, c->ev_gfree[gi], 0), "grid buffer wait");
   }
-  {
+  if (psr) {
+    GridSeg* gs = G.segs[0];
+    GridSegDev& g = gsegs.s[0];
+    g.g = nullptr;
+    g.nf = gs->nf;
+    g.half = gs->half;
+    g.nm = L.segs[G.anchor[0]]->d.nm;
+    g.col0 = L.segs[G.anchor[0]]->d.col0;
+    g.tq = gs->tq.as<double>();
+    g.ldq = gs->ldq;
+    g.ntq = gs->ntq;
+    if (pipe) {
+      HIPCHK(c, hipEventRecord(c->ev_gready, c->side), "event record");
+      c->coef_last_side = false;  // the interpolation on the ctx stream reads the coefficients
+    } else {
+      int rc = wait_coef_all(c);
+      if (rc) return rc;
+    }
+  } else {
     KTimer kt(c, FPTA_K_GRID, pipe ? c->side : c->stream);
     for (size_t s = 0; s < G.segs.size(); ++s) {
       GridSeg* gs = G.segs[s];
@@ -1393,7 +1483,8 @@ int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad, bool pipe = fa
     // the reduction of the block that last wrote this buffer (on the red stream) must have read it
     if (c->pfree_set[pi]) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_pfree[pi], 0), "partials buffer wait");
     a.part = pb.as<double>();
-    a.part_group = c->part_group;  // the diagnostic kernels below write one row per chunk
+    int rc = grid_part_groups(c, G, L.P, c->part_group);
+    if (rc) return rc;
     c->part_cur = pi;
     c->part_next = pi ^ 1;
   }
@@ -1401,7 +1492,7 @@ int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad, bool pipe = fa
   if (pipe && c->s2done_set) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_gready2, 0), "grid ready wait");
   KTimer kt(c, FPTA_K_SYNTH);
   GridBand band{G.chunks.as<int4>(), G.rows.as<int32_t>(), G.wd.as<double>(), gbase, G.n_chunks, G.vmax,
-                G.grid_rows};
+                G.grid_rows, a.part ? G.pgfirst.as<int32_t>() : nullptr, a.part ? G.n_pg : G.n_chunks};
   // the warp-specialised kernel for plain blocks; with fused partial checksums its reduce-scatter temporaries take
   // its VGPRs to 230 and the register kernel is faster (C3: 47.9 vs 52.5 ms per job, profiles/r02k_ab_c2c3_ws.txt)
   // k_grid_interp_ws tiles 512 realizations (4 compute waves x 128): when R_pad leaves some of the last tile's compute
@@ -1413,16 +1504,24 @@ int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad, bool pipe = fa
 #ifdef FPTA_DIAG_KERNELS
   } else if (c->interp_ws == 5 && !c->interp_lds && G.u_ok && !a.w_on) {
     kind = 5;
-    a.part_group = 1;
+    band.pgfirst = nullptr;  // the diagnostic kernels write one partial row per chunk
+    band.n_pg = G.n_chunks;
     GridUnion un{G.ugroups.as<int4>(), G.uurows.as<int32_t>(), G.ucbase.as<int32_t>(), G.udch.as<double>(),
                  G.uwrow.as<int32_t>(), G.u_groups, G.u_sig, {G.u_w[0], G.u_w[1]}, {G.u_hw[0], G.u_hw[1]},
                  {G.u_beta[0], G.u_beta[1]}};
     HIPCHK(c, launch_grid_interp_u(c->stream, a, band, un, R_pad), "k_grid_interp_u launch");
   } else if (c->interp_ws == 4 && !c->interp_lds) {
     kind = 4;
-    a.part_group = 1;
+    band.pgfirst = nullptr;
+    band.n_pg = G.n_chunks;
     HIPCHK(c, launch_grid_interp_st(c->stream, a, band, R_pad), "k_grid_interp_st launch");
 #endif
+  } else if (psr) {
+    kind = G.vmax <= 16 ? 6 : 7;  // launch_grid_interp_psr: NQ = 4 or 8 band steps
+    HIPCHK(c,
+           launch_grid_interp_psr(c->stream, a, band, gsegs.s[0],
+                                  a.part ? G.psr_pg.as<int32_t>() : G.psr_c0.as<int32_t>(), L.P, R_pad),
+           "k_grid_interp_psr launch");
   } else if ((c->interp_ws == 3 || ws2_fits) && !c->interp_lds && !a.w_on && !a.accumulate && !a.part) {
     kind = 2;
     HIPCHK(c, launch_grid_interp_ws(c->stream, a, band, R_pad, true), "k_grid_interp_ws2 launch");
@@ -1432,7 +1531,8 @@ int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad, bool pipe = fa
 #ifdef FPTA_DIAG_KERNELS
   } else if (c->interp_lds && G.lds_ok && !a.w_on) {
     kind = 3;
-    a.part_group = 1;
+    band.pgfirst = nullptr;
+    band.n_pg = G.n_chunks;
     GridLds lds{G.groups.as<int4>(), G.urows.as<int32_t>(), G.lrows.as<int32_t>(), G.n_groups, G.lds_rows};
     HIPCHK(c, launch_grid_interp_lds(c->stream, a, band, lds, R_pad), "k_grid_interp_lds launch");
 #endif
@@ -1448,7 +1548,7 @@ int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad, bool pipe = fa
   }
   if (a.part) {
     c->part_ready = true;
-    c->part_chunks = (G.n_chunks + a.part_group - 1) / a.part_group;  // partial rows
+    c->part_chunks = band.n_pg;  // partial rows
     c->part_rpad = R_pad;
   }
   return FPTA_OK;
@@ -1850,6 +1950,9 @@ int fpta_set_option(fpta_ctx* c, int32_t key, int64_t value) {
       if (value < 1 || value > kPartGroupMax) return fail(c, FPTA_EINVAL, "part_group must be 1 .. 16");
       c->part_group = (int)value;
       return FPTA_OK;
+    case FPTA_OPT_INTERP_PSR:
+      c->interp_psr = value ? 1 : 0;
+      return FPTA_OK;
     case FPTA_OPT_GRID_COALESCE:
       c->grid_coalesce = value ? 1 : 0;
       c->batch.grid.clear();
@@ -1906,6 +2009,7 @@ int fpta_get_option(fpta_ctx* c, int32_t key, int64_t* value) {
     case FPTA_OPT_GEN_MIX: *value = c->gen_mix; return FPTA_OK;
     case FPTA_OPT_ASYNC_SUMS: *value = c->async_sums; return FPTA_OK;
     case FPTA_OPT_PART_GROUP: *value = c->part_group; return FPTA_OK;
+    case FPTA_OPT_INTERP_PSR: *value = c->interp_psr; return FPTA_OK;
   }
   return fail(c, FPTA_EINVAL, "get_option: unknown key");
 }

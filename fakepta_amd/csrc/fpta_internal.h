@@ -55,10 +55,9 @@ struct SynthArgs {
   // realization tile the tile table was built for (0 when the kernel takes no tile table)
   int64_t coef_len;
   int32_t tile_toa, tile_real;
-  // gridded interpolation: partial checksums {sum, sum of squares} of the stored block per (group of part_group
-  // consecutive chunks, realization) [ceil(n_chunks / part_group)][R_pad], or null (FPTA_OPT_FUSE_CHECKSUMS)
+  // gridded interpolation: partial checksums {sum, sum of squares} of the stored block per (partial group of chunks,
+  // realization) [GridBand::n_pg][R_pad], or null (FPTA_OPT_FUSE_CHECKSUMS)
   double* part;
-  int32_t part_group;
 };
 
 // MFMA tile geometry
@@ -157,6 +156,10 @@ struct GridBand {
   const double* g;      // [grid_rows][R_pad] grid values (all signals)
   int32_t n_chunks, vmax;
   int64_t grid_rows;
+  // fused partial checksums: [n_pg + 1] first chunk of each partial group (runs of consecutive chunks of one pulsar,
+  // one partial row each); null: one chunk per group (n_pg = n_chunks)
+  const int32_t* pgfirst;
+  int32_t n_pg;
 };
 hipError_t launch_grid_interp_mfma(hipStream_t st, const SynthArgs& a, const GridBand& band, int32_t R_pad);
 // Warp-specialised variant (producer waves stage operands in an LDS ring, compute waves never load from global memory,
@@ -164,6 +167,12 @@ hipError_t launch_grid_interp_mfma(hipStream_t st, const SynthArgs& a, const Gri
 // ws2: k_grid_interp_ws2 (64-realization compute tiles, two workgroups per CU), plain blocks only
 hipError_t launch_grid_interp_ws(hipStream_t st, const SynthArgs& a, const GridBand& band, int32_t R_pad,
                                  bool ws2 = false);
+// Per-pulsar variant for one small grid signal (nf <= 124, vmax <= 32, no white epilogue): a workgroup makes one
+// pulsar's grid for 64 realizations in LDS (k_grid_dft_mfma's quarter-range DFT from the coefficient buffer) and
+// interpolates the pulsar's chunks from it; no grid buffer. psr_grp [P + 1]: the first partial group (a.part) or chunk
+// of each pulsar. Bit-identical to k_grid_dft_mfma + k_grid_interp_mfma.
+hipError_t launch_grid_interp_psr(hipStream_t st, const SynthArgs& a, const GridBand& band, const GridSegDev& gs,
+                                  const int32_t* psr_grp, int32_t P, int32_t R_pad);
 // Storer-wave variant: compute waves hand finished sums to storer waves through LDS; every block kind (white / ECORR
 // epilogue, partial checksums, accumulate) with R_pad a multiple of 128
 hipError_t launch_grid_interp_st(hipStream_t st, const SynthArgs& a, const GridBand& band, int32_t R_pad);

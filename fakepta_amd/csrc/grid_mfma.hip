@@ -515,12 +515,12 @@ __device__ __forceinline__ void rs_step(double (&x)[2 * H], bool up) {
 }
 
 // Partial checksums of the tile's chunk, after its stores (the accumulators then die as the first
-// reduce-scatter step consumes them). A wave takes the chunks of a group (SynthArgs::part_group consecutive chunks)
-// one after another for the same realizations: their partials add up in ps, in chunk order, and the group's last
-// chunk stores the row (C3: a quarter of the per-chunk rows' 0.41 GB per batch written and read back).
+// reduce-scatter step consumes them). A wave takes the chunks of a partial group (GridBand::pgfirst: consecutive
+// chunks of one pulsar) one after another for the same realizations: their partials add up in ps, in chunk order, and
+// the group's last chunk stores the row (C3, groups of 16: 1/16 of the per-chunk rows' 0.41 GB per batch).
 template <int RW>
 __device__ __forceinline__ void interp_partials(const SynthArgs& a, const InterpTile<RW>& t, const d4 (&acc)[2][RW],
-                                                double (&ps)[4]) {
+                                                double (&ps)[RW / 2]) {
   const int lane = threadIdx.x & 63;
   const int lr = lane & 15, lg = lane >> 4;
   const int tt = 2 * lr;
@@ -528,19 +528,22 @@ __device__ __forceinline__ void interp_partials(const SynthArgs& a, const Interp
     // partial checksums of this chunk: per realization the sum and sum of squares over the chunk's TOAs (lanes
     // without a TOA add 0), reduced over the 16 lanes of each row by a reduce-scatter (row_mirror, half_mirror,
     // xor 2, xor 1). Value k = 2 c + {0: sum, 1: sumsq} of combination c = 2 (4 m + g) + h (tile 2m + h,
-    // register g); lane lr ends with k in [4 lr, 4 lr + 4): the realization pair of tiles (2m, 2m + 1) at
-    // register g for m = lr >> 2, g = lr & 3, stored with two 16-byte stores (two store instructions per wave)
-    static_assert(RW == 8, "16 lanes of a row = 4 realization pairs x 4 registers");
+    // register g), NV = 8 RW values; lane lr ends with k in [NV / 16 lr, NV / 16 (lr + 1)). RW = 8: the realization
+    // pair of tiles (2m, 2m + 1) at register g for m = lr >> 2, g = lr & 3 (two 16-byte stores); RW = 4: combination
+    // c = lr (one 16-byte store). Every value is summed over the 16 lanes by the same pairing tree whatever RW (each
+    // step pairs the same lanes; only which half a lane keeps differs), so both give the same bits.
+    static_assert(RW == 8 || RW == 4, "16 lanes of a row hold 16 RW / 2 values after the first step");
+    constexpr int H1 = 4 * RW;  // values per lane after the first step
     double* __restrict__ pp = a.part + ((int64_t)(t.pg >= 0 ? t.pg : t.c) * a.R_pad + t.r0) * 2;
     const bool ok0 = tt < t.cnt, ok1 = tt + 1 < t.cnt;
-    double x[32];
+    double x[H1];
     {
-      // first step straight from the accumulators (the 64 values are never all live): lanes 8..15 keep
-      // combinations 16..31, lanes 0..7 combinations 0..15
+      // first step straight from the accumulators (the NV values are never all live): lanes 8..15 keep the upper
+      // half of the combinations, lanes 0..7 the lower
       const bool up = lr >= 8;
 #pragma unroll
-      for (int j = 0; j < 32; ++j) {
-        const int k0 = j, k1 = j + 32;  // the two values of this slot: kept or sent
+      for (int j = 0; j < H1; ++j) {
+        const int k0 = j, k1 = j + H1;  // the two values of this slot: kept or sent
         auto value = [&](int k) {
           const int c = k >> 1, h = c & 1, mg = c >> 1, m = mg >> 2, g = mg & 3;
           const double v0 = ok0 ? acc[0][2 * m + h][g] : 0.0, v1 = ok1 ? acc[1][2 * m + h][g] : 0.0;
@@ -551,22 +554,28 @@ __device__ __forceinline__ void interp_partials(const SynthArgs& a, const Interp
       }
     }
     {
-      double (&y)[32] = x;
-      rs_step<0x141, 16>(y, (lr & 7) >= 4);
-      double (&z)[16] = *reinterpret_cast<double(*)[16]>(&y[0]);
-      rs_step<0x4E, 8>(z, (lr & 3) >= 2);
-      double (&w)[8] = *reinterpret_cast<double(*)[8]>(&z[0]);
-      rs_step<0xB1, 4>(w, (lr & 1) != 0);
+      double (&y)[H1] = x;
+      rs_step<0x141, H1 / 2>(y, (lr & 7) >= 4);
+      double (&z)[H1 / 2] = *reinterpret_cast<double(*)[H1 / 2]>(&y[0]);
+      rs_step<0x4E, H1 / 4>(z, (lr & 3) >= 2);
+      double (&w)[H1 / 4] = *reinterpret_cast<double(*)[H1 / 4]>(&z[0]);
+      rs_step<0xB1, H1 / 8>(w, (lr & 1) != 0);
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) ps[i] = t.pfirst ? x[i] : ps[i] + x[i];
+    for (int i = 0; i < RW / 2; ++i) ps[i] = t.pfirst ? x[i] : ps[i] + x[i];
     if (!t.plast) return;
-    const int mm = lr >> 2, gg = lr & 3;
-    const int rl = 32 * mm + 2 * (lg + 4 * gg);  // realization of (tile 2mm, register gg); rl + 1: tile 2mm + 1
     // non-temporal, as the block's own stores: the partials are read back by k_part_reduce from HBM, and
     // L2-allocating them would evict the grid rows the next chunks re-read
-    __builtin_nontemporal_store(dbl2{ps[0], ps[1]}, (dbl2*)(pp + 2 * rl));
-    __builtin_nontemporal_store(dbl2{ps[2], ps[3]}, (dbl2*)(pp + 2 * rl + 2));
+    if constexpr (RW == 8) {
+      const int mm = lr >> 2, gg = lr & 3;
+      const int rl = 32 * mm + 2 * (lg + 4 * gg);  // realization of (tile 2mm, register gg); rl + 1: tile 2mm + 1
+      __builtin_nontemporal_store(dbl2{ps[0], ps[1]}, (dbl2*)(pp + 2 * rl));
+      __builtin_nontemporal_store(dbl2{ps[2], ps[3]}, (dbl2*)(pp + 2 * rl + 2));
+    } else {
+      const int h = lr & 1, mg = lr >> 1;
+      const int rl = 32 * (mg >> 2) + 2 * (lg + 4 * (mg & 3)) + h;
+      __builtin_nontemporal_store(dbl2{ps[0], ps[1]}, (dbl2*)(pp + 2 * rl));
+    }
   }
 }
 
@@ -638,7 +647,7 @@ __device__ __forceinline__ void interp_store_rows(const SynthArgs& a, double* __
 // The tile's epilogue: its block rows, then (FPTA_OPT_FUSE_CHECKSUMS) its partial checksums.
 template <bool PART, int RW, int PACE = 0>
 __device__ __forceinline__ void interp_store(const SynthArgs& a, double* __restrict__ out, const InterpTile<RW>& t,
-                                             const d4 (&acc)[2][RW], double (&ps)[4]) {
+                                             const d4 (&acc)[2][RW], double (&ps)[RW / 2]) {
   interp_store_rows<RW, PACE>(a, out, t, acc);
   if constexpr (PART) interp_partials<RW>(a, t, acc, ps);
 }
@@ -646,26 +655,38 @@ __device__ __forceinline__ void interp_store(const SynthArgs& a, double* __restr
 template <bool PART, int RW, int PACE = 0>
 __device__ __forceinline__ void interp_store(const SynthArgs& a, double* __restrict__ out, const InterpTile<RW>& t,
                                              const d4 (&acc)[2][RW]) {
-  double ps[4];
+  double ps[RW / 2];
   interp_store<PART, RW, PACE>(a, out, t, acc, ps);
 }
 
-// Tile walk of the persistent interpolation kernels. Work item = (group of G consecutive chunks, realization block),
-// items chunk-group-major (the realization blocks of a group run side by side on one XCD and share its weights and
-// grid rows in L2); a wave takes its item's chunks in order. G = SynthArgs::part_group for fused partial checksums,
-// else 1 (item = chunk x realization block).
+// Tile walk of the persistent interpolation kernels. Work item = (partial group, realization block), items
+// group-major (the realization blocks of a group run side by side on one XCD and share its weights and grid rows in
+// L2); a wave takes its item's chunks in order. Groups come from GridBand::pgfirst for fused partial checksums (PART),
+// else a group is one chunk (item = chunk x realization block). Every field is wave-uniform.
 struct TileWalk {
-  int item, k;
-  __device__ __forceinline__ int group(int n_rb) const { return item / n_rb; }
-  __device__ __forceinline__ int chunk(int n_rb, int G) const { return (item / n_rb) * G + k; }
-  // the current tile's chunk ends its group
-  __device__ __forceinline__ bool last(int n_rb, int G, int n_chunks) const {
-    return k + 1 == G || chunk(n_rb, G) + 1 == n_chunks;
+  int item, k, c0, c1;  // work item; chunk c0 + k of its group's chunks [c0, c1)
+  template <bool PART>
+  __device__ __forceinline__ void start(const GridBand& band, int n_rb, int end) {
+    k = 0;
+    if (item >= end) return;
+    const int g = item / n_rb;
+    if constexpr (PART) {
+      c0 = ld_uniform(band.pgfirst + g);
+      c1 = ld_uniform(band.pgfirst + g + 1);
+    } else {
+      c0 = g;
+      c1 = g + 1;
+    }
   }
-  __device__ __forceinline__ void next(int n_rb, int G, int n_chunks, int stride) {
-    if (last(n_rb, G, n_chunks)) {
+  __device__ __forceinline__ int group(int n_rb) const { return item / n_rb; }
+  __device__ __forceinline__ int chunk() const { return c0 + k; }
+  __device__ __forceinline__ bool first() const { return k == 0; }
+  __device__ __forceinline__ bool last() const { return c0 + k + 1 >= c1; }  // the tile's chunk ends its group
+  template <bool PART>
+  __device__ __forceinline__ void next(const GridBand& band, int n_rb, int stride, int end) {
+    if (last()) {
       item += stride;
-      k = 0;
+      start<PART>(band, n_rb, end);
     } else {
       ++k;
     }
@@ -684,8 +705,7 @@ __global__ __launch_bounds__(256, FPTA_INTERP_WPC) void k_grid_interp_mfma(Synth
   static_assert(RW % 2 == 0, "realization tiles come in pairs");
   static_assert(kGridTT == 32, "two 16-TOA B-tiles per chunk");
   constexpr int NP = RW / 2;
-  // n_tiles: work items (TileWalk), chunk groups x realization blocks
-  const int G = PART ? a.part_group : 1;
+  // n_tiles: work items (TileWalk), partial groups (or chunks) x realization blocks
   const int n_rb = (R_pad + 64 * RW - 1) / (64 * RW);
   const int per = (n_tiles + 7) >> 3;
   const int x = blockIdx.x & 7;
@@ -699,11 +719,11 @@ __global__ __launch_bounds__(256, FPTA_INTERP_WPC) void k_grid_interp_mfma(Synth
     // chunk-(group-)major tiles: the realization blocks of one chunk are consecutive tiles, so they run together on
     // one XCD and the chunk's weights are read from HBM once (realization-block-major read them once per block)
     const int grp = __builtin_amdgcn_readfirstlane(tw.group(n_rb));
-    t.c = __builtin_amdgcn_readfirstlane(grp * G + tw.k);
+    t.c = __builtin_amdgcn_readfirstlane(tw.chunk());
     const int rb = __builtin_amdgcn_readfirstlane(tw.item - grp * n_rb);  // realization block of 64 RW
     t.pg = grp;
-    t.pfirst = tw.k == 0;
-    t.plast = tw.last(n_rb, G, band.n_chunks);
+    t.pfirst = tw.first();
+    t.plast = tw.last();
     t.r0 = (rb * 4 + wave) * 16 * RW;
     const int4 ci = band.chunks[t.c];
     t.p = __builtin_amdgcn_readfirstlane(ci.x);
@@ -743,8 +763,9 @@ __global__ __launch_bounds__(256, FPTA_INTERP_WPC) void k_grid_interp_mfma(Synth
     }
   };
 
-  TileWalk tw{x * per + (int)(blockIdx.x >> 3), 0};
+  TileWalk tw{x * per + (int)(blockIdx.x >> 3)};
   if (tw.item >= end) return;
+  tw.start<PART>(band, n_rb, end);
   InterpTile<RW> cur;
   setup(tw, cur);
   FPTA_DCHECK(R_pad % (16 * RW) == 0, "k_grid_interp_mfma realization padding", R_pad % (16 * RW), 1);
@@ -796,13 +817,13 @@ __global__ __launch_bounds__(256, FPTA_INTERP_WPC) void k_grid_interp_mfma(Synth
         interp_white<RW>(a, cur, acc);
         interp_store<PART, RW>(a, out, cur, acc, ps);
       }
-      tw.next(n_rb, G, band.n_chunks, stride);
+      tw.next<PART>(band, n_rb, stride, end);
       if (tw.item >= end) break;
       setup(tw, cur);
       prefetch(cur);
     } else {
       // next tile: its first steps are in flight before this tile's stores enter the vmcnt queue
-      tw.next(n_rb, G, band.n_chunks, stride);
+      tw.next<PART>(band, n_rb, stride, end);
       const bool more = tw.item < end;
       InterpTile<RW> nxt = cur;
       if (more) {
@@ -877,7 +898,7 @@ __global__ __launch_bounds__(512, 1) void k_grid_interp_ws(SynthArgs a, GridBand
   const int end = min(n_tiles, (x + 1) * per);
   const int first = x * per + (int)(blockIdx.x >> 3);
   const int n_rb = (R_pad + 511) / 512;
-  const int G = PART ? a.part_group : 1;  // n_tiles: work items (TileWalk)
+  // n_tiles: work items (TileWalk)
   const bool producer = wave >= 4;
   const int w = wave & 3;  // compute wave w, or the producer serving it
   if (first >= end) return;  // no tile: every wave of the workgroup leaves (no barrier issued)
@@ -885,11 +906,12 @@ __global__ __launch_bounds__(512, 1) void k_grid_interp_ws(SynthArgs a, GridBand
   if (producer) {
     // cursor of the step the producer loads next: tile, step q of nq, chunk, realization base. Everything it
     // reads besides the operands is wave-uniform (scalar loads), so its vmcnt counts the ring loads alone.
-    TileWalk tw{first, 0};
+    TileWalk tw{first};
+    tw.start<PART>(band, n_rb, end);
     int q = 0, nq = 0, c = 0, r0 = 0;
     auto setup = [&]() {
       const int grp = __builtin_amdgcn_readfirstlane(tw.group(n_rb));
-      c = __builtin_amdgcn_readfirstlane(grp * G + tw.k);
+      c = __builtin_amdgcn_readfirstlane(tw.chunk());
       const int rb = __builtin_amdgcn_readfirstlane(tw.item - grp * n_rb);
       r0 = rb * 512 + w * 128;
       if (r0 >= R_pad) r0 = 0;  // a compute wave past R_pad: valid rows, its sums are never stored
@@ -916,7 +938,7 @@ __global__ __launch_bounds__(512, 1) void k_grid_interp_ws(SynthArgs a, GridBand
       ++issued;
       if (++q == nq) {
         q = 0;
-        tw.next(n_rb, G, band.n_chunks, stride);
+        tw.next<PART>(band, n_rb, stride, end);
         valid = tw.item < end;
         if (valid) setup();
       }
@@ -965,14 +987,15 @@ __global__ __launch_bounds__(512, 1) void k_grid_interp_ws(SynthArgs a, GridBand
   read(0, a0, b0);
   ws_wait_lgkm0();
   int S = 0;
-  for (TileWalk tw{first, 0}; tw.item < end; tw.next(n_rb, G, band.n_chunks, stride)) {
+  TileWalk tw{first};
+  for (tw.start<PART>(band, n_rb, end); tw.item < end; tw.next<PART>(band, n_rb, stride, end)) {
     InterpTile<RW> t;
     const int grp = __builtin_amdgcn_readfirstlane(tw.group(n_rb));
-    t.c = __builtin_amdgcn_readfirstlane(grp * G + tw.k);
+    t.c = __builtin_amdgcn_readfirstlane(tw.chunk());
     const int rb = __builtin_amdgcn_readfirstlane(tw.item - grp * n_rb);
     t.pg = grp;
-    t.pfirst = tw.k == 0;
-    t.plast = tw.last(n_rb, G, band.n_chunks);
+    t.pfirst = tw.first();
+    t.plast = tw.last();
     t.r0 = rb * 512 + w * 128;
     const int4 ci = ld_uniform4(band.chunks + t.c);
     t.p = __builtin_amdgcn_readfirstlane(ci.x);
@@ -1146,10 +1169,9 @@ hipError_t launch_grid_interp_ws(hipStream_t st, const SynthArgs& a, const GridB
   if (band.n_chunks <= 0 || band.vmax < 4 || band.vmax % 4 != 0 || band.vmax > kGridVMax || R_pad % 128 != 0 ||
       a.w_on || a.accumulate)
     return hipErrorInvalidValue;
-  if (a.part && (a.part_group < 1 || a.part_group > kPartGroupMax)) return hipErrorInvalidValue;
+  if (a.part && (!band.pgfirst || band.n_pg <= 0)) return hipErrorInvalidValue;
   const int32_t n_rb = (R_pad + 511) / 512;
-  const int32_t G = a.part ? a.part_group : 1;
-  const int64_t tiles = (int64_t)((band.n_chunks + G - 1) / G) * n_rb;  // work items (TileWalk)
+  const int64_t tiles = (int64_t)(a.part ? band.n_pg : band.n_chunks) * n_rb;  // work items (TileWalk)
   if (tiles > 0x7FFFFFFF) return hipErrorInvalidValue;
   static int n_cu = 0;
   if (!n_cu) {
@@ -1173,6 +1195,192 @@ hipError_t launch_grid_interp_ws(hipStream_t st, const SynthArgs& a, const GridB
   else
     hipLaunchKernelGGL(k_grid_interp_ws<false>, dim3((unsigned)grid), dim3(512), 0, st, a, band, (int32_t)tiles, R_pad,
                        a.out);
+  return hipGetLastError();
+}
+
+// ----------------------------------------------------------------------------- k_grid_interp_psr
+// Layouts with one small grid signal (C3: the common GWB, nf = 124 grid points per pulsar): a workgroup owns one
+// pulsar x 64 realizations, makes that pulsar's grid in LDS and interpolates every chunk of the pulsar from it. No grid
+// buffer: the DFT launch (which could not co-run beside the 247-VGPR fused-checksum interpolation and followed it) and
+// the grid's HBM round trip (0.41 GB written and read back per C3 batch) are gone.
+//  1. wave w, realizations r0 + 16 w + lr: the quarter-range DFT of k_grid_dft_mfma (one 32-row block: nf <= 124) with
+//     the same MFMA k-steps per parity (B = one realization's (cos, sin) coefficients per lane instead of a tile pair)
+//     and the same butterfly into LDS rows j, H + j, H - j, nf - j: the grid values are k_grid_dft_mfma's, bit for bit;
+//  2. one barrier; wave w takes the pulsar's partial groups w, w + 4, ... (chunks without partial checksums) and runs
+//     k_grid_interp_mfma's MFMA steps at RW = 4 (64 realizations): A = two ds_read_b128 of a grid row, B = weights
+//     from global memory, the next chunk's loaded before this chunk's stores; its grid-row indices come by scalar loads.
+// The same operands in the same order as the two-kernel path: blocks and partial checksums are bit-identical to it.
+constexpr int kPsrPitch = 66;   // doubles per LDS grid row: 64 realizations + 16 B (row starts 4 banks apart)
+constexpr int kPsrMaxNf = 124;  // one quarter-range DFT block of 32 rows
+template <bool PART, int NQ>
+__global__ __launch_bounds__(256, 2) void k_grid_interp_psr(SynthArgs a, GridBand band, GridSegDev gs,
+                                                            const int32_t* __restrict__ psr_grp, int32_t n_rb,
+                                                            int32_t n_items, int32_t R_pad, double* __restrict__ out) {
+  constexpr int RW = 4;
+  extern __shared__ __attribute__((aligned(16))) double glds[];  // [nf][kPsrPitch]
+  const int per = (n_items + 7) >> 3;
+  const int item = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);  // a pulsar's blocks on one XCD
+  if (item >= n_items) return;  // the whole workgroup, before its barrier
+  const int p = item / n_rb, rb = item - p * n_rb;
+  const int r0 = rb * 64;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int lr = lane & 15, lg = lane >> 4;
+  const int nf = gs.nf;
+  {
+    // 1. grid rows of pulsar p, realizations r0 + 16 wave + lr
+    d4 C[2][2], S[2][2];  // [parity: 0 odd k, 1 even k][row tile h: rows 2 i + h]
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) C[q][h] = S[q][h] = d4{0.0, 0.0, 0.0, 0.0};
+    const double* __restrict__ cb = a.coef + ((int64_t)p * a.K + gs.col0) * R_pad + r0 + 16 * wave + lr;
+    const double* __restrict__ t0 = gs.tq + (int64_t)lg * gs.ldq + 2 * lr;
+    const int64_t tstride = (int64_t)gs.ntq * gs.ldq;
+#pragma unroll
+    for (int par = 0; par < 2; ++par) {
+      const int n = par ? gs.nm >> 1 : (gs.nm + 1) >> 1;
+      const double* __restrict__ tc = t0 + 2 * par * tstride;
+      const double* __restrict__ ts = tc + tstride;
+      const int nq = ((n + 7) >> 3) << 1;
+      for (int q = 0; q < nq; ++q) {
+        const int m = 2 * min(4 * q + lg, n - 1) + par;  // clamped: a finite coefficient against a zero table row
+        const double bc = cb[(int64_t)(2 * m) * R_pad], bs = cb[(int64_t)(2 * m + 1) * R_pad];
+        const dbl2 ac = *(const dbl2*)(tc + (int64_t)(4 * q) * gs.ldq), as = *(const dbl2*)(ts + (int64_t)(4 * q) * gs.ldq);
+        C[par][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(ac.x, bc, C[par][0], 0, 0, 0);
+        C[par][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(ac.y, bc, C[par][1], 0, 0, 0);
+        S[par][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(as.x, bs, S[par][0], 0, 0, 0);
+        S[par][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(as.y, bs, S[par][1], 0, 0, 0);
+      }
+    }
+    const int Q = nf >> 2, H = nf >> 1;
+    double* __restrict__ gcol = glds + 16 * wave + lr;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int j = 2 * (lg + 4 * g) + h;
+        if (j > Q) continue;
+        const double oc = C[0][h][g], os = S[0][h][g], ec = C[1][h][g], es = S[1][h][g];
+        const double pe = ec + es, me = ec - es, po = oc + os, mo = oc - os;
+        gcol[j * kPsrPitch] = pe + po;
+        gcol[(H + j) * kPsrPitch] = pe - po;
+        if (j > 0 && j < Q) {
+          gcol[(H - j) * kPsrPitch] = me - mo;
+          gcol[(nf - j) * kPsrPitch] = me + mo;
+        }
+      }
+  }
+  __syncthreads();
+  // 2. the pulsar's chunks; a wave's sequence: groups g0 + wave, g0 + wave + 4, ..., each group's chunks in order
+  const int g1 = ld_uniform(psr_grp + p + 1);
+  int g = ld_uniform(psr_grp + p) + wave;
+  if (g >= g1) return;
+  auto group_chunks = [&](int gg, int& c0, int& c1) {
+    if constexpr (PART) {
+      c0 = ld_uniform(band.pgfirst + gg);
+      c1 = ld_uniform(band.pgfirst + gg + 1);
+    } else {
+      c0 = gg;
+      c1 = gg + 1;
+    }
+  };
+  const int rowbase = p * nf;  // grid-buffer row of the pulsar's first grid point (one grid signal: rowoff 0)
+  struct Ops {
+    int4 ci;
+    int nq;
+    dbl2 b[NQ];
+    int row[NQ];  // LDS row of band row 4 q + lg
+  };
+  auto load = [&](int c, Ops& o) {
+    o.ci = ld_uniform4(band.chunks + c);
+    o.nq = __builtin_amdgcn_readfirstlane(o.ci.w) >> 2;
+    FPTA_DCHECK(o.nq <= NQ && o.nq > 0, "k_grid_interp_psr band steps", o.nq, NQ + 1);
+    const int32_t* __restrict__ rt = band.rows + (int64_t)c * band.vmax;
+    const double* __restrict__ wp = band.wd + ((int64_t)c * band.vmax + lg) * kGridTT + 2 * lr;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const int qq = min(q, o.nq - 1);  // steps past nq re-load the last one (never used)
+      const int4 r4 = ld_uniform4(rt + 4 * qq);
+      o.row[q] = (lg == 0 ? r4.x : lg == 1 ? r4.y : lg == 2 ? r4.z : r4.w) - rowbase;
+      FPTA_DCHECK(o.row[q] >= 0 && o.row[q] < nf, "k_grid_interp_psr grid row", o.row[q], nf);
+      o.b[q] = *(const dbl2*)(wp + 4 * kGridTT * qq);
+    }
+  };
+  int c0, c1;
+  group_chunks(g, c0, c1);
+  int c = c0;
+  Ops cur, nxt;
+  load(c, cur);
+  double ps[RW / 2];
+  d4 acc[2][RW];
+  while (true) {
+#pragma unroll
+    for (int e = 0; e < 2; ++e)
+#pragma unroll
+      for (int i = 0; i < RW; ++i) acc[e][i] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      if (q < cur.nq) {
+        const double* __restrict__ gr = glds + cur.row[q] * kPsrPitch + 2 * lr;
+        const dbl2 av0 = *(const dbl2*)gr, av1 = *(const dbl2*)(gr + 32);
+        const dbl2 bv = cur.b[q];
+        acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(av0.x, bv.x, acc[0][0], 0, 0, 0);
+        acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(av0.y, bv.x, acc[0][1], 0, 0, 0);
+        acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(av0.x, bv.y, acc[1][0], 0, 0, 0);
+        acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(av0.y, bv.y, acc[1][1], 0, 0, 0);
+        acc[0][2] = __builtin_amdgcn_mfma_f64_16x16x4f64(av1.x, bv.x, acc[0][2], 0, 0, 0);
+        acc[0][3] = __builtin_amdgcn_mfma_f64_16x16x4f64(av1.y, bv.x, acc[0][3], 0, 0, 0);
+        acc[1][2] = __builtin_amdgcn_mfma_f64_16x16x4f64(av1.x, bv.y, acc[1][2], 0, 0, 0);
+        acc[1][3] = __builtin_amdgcn_mfma_f64_16x16x4f64(av1.y, bv.y, acc[1][3], 0, 0, 0);
+      }
+    }
+    InterpTile<RW> t;
+    t.c = c;
+    t.p = p;
+    t.r0 = r0;
+    t.y = cur.ci.y;
+    t.cnt = cur.ci.z;
+    t.nq = cur.nq;
+    t.pg = g;
+    t.pfirst = c == c0;
+    t.plast = c + 1 == c1;
+    // next chunk: its operands are in flight before this chunk's stores enter the vmcnt queue
+    bool more = true;
+    if (c + 1 < c1) {
+      ++c;
+    } else {
+      g += 4;
+      more = g < g1;
+      if (more) {
+        group_chunks(g, c0, c1);
+        c = c0;
+      }
+    }
+    if (more) load(c, nxt);
+    __builtin_amdgcn_sched_barrier(0);
+    interp_store<PART, RW>(a, out, t, acc, ps);
+    if (!more) break;
+    cur = nxt;
+  }
+}
+
+hipError_t launch_grid_interp_psr(hipStream_t st, const SynthArgs& a, const GridBand& band, const GridSegDev& gs,
+                                  const int32_t* psr_grp, int32_t P, int32_t R_pad) {
+  if (band.n_chunks <= 0 || band.vmax < 4 || band.vmax % 4 != 0 || band.vmax > 32 || R_pad % 64 != 0 || a.w_on ||
+      gs.nf > kPsrMaxNf || gs.nf < 4 || gs.nf % 4 != 0 || gs.ldq != kGridDftRows || gs.nm <= 0 || !psr_grp ||
+      (a.part && (!band.pgfirst || band.n_pg <= 0)))
+    return hipErrorInvalidValue;
+  const int32_t n_rb = R_pad / 64;
+  const int64_t items = (int64_t)P * n_rb;
+  if (items > 0x7FFFFFFF) return hipErrorInvalidValue;
+  const int64_t grid = (items + 7) / 8 * 8;
+  const size_t lds = sizeof(double) * (size_t)gs.nf * kPsrPitch;
+  const bool small = band.vmax <= 16;
+  auto kernel = a.part ? (small ? k_grid_interp_psr<true, 4> : k_grid_interp_psr<true, 8>)
+                       : (small ? k_grid_interp_psr<false, 4> : k_grid_interp_psr<false, 8>);
+  hipLaunchKernelGGL(kernel, dim3((unsigned)grid), dim3(256), lds, st, a, band, gs, psr_grp, n_rb, (int32_t)items,
+                     R_pad, a.out);
   return hipGetLastError();
 }
 
@@ -1202,10 +1410,9 @@ hipError_t launch_grid_interp_mfma(hipStream_t st, const SynthArgs& a, const Gri
   constexpr int RW = kInterpRW;
   if (band.n_chunks <= 0 || band.vmax < 4 || band.vmax % 4 != 0 || R_pad % (16 * RW) != 0)
     return hipErrorInvalidValue;
-  if (a.part && (a.part_group < 1 || a.part_group > kPartGroupMax)) return hipErrorInvalidValue;
+  if (a.part && (!band.pgfirst || band.n_pg <= 0)) return hipErrorInvalidValue;
   const int32_t n_rb = (R_pad + 64 * RW - 1) / (64 * RW);
-  const int32_t G = a.part ? a.part_group : 1;
-  const int64_t tiles = (int64_t)((band.n_chunks + G - 1) / G) * n_rb;  // work items (TileWalk)
+  const int64_t tiles = (int64_t)(a.part ? band.n_pg : band.n_chunks) * n_rb;  // work items (TileWalk)
   if (tiles > 0x7FFFFFFF) return hipErrorInvalidValue;
   static int n_cu = 0;
   if (!n_cu) {

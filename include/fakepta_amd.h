@@ -211,7 +211,8 @@ int fpta_batch_info(fpta_ctx* ctx, int64_t* info);
  * out[12] grid signals of the plan (signals after FPTA_OPT_GRID_COALESCE), out[13] layout signals, out[14]
  * mean band rows per chunk (all grid signals, padded to 4), out[15] the interpolation kernel of the last gridded
  * block: 0 none, else 1 + 4 kind + 2 (white / ECORR epilogue) + (fused partial checksums), kind 0
- * k_grid_interp_mfma, 1 k_grid_interp_ws, 2 k_grid_interp_ws2, 3 k_grid_interp_lds, 4 k_grid_interp_st.
+ * k_grid_interp_mfma, 1 k_grid_interp_ws, 2 k_grid_interp_ws2, 3 k_grid_interp_lds, 4 k_grid_interp_st, 5
+ * k_grid_interp_u, 6 / 7 k_grid_interp_psr with 4 / 8 band steps.
  * fpta_batch_grid_info_n writes the first min(n_out, FPTA_GRID_INFO_LEN) values and returns FPTA_GRID_INFO_LEN
  * (negative on error); fpta_batch_grid_info keeps the round-1 contract: out[0..8], host double[9]. */
 #define FPTA_GRID_INFO_LEN 16
@@ -342,6 +343,12 @@ int fpta_comm_gather(fpta_comm* comm, const double* send, int64_t count, double*
                                      and writes one {sum, sum of squares} row per group; the reduction then sums the
                                      groups in order. Deterministic and batch-split invariant for every value; the
                                      value changes the order of the additions (checksums agree to rounding). */
+#define FPTA_OPT_INTERP_PSR 21    /* gridded path with one grid signal of <= 124 grid points whose coefficients the MFMA
+                                     DFT would read from the coefficient buffer (e.g. C3's common GWB), <= 32 band
+                                     rows and no fused white noise: 1 (default) k_grid_interp_psr (a workgroup makes
+                                     one pulsar's grid for 64 realizations in LDS and interpolates the pulsar's chunks
+                                     from it: no grid buffer, no separate DFT launch; pipelined blocks alternate two
+                                     coefficient buffers); 0 the DFT + interpolation kernels. Results are identical. */
 int fpta_set_option(fpta_ctx* ctx, int32_t key, int64_t value);
 /* Current value of option `key` (same keys as fpta_set_option). */
 int fpta_get_option(fpta_ctx* ctx, int32_t key, int64_t* value);

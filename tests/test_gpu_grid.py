@@ -683,3 +683,109 @@ def test_gen_mix_matches_two_kernels(ctx, capi, shipped, factor):
                 assert_parity(res[1], O.batch_synth(offs, toas, nu, segs, 17, 40, 300), TOL)
         finally:
             ctx.set_options(shipped)
+
+
+@pytest.mark.parametrize("case", ["common", "common_short", "per_psr", "modes40"])
+@pytest.mark.parametrize("fuse,pgroup", [(0, 16), (1, 1), (1, 16)])
+@pytest.mark.parametrize("R", [333, 1100])
+def test_psr_interpolation_is_bitwise_identical(ctx, capi, shipped, case, fuse, pgroup, R):
+    """FPTA_OPT_INTERP_PSR (k_grid_interp_psr: a workgroup makes one pulsar's grid for 64 realizations in LDS with
+    k_grid_dft_mfma's MFMA steps and butterfly, then interpolates the pulsar's chunks from it) returns the two-kernel
+    path's block and partial checksums bit for bit: a common 30-mode GWB on ragged pulsars (C3-like; one pulsar of a
+    single short chunk in "common_short"), a per-pulsar red noise drawn into the coefficient buffer (FPTA_OPT_DFT_GEN
+    0), and 40 modes (nf = 124, the largest one-block grid); partial rows of 1 and 16 chunks; every sample written
+    (NaN-poisoned block); the kernel that ran is the per-pulsar one."""
+    rng = np.random.default_rng(83 + len(case))
+    # dense TOAs (bands of <= 32 rows: a 32-TOA chunk spans a few grid cells), ragged counts
+    offs, toas, nu = random_layout(rng, 13, (700, 2100))
+    if case == "common_short":  # plus a pulsar of 5 TOAs within a day: one short chunk
+        offs = np.append(offs, offs[-1] + 5)
+        toas = np.concatenate([toas, 2e8 + np.sort(rng.uniform(0, 86400.0, 5))])
+        nu = np.concatenate([nu, np.full(5, 1400.0)])
+    ctx.batch_set_toas(offs, toas, nu)
+    if case == "per_psr":
+        f, a = per_psr_signal(rng, offs, toas, 30)
+        ctx.batch_add_signal(0, f, a, idx=0.0)
+    else:
+        f, a, L, _ = common_signal(rng, offs, toas, 40 if case == "modes40" else 30)
+        ctx.batch_add_signal(1, f, a, L=L)
+    try:
+        ctx.set_option(capi.OPT_SYNTH_PATH, 4)
+        ctx.set_option(capi.OPT_DFT_GEN, 0 if case == "per_psr" else 1)
+        ctx.set_option(capi.OPT_FUSE_CHECKSUMS, fuse)
+        ctx.set_option(capi.OPT_PART_GROUP, pgroup)
+        res = {}
+        for psr in (0, 1):
+            ctx.set_option(capi.OPT_INTERP_PSR, psr)
+            ctx.batch_synth(7, 0, R, to_host=False)
+            ctx.debug_fill_out(np.nan)
+            res[psr] = (ctx.batch_synth(7, 64, R), ctx.batch_checksums())
+            name = ctx.batch_grid_info()["interp_kernel"]
+            assert name.startswith("k_grid_interp_psr") == bool(psr), name
+        assert np.all(np.isfinite(res[1][0]))
+        np.testing.assert_array_equal(res[0][0], res[1][0])
+        np.testing.assert_array_equal(res[0][1], res[1][1])
+    finally:
+        ctx.set_options(shipped)
+
+
+def test_psr_interpolation_not_taken_outside_its_layouts(ctx, capi, shipped):
+    """k_grid_interp_psr serves one grid signal of <= 124 grid points without fused white noise: 60 modes (nf > 124),
+    two grid signals and a white-noise block take the other kernels."""
+    rng = np.random.default_rng(89)
+    offs, toas, nu = random_layout(rng, 12, (100, 300))
+    try:
+        ctx.set_option(capi.OPT_SYNTH_PATH, 4)
+        for case in ("modes60", "two", "white"):
+            ctx.batch_clear()
+            ctx.batch_set_toas(offs, toas, nu)
+            f, a, L, _ = common_signal(rng, offs, toas, 60 if case == "modes60" else 30)
+            ctx.batch_add_signal(1, f, a, L=L)
+            if case == "two":
+                f2, a2 = per_psr_signal(rng, offs, toas, 100)
+                ctx.batch_add_signal(0, f2, a2, idx=2.0)
+            if case == "white":
+                ctx.batch_set_white(np.full(offs[-1], 1e-7), [], [])
+            ctx.batch_synth(3, 0, 256, to_host=False)
+            assert not ctx.batch_grid_info()["interp_kernel"].startswith("k_grid_interp_psr"), case
+            ctx.batch_set_white()
+    finally:
+        ctx.batch_clear()
+        ctx.set_options(shipped)
+
+
+@pytest.mark.parametrize("fuse", [0, 1])
+def test_psr_pipelined_batches_are_bitwise_identical(ctx, capi, shipped, fuse):
+    """Pipelined per-pulsar blocks (two coefficient buffers: block b + 1 draws into one while block b's interpolation
+    reads the other): the checksums of 7 back-to-back blocks equal the single-stream and the two-kernel ones bit for
+    bit, and so do they when the layout switches between a per-pulsar and a two-signal plan on one context."""
+    rng = np.random.default_rng(97)
+    offs, toas, nu = random_layout(rng, 30, (600, 1500))
+    f, a, L, _ = common_signal(rng, offs, toas, 30)
+    f2, a2 = per_psr_signal(rng, offs, toas, 100)
+
+    def layout(two):
+        ctx.batch_clear()
+        ctx.batch_set_toas(offs, toas, nu)
+        ctx.batch_add_signal(1, f, a, L=L)
+        if two:
+            ctx.batch_add_signal(0, f2, a2, idx=2.0)
+        ctx.set_option(capi.OPT_SYNTH_PATH, 4)
+
+    try:
+        ctx.set_option(capi.OPT_FUSE_CHECKSUMS, fuse)
+        res = {}
+        for psr, ov in ((0, 0), (1, 0), (1, 1), (0, 1)):
+            ctx.set_option(capi.OPT_INTERP_PSR, psr)
+            ctx.set_option(capi.OPT_OVERLAP, ov)
+            out = []
+            for two in (False, True, False):
+                layout(two)
+                out.append(ctx.batch_synth_checksums(13, 5, 7 * 256 - 3, batch=256))
+            res[psr, ov] = out
+        for key in ((1, 0), (1, 1), (0, 1)):
+            for x, y in zip(res[0, 0], res[key]):
+                np.testing.assert_array_equal(x, y)
+    finally:
+        ctx.batch_clear()
+        ctx.set_options(shipped)
