@@ -717,8 +717,11 @@ int run_coefficients(fpta_ctx* c, Layout& L, uint64_t seed, int64_t real0, int32
     if (in_fused[i] && d.kind == 0) continue;  // drawn inside its grid signal's DFT
     if (d.kind == 1 && c->gen_mix && mfma_mix && !zin && !x_out && fuse_into[i] < 0 && P <= kGenMixMaxP) {
       KTimer kt(c, FPTA_K_MIX, st);  // draws + mixing in one kernel, into the signal's own columns
+      // 16-realization workgroups (FPTA_OPT_GEN_MIX 3: they fit in the LDS two k_grid_interp_psr workgroups leave;
+      // C3 measured the same either way, profiles/round4/R5d)
+      const int rb = c->gen_mix == 3 ? 16 : 32;
       HIPCHK(c, launch_gen_mix(st, d, (int32_t)i, P, R, R_pad, real0, k0, k1, c->coef.as<double>(), L.K,
-                               c->gen_mix == 2 ? 1 : 2),
+                               c->gen_mix == 1 ? 2 : 1, rb),
              "k_gen_mix launch");
     } else {
     {
@@ -1940,7 +1943,7 @@ int fpta_set_option(fpta_ctx* c, int32_t key, int64_t value) {
       c->dft_gen = value ? 1 : 0;
       return FPTA_OK;
     case FPTA_OPT_GEN_MIX:
-      if (value < 0 || value > 2) return fail(c, FPTA_EINVAL, "gen_mix must be 0 .. 2");
+      if (value < 0 || value > 3) return fail(c, FPTA_EINVAL, "gen_mix must be 0 .. 3");
       c->gen_mix = (int)value;
       return FPTA_OK;
     case FPTA_OPT_ASYNC_SUMS:

@@ -230,7 +230,7 @@ hipError_t launch_mix_mfma(hipStream_t st, const SegDesc& sd, int32_t P, int32_t
 // draw + mixing of a common signal in one kernel (kMixTiledMinP <= P <= kGenMixMaxP): writes the signal's own columns
 constexpr int kGenMixMaxP = 256;
 hipError_t launch_gen_mix(hipStream_t st, const SegDesc& sd, int32_t seg_id, int32_t P, int32_t n_real, int32_t R_pad,
-                          int64_t real0, uint32_t k0, uint32_t k1, double* coef, int32_t K, int rh = 2);
+                          int64_t real0, uint32_t k0, uint32_t k1, double* coef, int32_t K, int rh = 2, int rb = 32);
 hipError_t launch_mix_tiled(hipStream_t st, const SegDesc& sd, int32_t P, int32_t R_pad, const double* zbuf,
                             double* coef, int32_t K, double* x_out);
 hipError_t launch_epoch_normals(hipStream_t st, int64_t n_blocks, int32_t n_real, int64_t real0, uint32_t k0,

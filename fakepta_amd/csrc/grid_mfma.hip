@@ -1548,16 +1548,18 @@ __global__ __launch_bounds__(256, OCC) void k_mix_mfma(const double* __restrict_
 // RH realization tiles of 16 per wave (RH = 2: waves (u, h) over 32 realizations; RH = 1: twice the waves, each on
 // 16 realizations, so a workgroup's draws and MFMA steps spread over 8 waves per 64-pulsar tile pair). The products
 // and their k-step order per coefficient are the same either way.
-template <int RH>
+// RB realizations per workgroup (32, or 16 with RH = 1: a quarter of the LDS, 27 KB at P = 100, FPTA_OPT_GEN_MIX 3)
+template <int RH, int RB>
 __global__ __launch_bounds__(1024) void k_gen_mix(SegDesc sd, int32_t seg_id, int32_t P, int32_t n_real, int32_t R_pad,
                                                   int64_t real0, uint32_t k0, uint32_t k1, double* __restrict__ coef,
                                                   int32_t K) {
-  extern __shared__ __attribute__((aligned(16))) double Zs[];  // [q_pad][64]: cos of 32 realizations, then sin
-  const int n_rb = R_pad >> 5;
-  const int k = blockIdx.x / n_rb, r0 = (blockIdx.x - k * n_rb) * 32;
+  static_assert(RB == 32 || (RB == 16 && RH == 1), "16-realization workgroups: one realization tile per wave");
+  extern __shared__ __attribute__((aligned(16))) double Zs[];  // [q_pad][2 RB]: cos of RB realizations, then sin
+  const int n_rb = R_pad / RB;
+  const int k = blockIdx.x / n_rb, r0 = (blockIdx.x - k * n_rb) * RB;
   const int q_pad = (P + 7) & ~7;  // k-steps of 4 in pairs: the last step may read up to 8 rows past P
-  for (int idx = threadIdx.x; idx < q_pad * 16; idx += blockDim.x) {  // a realization pair per thread and pulsar
-    const int q = idx >> 4, rl = 2 * (idx & 15);
+  for (int idx = threadIdx.x; idx < q_pad * (RB / 2); idx += blockDim.x) {  // a realization pair per thread and pulsar
+    const int q = idx / (RB / 2), rl = 2 * (idx % (RB / 2));
     double z[4] = {0.0, 0.0, 0.0, 0.0};
     const int r = r0 + rl;
     if (q < sd.n_q && r < n_real) {  // columns q >= n_q of L are zero: their normals are never needed
@@ -1570,14 +1572,14 @@ __global__ __launch_bounds__(1024) void k_gen_mix(SegDesc sd, int32_t seg_id, in
       }
       if (r + 1 >= n_real) z[2] = z[3] = 0.0;
     }
-    *(dbl2*)(Zs + q * 64 + rl) = dbl2{z[0], z[2]};
-    *(dbl2*)(Zs + q * 64 + 32 + rl) = dbl2{z[1], z[3]};
+    *(dbl2*)(Zs + q * 2 * RB + rl) = dbl2{z[0], z[2]};
+    *(dbl2*)(Zs + q * 2 * RB + RB + rl) = dbl2{z[1], z[3]};
   }
   __syncthreads();
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const int lr = lane & 15, lg = lane >> 4;
-  constexpr int NRH = 2 / RH;  // realization halves per (u, h)
+  constexpr int NRH = RB / 16 / RH;  // realization tiles of 16 RH per (u, h)
   const int rh = wave % NRH, uh = wave / NRH;
   const int u = uh >> 1, h = uh & 1;  // pulsar tile (64 pulsars), column half (cos / sin)
   const int p0 = 64 * u;
@@ -1589,18 +1591,18 @@ __global__ __launch_bounds__(1024) void k_gen_mix(SegDesc sd, int32_t seg_id, in
     for (int e = 0; e < RH; ++e) acc[i][e] = d4{0.0, 0.0, 0.0, 0.0};
   const double* __restrict__ lt = sd.LT + p0 + 2 * lr;
   // B operand of realization tile e: RH = 2 realizations 2 lr + e (one 16-byte pair); RH = 1 realization 16 rh + lr
-  const double* __restrict__ zb = Zs + 32 * h + (RH == 2 ? 2 * lr : 16 * rh + lr);
+  const double* __restrict__ zb = Zs + RB * h + (RH == 2 ? 2 * lr : 16 * rh + lr);
   auto step = [&](int q0) {
     const int q = q0 + lg;
     const dbl2 a0 = *(const dbl2*)(lt + (int64_t)q * sd.lt_ld);
     const dbl2 a1 = *(const dbl2*)(lt + (int64_t)q * sd.lt_ld + 32);
     double b[RH];
     if constexpr (RH == 2) {
-      const dbl2 bv = *(const dbl2*)(zb + q * 64);
+      const dbl2 bv = *(const dbl2*)(zb + q * 2 * RB);
       b[0] = bv.x;
       b[1] = bv.y;
     } else {
-      b[0] = zb[q * 64];
+      b[0] = zb[q * 2 * RB];
     }
 #pragma unroll
     for (int e = 0; e < RH; ++e) {
@@ -1632,20 +1634,24 @@ __global__ __launch_bounds__(1024) void k_gen_mix(SegDesc sd, int32_t seg_id, in
 }
 
 hipError_t launch_gen_mix(hipStream_t st, const SegDesc& sd, int32_t seg_id, int32_t P, int32_t n_real, int32_t R_pad,
-                          int64_t real0, uint32_t k0, uint32_t k1, double* coef, int32_t K, int rh) {
+                          int64_t real0, uint32_t k0, uint32_t k1, double* coef, int32_t K, int rh, int rb) {
   const int32_t n_pt = (P + 63) / 64;
   if (sd.kind != 1 || !sd.LT || P < 1 || P > kGenMixMaxP || R_pad % 32 != 0 || sd.lt_ld < 64 * n_pt ||
-      sd.lt_rows < ((P + 7) & ~7) || sd.col0 < 0 || sd.col0 + 2 * sd.nm > K || (rh != 1 && rh != 2))
+      sd.lt_rows < ((P + 7) & ~7) || sd.col0 < 0 || sd.col0 + 2 * sd.nm > K || (rh != 1 && rh != 2) ||
+      (rb != 32 && (rb != 16 || rh != 1)))
     return hipErrorInvalidValue;
-  const int64_t blocks = (int64_t)sd.nm * (R_pad / 32);
+  const int64_t blocks = (int64_t)sd.nm * (R_pad / rb);
   if (blocks > 0x7FFFFFFF) return hipErrorInvalidValue;
-  const size_t lds = sizeof(double) * 64 * (size_t)((P + 7) & ~7);
-  if (rh == 2)
-    hipLaunchKernelGGL(k_gen_mix<2>, dim3((unsigned)blocks), dim3(128 * n_pt), lds, st, sd, seg_id, P, n_real, R_pad,
-                       real0, k0, k1, coef, K);
+  const size_t lds = sizeof(double) * 2 * rb * (size_t)((P + 7) & ~7);
+  if (rb == 16)
+    hipLaunchKernelGGL((k_gen_mix<1, 16>), dim3((unsigned)blocks), dim3(128 * n_pt), lds, st, sd, seg_id, P, n_real,
+                       R_pad, real0, k0, k1, coef, K);
+  else if (rh == 2)
+    hipLaunchKernelGGL((k_gen_mix<2, 32>), dim3((unsigned)blocks), dim3(128 * n_pt), lds, st, sd, seg_id, P, n_real,
+                       R_pad, real0, k0, k1, coef, K);
   else
-    hipLaunchKernelGGL(k_gen_mix<1>, dim3((unsigned)blocks), dim3(256 * n_pt), lds, st, sd, seg_id, P, n_real, R_pad,
-                       real0, k0, k1, coef, K);
+    hipLaunchKernelGGL((k_gen_mix<1, 32>), dim3((unsigned)blocks), dim3(256 * n_pt), lds, st, sd, seg_id, P, n_real,
+                       R_pad, real0, k0, k1, coef, K);
   return hipGetLastError();
 }
 

@@ -333,8 +333,10 @@ int fpta_comm_gather(fpta_comm* comm, const double* send, int64_t count, double*
                                      buffer and k_grid_dft_mfma reads them back. Same draws; sums agree to rounding. */
 #define FPTA_OPT_GEN_MIX 18       /* common signals of 64..256 pulsars (fp64 MFMA mixing): 2 (default) draws and ORF
                                      mixing in one kernel (k_gen_mix: normals in LDS, no zbuf round trip), one wave per
-                                     16 realizations; 1 the same kernel with waves of 32 realizations; 0 k_gen then
-                                     k_mix_mfma. Same draws and products; results identical. */
+                                     16 realizations, 32 realizations per workgroup; 3 the same with 16 realizations
+                                     per workgroup (a quarter of the LDS);
+                                     1 waves of 32 realizations; 0 k_gen then k_mix_mfma. Same draws and products;
+                                     results identical. */
 #define FPTA_OPT_ASYNC_SUMS 19    /* streamed jobs (fpta_batch_synth_checksums, fpta_multi_synth): 1 a block's partial
                                      checksums are reduced on a stream of their own, beside the next block, into one
                                      of two partials buffers; 0 (default) on the context stream. Identical results. */

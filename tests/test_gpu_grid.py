@@ -650,7 +650,7 @@ def zlib_crc(s):
 
 @pytest.mark.parametrize("factor", ["cholesky", "svd", "dipole_rank3"])
 def test_gen_mix_matches_two_kernels(ctx, capi, shipped, factor):
-    """k_gen_mix (FPTA_OPT_GEN_MIX 1 and 2) draws a common signal's normals into LDS and mixes them on fp64 MFMA in one
+    """k_gen_mix (FPTA_OPT_GEN_MIX 1, 2 and 3) draws a common signal's normals into LDS and mixes them on fp64 MFMA in one
     kernel: same counters, same products in the same k-step order as k_gen + k_mix_mfma, so blocks are bit-identical
     on the gridded (with and without k_grid_dft_gen) and exact paths, for a triangular (Cholesky) and a dense (SVD)
     ORF factor and the batch path's rank-3 factor of the singular dipole ORF (columns past the third exactly zero:
@@ -675,11 +675,13 @@ def test_gen_mix_matches_two_kernels(ctx, capi, shipped, factor):
                 ctx.set_option(capi.OPT_SYNTH_PATH, path)
                 ctx.set_option(capi.OPT_DFT_GEN, dft_gen)
                 res = {}
-                for gm in (0, 1, 2):  # 2: k_gen_mix with 16-realization waves (twice the waves per workgroup)
+                # 2: k_gen_mix with 16-realization waves (twice the waves per workgroup); 3: and 16-realization
+                # workgroups
+                for gm in (0, 1, 2, 3):
                     ctx.set_option(capi.OPT_GEN_MIX, gm)
                     res[gm] = ctx.batch_synth(17, 40, 300)
-                np.testing.assert_array_equal(res[0], res[1])
-                np.testing.assert_array_equal(res[0], res[2])
+                for gm in (1, 2, 3):
+                    np.testing.assert_array_equal(res[0], res[gm])
                 assert_parity(res[1], O.batch_synth(offs, toas, nu, segs, 17, 40, 300), TOL)
         finally:
             ctx.set_options(shipped)

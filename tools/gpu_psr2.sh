@@ -1,0 +1,10 @@
+#!/bin/bash
+set -o pipefail
+tag=${1:-PSR3}
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out
+o=gpurun_out/$tag
+timeout -k 10 400 python -u -m pytest tests/test_gpu_grid.py tests/test_gpu_c3.py -m gpu -x -v --timeout 120 --timeout-method thread -p no:cacheprovider -k "psr or gen_mix or pipelined or c3 or checksums" > ${o}_tests.log 2>&1 || { grep -E "FAILED|Error|error" ${o}_tests.log | head -20; tail -40 ${o}_tests.log; exit 1; }
+tail -1 ${o}_tests.log
+bash tools/gpu_ab_cfg.sh ${tag} "" c3 "" "GEN_MIX=1" "INTERP_PSR=0" || exit 1
+bash tools/gpu_c3_trace2.sh ${tag}T || exit 1
