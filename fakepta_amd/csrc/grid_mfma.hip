@@ -752,7 +752,7 @@ __global__ __launch_bounds__(256, FPTA_INTERP_WPC) void k_grid_interp_mfma(Synth
     bv = *(const dbl2*)(t.Wp + 4 * kGridTT * qq);
   };
   d4 acc[2][RW];  // [TOA parity][realization tile]
-  double ps[4];   // partial checksums of the chunk group so far (PART)
+  double ps[RW / 2];  // partial checksums of the chunk group so far (PART)
   auto mfma = [&](const dbl2(&av)[NP], const dbl2& bv) {
 #pragma unroll
     for (int m = 0; m < NP; ++m) {
