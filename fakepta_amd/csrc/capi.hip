@@ -94,6 +94,11 @@ struct GridPlan {
   int32_t pg_size = 0, n_pg = 0;
   DevBuf pgfirst, psr_pg;
   DevBuf psr_c0;  // device copy of psr_chunk0 (k_grid_interp_psr without partial checksums)
+  // k_grid_interp_wr plan (GridWindow): <= 2 grid signals, each signal's band rows in a ring of kWrSlots LDS slots by
+  // unwrapped row; per chunk the slot of each band row, and the rows to load: all its band rows (full) or those not in
+  // the previous chunk's band (new; = full and flagged fresh when the two bands do not fit one ring window)
+  bool wr_ok = false;
+  DevBuf wr_meta, wr_list, wr_slot;
   // k_grid_interp_lds plan: groups int4 {first chunk, chunks, union rows U, offset into urows}; urows the grid-
   // buffer rows of each group's union; lrows [n_chunks][vmax] the union slot of each band row
   bool lds_ok = false;
@@ -137,6 +142,7 @@ struct GridPlan {
     g_rpad = 0;
     psr_chunk0.clear();
     pg_size = n_pg = 0;
+    wr_ok = false;
     members.clear();
     anchor.clear();
     last.clear();
@@ -215,6 +221,7 @@ struct fpta_ctx {
   int grid_coalesce = 1;  // gridded path: signals sharing w0 and the chromatic weight share one grid (FPTA_OPT_GRID_COALESCE)
   int part_group = kPartGroup;  // fused partial checksums: consecutive chunks per partial row (FPTA_OPT_PART_GROUP)
   int interp_psr = 1;  // k_grid_interp_psr where the layout allows it (FPTA_OPT_INTERP_PSR)
+  int interp_wr = 0;   // k_grid_interp_wr for plain blocks where the plan allows it (FPTA_OPT_INTERP_WR)
   // pipelined per-pulsar blocks read their coefficients in the interpolation (ctx stream): two coefficient buffers,
   // coef2 the other one; coef_slot = the grid-buffer index whose block owns c->coef; prev_psr: the last pipelined
   // block ran that way (its draws waited for the interpolation two blocks back, not for the whole ctx stream)
@@ -1073,6 +1080,70 @@ int grid_build(fpta_ctx* c, Layout& L) {
       }
     for (; v < vmax; ++v) r[v] = r[0];
   }
+  // k_grid_interp_wr (diagnostic kernel): ring slot kWrSlots s + (unwrapped row mod kWrSlots) per band row; load
+  // lists per chunk
+  std::vector<int4> wr_meta;
+  std::vector<int2> wr_list;
+  std::vector<int32_t> wr_slot;
+#ifdef FPTA_DIAG_KERNELS
+  bool wr_ok = n_seg <= kWrMaxSig && vmax <= kWrVMax;
+#else
+  bool wr_ok = false;
+#endif
+  for (int32_t s = 0; s < n_seg && wr_ok; ++s)
+    for (int32_t ci = 0; ci < n_chunks && wr_ok; ++ci) wr_ok = band_n[s][ci] <= kWrSlots;
+  if (wr_ok) {
+    wr_meta.resize(n_chunks);
+    wr_slot.assign((size_t)n_chunks * vmax, 0);
+    for (int32_t ci = 0; ci < n_chunks; ++ci) {
+      const int32_t p = chunks[ci].x;
+      int32_t* sl = wr_slot.data() + (size_t)ci * vmax;
+      int32_t v = 0;
+      for (int32_t s = 0; s < n_seg; ++s)
+        for (int32_t i = 0; i < band_n[s][ci]; ++i)
+          sl[v++] = kWrSlots * s + (int32_t)((band_lo[s][ci] + i) & (kWrSlots - 1));
+      for (; v < vmax; ++v) sl[v] = sl[0];
+      // the bands of chunks ci - back .. ci (same pulsar) in one ring window per signal: compat (back 1) = only the rows
+      // the previous band does not hold load, after the chunk before has been computed; near (back 2) = they may load
+      // while the chunk two back is computed
+      auto window = [&](int32_t back) {
+        if (ci < back) return false;
+        for (int32_t b = 1; b <= back; ++b)
+          if (chunks[ci - b].x != p) return false;
+        for (int32_t s = 0; s < n_seg; ++s) {
+          int64_t lo = band_lo[s][ci], hi = band_lo[s][ci] + band_n[s][ci];
+          for (int32_t b = 1; b <= back; ++b) {
+            lo = std::min(lo, band_lo[s][ci - b]);
+            hi = std::max(hi, band_lo[s][ci - b] + (int64_t)band_n[s][ci - b]);
+          }
+          if (hi - lo > kWrSlots) return false;
+        }
+        return true;
+      };
+      const bool compat = window(1), near = compat && window(2);
+      auto add_rows = [&](bool only_new) {
+        int32_t n = 0;
+        for (int32_t s = 0; s < n_seg; ++s)
+          for (int32_t i = 0; i < band_n[s][ci]; ++i) {
+            const int64_t u = band_lo[s][ci] + i;
+            if (only_new && u >= band_lo[s][ci - 1] && u < band_lo[s][ci - 1] + band_n[s][ci - 1]) continue;
+            const int64_t j = (u % nf[s] + nf[s]) % nf[s];
+            wr_list.push_back(make_int2(kWrSlots * s + (int32_t)(u & (kWrSlots - 1)),
+                                        (int32_t)(rowoff[s] + (int64_t)p * nf[s] + j)));
+            ++n;
+          }
+        return n;
+      };
+      const int32_t full_off = (int32_t)wr_list.size();
+      const int32_t full_n = add_rows(false);
+      int32_t new_off = full_off, new_n = full_n;
+      if (compat) {
+        new_off = (int32_t)wr_list.size();
+        new_n = add_rows(true);
+      }
+      wr_meta[ci] = make_int4(full_off, full_n, new_off, new_n | (compat ? 0 : kWrFresh) | (near ? 0 : kWrFar));
+    }
+  }
   // LDS-staged interpolation (k_grid_interp_lds): groups of <= kLdsGroup consecutive chunks of one pulsar whose
   // bands, over all signals, unite to <= kLdsRowsMax rows. Per group the union's grid-buffer rows (signal by
   // signal, each signal's rows one contiguous unwrapped range), per chunk the union slot of each band row.
@@ -1203,6 +1274,12 @@ int grid_build(fpta_ctx* c, Layout& L) {
     }
   }
   int rc;
+  G.wr_ok = wr_ok;
+  if (wr_ok && ((rc = upload(c, G.wr_meta, wr_meta.data(), sizeof(int4) * wr_meta.size(), "window plan")) ||
+                (rc = upload(c, G.wr_list, wr_list.data(), sizeof(int2) * std::max<size_t>(wr_list.size(), 1),
+                             "window rows")) ||
+                (rc = upload(c, G.wr_slot, wr_slot.data(), sizeof(int32_t) * wr_slot.size(), "window slots"))))
+    return rc;
   if ((rc = upload(c, G.chunks, chunks.data(), sizeof(int4) * chunks.size(), "grid chunks")) ||
       (rc = upload(c, G.rows, rt.data(), sizeof(int32_t) * rt.size(), "grid band rows")))
     return rc;
@@ -1518,6 +1595,11 @@ int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad, bool pipe = fa
     band.pgfirst = nullptr;
     band.n_pg = G.n_chunks;
     HIPCHK(c, launch_grid_interp_st(c->stream, a, band, R_pad), "k_grid_interp_st launch");
+  } else if (c->interp_wr && G.wr_ok && !c->interp_lds && c->interp_ws > 0 && !a.w_on && !a.accumulate && !a.part &&
+             R_pad % kWrReal == 0 && !psr) {
+    kind = 10;
+    GridWindow wrp{G.wr_meta.as<int4>(), G.wr_list.as<int2>(), G.wr_slot.as<int32_t>()};
+    HIPCHK(c, launch_grid_interp_wr(c->stream, a, band, wrp, R_pad), "k_grid_interp_wr launch");
 #endif
   } else if (psr) {
     kind = G.vmax <= 16 ? 6 : 7;  // launch_grid_interp_psr: NQ = 4 or 8 band steps
@@ -1956,6 +2038,12 @@ int fpta_set_option(fpta_ctx* c, int32_t key, int64_t value) {
     case FPTA_OPT_INTERP_PSR:
       c->interp_psr = value ? 1 : 0;
       return FPTA_OK;
+    case FPTA_OPT_INTERP_WR:
+#ifndef FPTA_DIAG_KERNELS
+      if (value) return fail(c, FPTA_EINVAL, "interp_wr: k_grid_interp_wr is a diagnostic kernel, not in this build");
+#endif
+      c->interp_wr = value ? 1 : 0;
+      return FPTA_OK;
     case FPTA_OPT_GRID_COALESCE:
       c->grid_coalesce = value ? 1 : 0;
       c->batch.grid.clear();
@@ -2013,6 +2101,7 @@ int fpta_get_option(fpta_ctx* c, int32_t key, int64_t* value) {
     case FPTA_OPT_ASYNC_SUMS: *value = c->async_sums; return FPTA_OK;
     case FPTA_OPT_PART_GROUP: *value = c->part_group; return FPTA_OK;
     case FPTA_OPT_INTERP_PSR: *value = c->interp_psr; return FPTA_OK;
+    case FPTA_OPT_INTERP_WR: *value = c->interp_wr; return FPTA_OK;
   }
   return fail(c, FPTA_EINVAL, "get_option: unknown key");
 }

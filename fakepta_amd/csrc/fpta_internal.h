@@ -167,6 +167,21 @@ hipError_t launch_grid_interp_mfma(hipStream_t st, const SynthArgs& a, const Gri
 // ws2: k_grid_interp_ws2 (64-realization compute tiles, two workgroups per CU), plain blocks only
 hipError_t launch_grid_interp_ws(hipStream_t st, const SynthArgs& a, const GridBand& band, int32_t R_pad,
                                  bool ws2 = false);
+// Window-ring variant (k_grid_interp_wr, diagnostic builds only): a workgroup walks a contiguous range of chunks for 256 realizations; each
+// grid signal's band rows stay in a ring of kWrSlots LDS rows (slot = unwrapped row mod kWrSlots), so producer waves
+// load only the rows the previous chunk's band did not hold, plus the chunk's weights; one barrier per chunk (two
+// when the bands do not fit one window). Plain blocks, <= kWrMaxSig grid signals, R_pad a multiple of 256.
+constexpr int kWrSlots = 32, kWrMaxSig = 2, kWrVMax = 40, kWrReal = 256;  // 128 + 30 KB of LDS
+constexpr int kWrFresh = 1 << 30;  // GridWindow::meta .w flag: load every band row, after the previous chunk is done
+constexpr int kWrFar = 1 << 29;    // .w flag: the new rows may load only once the chunk two back is done
+constexpr int kWrBufs = 3;         // weight buffers: the chunk being computed, the next one, the one after
+struct GridWindow {
+  const int4* meta;    // [n_chunks] {full list offset, full count, new list offset, new count | kWrFresh}
+  const int2* list;    // {LDS slot, grid-buffer row} load items
+  const int32_t* slot; // [n_chunks][vmax] LDS slot of each band row
+};
+hipError_t launch_grid_interp_wr(hipStream_t st, const SynthArgs& a, const GridBand& band, const GridWindow& wr,
+                                 int32_t R_pad);
 // Per-pulsar variant for one small grid signal (nf <= 124, vmax <= 32, no white epilogue): a workgroup makes one
 // pulsar's grid for 64 realizations in LDS (k_grid_dft_mfma's quarter-range DFT from the coefficient buffer) and
 // interpolates the pulsar's chunks from it; no grid buffer. psr_grp [P + 1]: the first partial group (a.part) or chunk

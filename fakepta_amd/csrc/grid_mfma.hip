@@ -1738,6 +1738,7 @@ hipError_t launch_part_checksums(hipStream_t st, const double* part, int32_t n_r
 #include "diag/interp_lds.inc"
 #include "diag/interp_st.inc"
 #include "diag/interp_u.inc"
+#include "diag/interp_wr.inc"
 #endif
 
 }  // namespace fpta

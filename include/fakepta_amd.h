@@ -351,6 +351,11 @@ int fpta_comm_gather(fpta_comm* comm, const double* send, int64_t count, double*
                                      one pulsar's grid for 64 realizations in LDS and interpolates the pulsar's chunks
                                      from it: no grid buffer, no separate DFT launch; pipelined blocks alternate two
                                      coefficient buffers); 0 the DFT + interpolation kernels. Results are identical. */
+#define FPTA_OPT_INTERP_WR 22     /* diagnostic builds only (FPTA_BUILD_DIAG; the product library refuses 1): gridded
+                                     plain blocks of <= 2 grid signals, R_pad a multiple of 256: 1 k_grid_interp_wr
+                                     (each grid signal's band rows kept in a ring of LDS rows across consecutive chunks:
+                                     only the rows the previous chunk did not hold are loaded; measured slower); 0
+                                     (default) the other kernels. Results are identical. */
 int fpta_set_option(fpta_ctx* ctx, int32_t key, int64_t value);
 /* Current value of option `key` (same keys as fpta_set_option). */
 int fpta_get_option(fpta_ctx* ctx, int32_t key, int64_t* value);

@@ -791,3 +791,45 @@ def test_psr_pipelined_batches_are_bitwise_identical(ctx, capi, shipped, fuse):
     finally:
         ctx.batch_clear()
         ctx.set_options(shipped)
+
+
+@pytest.mark.parametrize("layout", ["shared", "two_unsorted", "dense"])
+@pytest.mark.parametrize("R", [256, 1024, 1100])
+def test_window_ring_interpolation_is_bitwise_identical(ctx, capi, shipped, layout, R):
+    """FPTA_OPT_INTERP_WR (k_grid_interp_wr: each grid signal's band rows kept in a ring of LDS rows across consecutive
+    chunks, only the rows the previous chunk did not hold loaded) returns the warp-specialised kernel's block bit for
+    bit: the coalesced C2-like two-signal layout, two signals on ragged pulsars with one pulsar's TOAs in two sorted
+    runs, the later first (the bands jump: a fresh chunk inside a pulsar), dense TOAs; every sample written
+    (NaN-poisoned block). R_pad not a multiple of 256 (R = 1100) takes the other kernels. A diagnostic kernel
+    (measured slower, not adopted): the product library refuses the option."""
+    if not _diag_build(capi):
+        with pytest.raises(capi.FptaError, match="diagnostic"):
+            ctx.set_option(capi.OPT_INTERP_WR, 1)
+        assert ctx.get_option(capi.OPT_INTERP_WR) == 0
+        return
+    rng = np.random.default_rng(101 + len(layout))
+    if layout == "shared":
+        _shared_span_layout(ctx, rng, n=(1500, 2400), nu_const=False)
+    else:
+        offs, toas, nu = random_layout(rng, 17, (2000, 2400))  # bands of <= 40 rows over both signals
+        if layout == "two_unsorted":  # one pulsar's TOAs as two sorted runs, the later half first: the bands jump
+            k = (offs[2] - offs[1]) // 2
+            toas[offs[1]:offs[2]] = np.roll(toas[offs[1]:offs[2]], k)
+        ctx.batch_set_toas(offs, toas, nu)
+        for nm, idx in ((30, 0.0), (100, 2.0)):
+            f, a = per_psr_signal(rng, offs, toas, nm)
+            ctx.batch_add_signal(0, f, a, idx=idx)
+    try:
+        ctx.set_option(capi.OPT_SYNTH_PATH, 4)
+        res = {}
+        for wr in (0, 1):
+            ctx.set_option(capi.OPT_INTERP_WR, wr)
+            ctx.batch_synth(3, 0, R, to_host=False)
+            ctx.debug_fill_out(np.nan)
+            res[wr] = ctx.batch_synth(3, 32, R)
+            name = ctx.batch_grid_info()["interp_kernel"]
+            assert (name == "k_grid_interp_wr") == (wr == 1 and R % 256 == 0), name
+        assert np.all(np.isfinite(res[1]))
+        np.testing.assert_array_equal(res[0], res[1])
+    finally:
+        ctx.set_options(shipped)
