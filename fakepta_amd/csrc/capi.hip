@@ -2550,7 +2550,11 @@ int fpta_batch_device_out(fpta_ctx* c, double** dptr, int64_t* ld, int32_t* n_re
 // Per-realization {sum, sum of squares} of the context's last block into c->sums (device): from the interpolation's
 // partial checksums when it wrote them for this block, else one pass over the block. On the ctx stream, or (async,
 // streamed jobs with partials) on the red stream beside the next block's work; *used: the stream the sums are on.
-static int launch_block_checksums(fpta_ctx* c, bool async = false, hipStream_t* used = nullptr) {
+// With dst (device or pinned host memory), sums from the partials are written there directly (*direct = true)
+// instead of into c->sums.
+static int launch_block_checksums(fpta_ctx* c, bool async = false, hipStream_t* used = nullptr, double* dst = nullptr,
+                                  bool* direct = nullptr) {
+  if (direct) *direct = false;
   hipStream_t st = c->stream;
   if (async && c->part_ready) {
     if (!c->red) HIPCHK(c, hipStreamCreateWithFlags(&c->red, hipStreamNonBlocking), "red stream create");
@@ -2565,7 +2569,9 @@ static int launch_block_checksums(fpta_ctx* c, bool async = false, hipStream_t* 
     if (rc) return rc;
   }
   if (used) *used = st;
-  if (c->sums.cap < sizeof(double) * 2 * c->out_R) {
+  if (c->part_ready && dst) {
+    if (direct) *direct = true;
+  } else if (c->sums.cap < sizeof(double) * 2 * c->out_R) {
     HIPCHK(c, hipStreamSynchronize(st), "sums regrow sync");
     HIPCHK(c, c->sums.ensure(sizeof(double) * 2 * c->out_R), "sums alloc");
   }
@@ -2577,7 +2583,7 @@ static int launch_block_checksums(fpta_ctx* c, bool async = false, hipStream_t* 
     }
     HIPCHK(c,
            launch_part_checksums(st, c->part[c->part_cur].as<double>(), c->part_chunks, c->part_rpad, c->out_R,
-                                 c->part_tmp.as<double>(), c->sums.as<double>()),
+                                 c->part_tmp.as<double>(), dst ? dst : c->sums.as<double>()),
            "k_part_reduce launch");
     if (st == c->red) {
       HIPCHK(c, hipEventRecord(c->ev_pfree[c->part_cur], c->red), "event record");
@@ -2768,8 +2774,10 @@ int multi_fail(fpta_multi* m, int i, int rc) {
 // red stream beside the next block when the interpolation wrote partials, else on the ctx stream.
 int checksums_async(fpta_ctx* c, double* dst, bool d2d = false) {
   hipStream_t st = nullptr;
-  int rc = launch_block_checksums(c, c->async_sums != 0, &st);
+  bool direct = false;
+  int rc = launch_block_checksums(c, c->async_sums != 0, &st, dst, &direct);
   if (rc) return rc;
+  if (direct) return FPTA_OK;  // the reduction wrote dst
   HIPCHK(c,
          hipMemcpyAsync(dst, c->sums.p, sizeof(double) * 2 * c->out_R,
                         d2d ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, st),
@@ -2933,7 +2941,8 @@ static int stream_checksums(fpta_multi* m, uint64_t seed, int64_t real0, int64_t
       if (n == 0) continue;
       fpta_ctx* c = m->ctx[g];
       hipError_t e = hipSetDevice(c->device);
-      if (e == hipSuccess) e = hipHostMalloc((void**)&stage[g], sizeof(double) * 2 * n, hipHostMallocDefault);
+      // coherent: the partial-checksum reduction writes its sums here directly from the device (checksums_async)
+      if (e == hipSuccess) e = hipHostMalloc((void**)&stage[g], sizeof(double) * 2 * n, hipHostMallocCoherent);
       if (e != hipSuccess) rc = multi_fail(m, (int)g, hip_fail(c, e, "multi_synth staging"));
     }
   }

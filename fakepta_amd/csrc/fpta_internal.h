@@ -222,8 +222,10 @@ struct GridUnion {
 hipError_t launch_grid_interp_u(hipStream_t st, const SynthArgs& a, const GridBand& band, const GridUnion& un,
                                 int32_t R_pad);
 // checksums [n_real][2] from the interpolation's partials [n_rows][R_pad][2] (one row per group of part_group
-// consecutive chunks), summed over rows in a fixed order (tmp: kPartSegs * R_pad * 2 doubles)
+// consecutive chunks), summed over rows in a fixed order: one pass (k_part_sums) for n_rows <= kPartOneRows, else two
+// (tmp: kPartSegs * R_pad * 2 doubles). sums may be pinned host memory.
 constexpr int kPartSegs = 64;
+constexpr int kPartOneSegs = 16, kPartOneRows = 16 * 48;
 constexpr int kPartGroup = 16, kPartGroupMax = 16;
 hipError_t launch_part_checksums(hipStream_t st, const double* part, int32_t n_rows, int32_t R_pad, int32_t n_real,
                                  double* tmp, double* sums);

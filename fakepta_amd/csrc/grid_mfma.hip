@@ -1722,9 +1722,47 @@ __global__ __launch_bounds__(64) void k_part_final(const double* __restrict__ tm
   sums[2 * r + 1] = b;
 }
 
+// One pass for up to kPartOneRows rows: a workgroup is 16 realizations x kPartOneSegs row segments; thread (ri, s) sums
+// rows [s L, (s + 1) L) of realization 16 b + ri in order, and the segment sums are added in segment order through
+// LDS. A wave's load reads four 256-byte runs. One launch instead of two beside the streamed job's next block.
+__global__ __launch_bounds__(256) void k_part_sums(const double* __restrict__ part, int32_t n_rows, int32_t R_pad,
+                                                   int32_t L, int32_t n_real, double* __restrict__ sums) {
+  static_assert(16 * kPartOneSegs == 256, "16 realizations x kPartOneSegs segments per workgroup");
+  __shared__ dbl2 seg[kPartOneSegs][16];
+  const int ri = threadIdx.x & 15, s = threadIdx.x >> 4;
+  const int r = blockIdx.x * 16 + ri;
+  double a = 0.0, b = 0.0;
+  if (r < R_pad) {
+    const int c1 = min(n_rows, (s + 1) * L);
+#pragma unroll 8
+    for (int c = s * L; c < c1; ++c) {
+      const dbl2 v = *(const dbl2*)(part + ((int64_t)c * R_pad + r) * 2);
+      a += v.x;
+      b += v.y;
+    }
+  }
+  seg[s][ri] = dbl2{a, b};
+  __syncthreads();
+  if (s == 0 && r < n_real) {
+    double x = 0.0, y = 0.0;
+#pragma unroll
+    for (int k = 0; k < kPartOneSegs; ++k) {
+      x += seg[k][ri].x;
+      y += seg[k][ri].y;
+    }
+    *(dbl2*)(sums + 2 * (int64_t)r) = dbl2{x, y};
+  }
+}
+
 hipError_t launch_part_checksums(hipStream_t st, const double* part, int32_t n_rows, int32_t R_pad, int32_t n_real,
                                  double* tmp, double* sums) {
   if (n_rows <= 0 || n_real <= 0 || n_real > R_pad) return hipErrorInvalidValue;
+  if (n_rows <= kPartOneRows) {
+    const int32_t L1 = (n_rows + kPartOneSegs - 1) / kPartOneSegs;
+    hipLaunchKernelGGL(k_part_sums, dim3((unsigned)((n_real + 15) / 16)), dim3(256), 0, st, part, n_rows, R_pad, L1,
+                       n_real, sums);
+    return hipGetLastError();
+  }
   const int32_t L = (n_rows + kPartSegs - 1) / kPartSegs;
   const int32_t n_seg = (n_rows + L - 1) / L;
   hipLaunchKernelGGL(k_part_reduce, dim3((unsigned)((R_pad + 255) / 256), (unsigned)n_seg), dim3(256), 0, st, part,

@@ -14,6 +14,9 @@ def main():
     ap.add_argument("trace")
     ap.add_argument("--marker", default="k_grid_interp")
     ap.add_argument("--last", type=int, default=10)
+    ap.add_argument("--timeline", type=int, default=0,
+                    help="also list every launch (copies included) of the last N steps: start/end/duration us "
+                         "relative to the end of the step before them, stream, name")
     a = ap.parse_args()
     rows = list(csv.DictReader(open(a.trace)))
     ev = sorted(((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"], r.get("Stream_Id", ""),
@@ -35,6 +38,12 @@ def main():
         print(f"  {k[:70]:70s} {len(es) / a.last:5.2f}/step  mean {sum(d) / len(d):.4f} ms  "
               f"sum/step {sum(d) / a.last:.4f} ms  vgpr {es[0][4]}+{es[0][5]} lds {es[0][6]} grid {es[0][7]} "
               f"stream {es[0][3]}")
+    if a.timeline:
+        z = ev[ends[-a.timeline - 1]][1]
+        print(f"timeline of the last {a.timeline} steps (us from the end of the {a.marker} before them)")
+        for e in ev[ends[-a.timeline - 1] + 1:ends[-1] + 1]:
+            print(f"  {(e[0] - z) / 1e3:9.1f} {(e[1] - z) / 1e3:9.1f} {(e[1] - e[0]) / 1e3:8.1f} s{e[3]} "
+                  f"{e[2].split('(')[0][:60]}")
 
 
 if __name__ == "__main__":
