@@ -9,7 +9,7 @@ nothing is copied back inside it. Weak scaling: rank g of G owns realizations (s
 
 --config c3 (BASELINE configs[2]): the same 100-psr array with the HD GWB only (K = 60), a job of
 100,000 realizations sharded over the ranks (fakepta_amd.batch.simulate_sharded: rank g owns
-[g R/G, (g+1) R/G)), streamed in batches of 4096 per GPU, per-realization checksums gathered to
+[g R/G, (g+1) R/G)), streamed in batches of 7168 per GPU, per-realization checksums gathered to
 rank 0. Strong scaling (the job is fixed); one step = the whole job.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3]
@@ -65,7 +65,10 @@ def parse():
     ap.add_argument("--config", default="c2", choices=("c2", "c3"))
     ap.add_argument("--real", type=int, default=1024, help="c2: realizations per GPU per step")
     ap.add_argument("--c3-real", type=int, default=100000, help="c3: realizations of the whole job")
-    ap.add_argument("--c3-batch", type=int, default=4096, help="c3: realizations per batch per GPU")
+    # 7168 = 112 blocks of 64 realizations: 100 pulsars x 112 = 11200 k_grid_interp_psr workgroups, 21.9 rounds of
+    # the 512 the chip holds (4096: 12.5 rounds, half of the last one idle); 37.8-38.1 vs 39.5-39.6 ms per job on
+    # one box (profiles/round4/R5v_c3_batch_sizes.txt). The checksums do not depend on the batch size.
+    ap.add_argument("--c3-batch", type=int, default=7168, help="c3: realizations per batch per GPU")
     ap.add_argument("--npsr", type=int, default=100)
     ap.add_argument("--ntoa", type=int, default=2000)
     ap.add_argument("--seed", type=int, default=1234)

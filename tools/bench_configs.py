@@ -4,7 +4,7 @@
 
 c1  make_fake_array(25 psr, Tobs 10, ntoas 1000, gaps, RN30) drop-in latency, seed 0
     (the reference: 0.045 s on the survey container's CPU)
-c3  100-psr HD GWB30 only (K = 60), realizations streamed in batches of 4096, checksums only
+c3  100-psr HD GWB30 only (K = 60), realizations streamed in batches of 7168 (bench.py --c3-batch), checksums only
 c4  1000 psr x 10k TOAs, HD GWB100 (K = 200), 1000x1000 ORF factor, R = 256
 c5  100 psr, RN30 + DM100 + Sv100 + HD30 + monopole30 + dipole30 + white + ECORR (K = 640), R = 1024
 Prints one JSON line per config: samples/s end-to-end (pipelined, no per-kernel events) and per-kernel-class
@@ -100,7 +100,7 @@ def _interp_entry(gi, n_toa, R, ms):
                 frac=gbs / HBM_PEAK_GBS if gbs else None)
 
 
-def c3_job(total=100000, batch=4096, jobs=2):
+def c3_job(total=100000, batch=7168, jobs=2):
     """C3 as bench.py --config c3 runs it on one GPU: the HD GWB job of `total` realizations streamed through
     simulate_sharded (fused partial checksums, pipelined batches), `jobs` timed jobs after one warm job; the
     fused-checksum interpolation's average launch time over the timed jobs (HIP events; it co-runs with the next
