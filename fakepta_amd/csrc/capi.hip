@@ -262,10 +262,11 @@ struct fpta_ctx {
   // FPTA_OPT_SIDE_SPLIT: grid signal split_g (per-pulsar members only) of the current pipelined block runs its draws
   // and DFT on side2. At each block start side waits for side2's previous work (ev_s2done) and side2 for side's
   // (ev_s2begin), so a layout change never lets one stream write columns the other still reads; ev_gready2: side2's
-  // DFT is done.
-  int side_split = 1;
+  // DFT is done. side_split 2: side2's DFT also waits for the common signals' draws queued on side before it
+  // (ev_s2mix), so those draws get the room beside the previous block's interpolation first.
+  int side_split = 2;
   hipStream_t side2 = nullptr;
-  hipEvent_t ev_s2begin = nullptr, ev_s2done = nullptr, ev_gready2 = nullptr;
+  hipEvent_t ev_s2begin = nullptr, ev_s2done = nullptr, ev_gready2 = nullptr, ev_s2mix = nullptr;
   bool s2done_set = false;
   int32_t split_g = -1;
   bool coef_copy_pending = false;  // the block's coefficients are still to be downloaded after the synthesis
@@ -1511,6 +1512,11 @@ int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad, bool pipe = fa
         if (s != split) rest_sigs.push_back(s);
       {
         if (c->gfree_set[gi]) HIPCHK(c, hipStreamWaitEvent(c->side2, c->ev_gfree[gi], 0), "grid buffer wait");
+        if (c->side_split == 2) {
+          if (!c->ev_s2mix) HIPCHK(c, hipEventCreateWithFlags(&c->ev_s2mix, hipEventDisableTiming), "event create");
+          HIPCHK(c, hipEventRecord(c->ev_s2mix, c->side), "event record");
+          HIPCHK(c, hipStreamWaitEvent(c->side2, c->ev_s2mix, 0), "side wait");
+        }
         KTimer kt2(c, FPTA_K_GRID, c->side2);
         int rc = dfts(c->side2, {split});
         if (rc) return rc;
@@ -1969,7 +1975,7 @@ int fpta_destroy(fpta_ctx* c) {
   }
   for (hipEvent_t e : {c->ev_pready, c->ev_pfree[0], c->ev_pfree[1], c->ev_red})
     if (e) (void)hipEventDestroy(e);
-  for (hipEvent_t e : {c->ev_s2begin, c->ev_s2done, c->ev_gready2})
+  for (hipEvent_t e : {c->ev_s2begin, c->ev_s2done, c->ev_gready2, c->ev_s2mix})
     if (e) (void)hipEventDestroy(e);
   if (c->ev_begin) (void)hipEventDestroy(c->ev_begin);
   if (c->ev_coef_free) (void)hipEventDestroy(c->ev_coef_free);
@@ -2057,7 +2063,8 @@ int fpta_set_option(fpta_ctx* c, int32_t key, int64_t value) {
       c->interp_ws = (int)value;
       return FPTA_OK;
     case FPTA_OPT_SIDE_SPLIT:
-      c->side_split = value ? 1 : 0;
+      if (value < 0 || value > 2) return fail(c, FPTA_EINVAL, "side_split must be 0 .. 2");
+      c->side_split = (int)value;
       return FPTA_OK;
     case FPTA_OPT_VALU_VARIANT:
       if (value < 0 || value >= kNumValuVariants) return fail(c, FPTA_EINVAL, "unknown VALU variant");

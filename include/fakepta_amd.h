@@ -323,10 +323,13 @@ int fpta_comm_gather(fpta_comm* comm, const double* send, int64_t count, double*
                                      (compute waves hand their sums to storer waves through LDS; the storers add
                                      white noise / ECORR, store and reduce partial checksums). Results are
                                      identical. */
-#define FPTA_OPT_SIDE_SPLIT 16    /* pipelined gridded blocks (FPTA_OPT_OVERLAP): 1 (default) the grid signal with
-                                     the largest DFT, when it has no common (ORF-mixed) member, is drawn and
+#define FPTA_OPT_SIDE_SPLIT 16    /* pipelined gridded blocks (FPTA_OPT_OVERLAP): 1 the grid signal with the
+                                     largest DFT, when it has no common (ORF-mixed) member, is drawn and
                                      transformed on a second side stream, beside the other signals' draws, mixing
-                                     and DFT; 0 one side stream for all. Results are identical. */
+                                     and DFT; 2 (default) the same, its DFT started after the common signals'
+                                     draws + mixing queued on the first side stream (they get the room beside the
+                                     previous block's interpolation first: C2 -1.3 %, C5 -1.4 %); 0 one side
+                                     stream for all. Results are identical. */
 #define FPTA_OPT_DFT_GEN 17       /* gridded path: 1 (default) a grid signal with a per-pulsar member draws its
                                      coefficients inside its DFT kernel (k_grid_dft_gen: Philox + Box-Muller into
                                      LDS, same counters and draws as k_gen); 0 k_gen writes them to the coefficient

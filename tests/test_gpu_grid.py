@@ -399,7 +399,8 @@ def test_pipelined_batches_are_bitwise_identical(ctx, capi, shipped, fuse, layou
     the side stream into the other grid buffer while block b interpolates; the per-realization checksums of 5
     back-to-back blocks (no host round trip) equal the single-stream ones bit for bit, with and without fused
     checksums, for a coalesced multi-signal layout and a one-signal (C3-like) layout; and so do they with the
-    per-pulsar DM grid signal drawn and transformed on a second side stream (FPTA_OPT_SIDE_SPLIT 1) or not."""
+    per-pulsar DM grid signal drawn and transformed on a second side stream (FPTA_OPT_SIDE_SPLIT 1, or 2: after the
+    common draws) or not."""
     rng = np.random.default_rng(61)
     if layout == "coalesced":
         _shared_span_layout(ctx, rng, nu_const=False)
@@ -412,12 +413,13 @@ def test_pipelined_batches_are_bitwise_identical(ctx, capi, shipped, fuse, layou
         ctx.set_option(capi.OPT_SYNTH_PATH, 4)
         ctx.set_option(capi.OPT_FUSE_CHECKSUMS, fuse)
         res = {}
-        for ov, split in ((0, 1), (1, 1), (1, 0)):
+        for ov, split in ((0, 1), (1, 1), (1, 0), (1, 2)):
             ctx.set_option(capi.OPT_OVERLAP, ov)
             ctx.set_option(capi.OPT_SIDE_SPLIT, split)
             res[ov, split] = ctx.batch_synth_checksums(21, 3, 5 * 256 - 17, batch=256)
         np.testing.assert_array_equal(res[0, 1], res[1, 1])
         np.testing.assert_array_equal(res[0, 1], res[1, 0])
+        np.testing.assert_array_equal(res[0, 1], res[1, 2])
     finally:
         ctx.set_options(shipped)
 
@@ -439,7 +441,7 @@ def test_pipelined_layout_switches_are_bitwise_identical(ctx, capi, shipped):
         return out
     try:
         ref = run(0, 1)
-        for ov, split in ((1, 1), (1, 0)):
+        for ov, split in ((1, 1), (1, 0), (1, 2)):
             for a, b in zip(ref, run(ov, split)):
                 np.testing.assert_array_equal(a, b)
     finally:
