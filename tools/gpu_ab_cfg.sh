@@ -34,7 +34,7 @@ import json,sys
 d=json.loads(sys.stdin.read())
 ms=d.get('ms_per_step')
 r=d.get('roofline',{})
-print('rep $rep', '$cfg', repr('$v'), round(ms,4), 'ms/step', 'interp', r.get('avg_launch_ms'), 'iso', r.get('isolated',{}).get('avg_launch_ms'), 'k', d.get('isolated_kernels_ms_per_step'))" | tee -a $out
+print('rep $rep', '$cfg', repr('$v'), round(ms,4), 'ms/step', 'interp', r.get('avg_launch_ms'), 'iso', r.get('isolated',{}).get('avg_launch_ms'), 'dft_iso', r.get('isolated',{}).get('dft_ms_per_block'), 'k', d.get('isolated_kernels_ms_per_step'))" | tee -a $out
     i=$((i+1))
   done
 done
