@@ -1676,7 +1676,10 @@ hipError_t launch_mix_mfma_t(hipStream_t st, const SegDesc& sd, int32_t P, int32
 
 // Wave tile 64 pulsars x 64 columns at 2 waves per SIMD for large arrays (C4: the mix is a kernel of its own);
 // 64 x 32 at 3 waves per SIMD for small ones, whose mixing co-runs with the previous block's interpolation.
-constexpr int kMixLargeP = 256;
+#ifndef FPTA_MIX_LARGE_P
+#define FPTA_MIX_LARGE_P 256
+#endif
+constexpr int kMixLargeP = FPTA_MIX_LARGE_P;
 
 hipError_t launch_mix_mfma(hipStream_t st, const SegDesc& sd, int32_t P, int32_t R_pad, const double* zbuf,
                            double* coef, int32_t K, double* x_out, int32_t acc_col0) {
