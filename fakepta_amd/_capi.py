@@ -106,10 +106,11 @@ OPT_SYNTH_PATH, OPT_MFMA_MIN_REAL, OPT_PROFILE, OPT_ANCHOR, OPT_VALU_VARIANT, OP
 OPT_GRID_WIDTH, OPT_GRID_SIGMA, OPT_GRID_MFMA, OPT_FUSE_CHECKSUMS = 7, 8, 9, 10
 OPT_MIX_MFMA, OPT_OVERLAP, OPT_INTERP_LDS, OPT_GRID_COALESCE, OPT_INTERP_WS, OPT_SIDE_SPLIT = 11, 12, 13, 14, 15, 16
 OPT_DFT_GEN, OPT_GEN_MIX, OPT_ASYNC_SUMS, OPT_PART_GROUP, OPT_INTERP_PSR, OPT_INTERP_WR = 17, 18, 19, 20, 21, 22
+OPT_INTERP_FUSED = 23
 OPTIONS = (OPT_SYNTH_PATH, OPT_MFMA_MIN_REAL, OPT_PROFILE, OPT_ANCHOR, OPT_VALU_VARIANT, OPT_FUSE_WHITE,
            OPT_GRID_WIDTH, OPT_GRID_SIGMA, OPT_GRID_MFMA, OPT_FUSE_CHECKSUMS, OPT_MIX_MFMA, OPT_OVERLAP,
            OPT_INTERP_LDS, OPT_GRID_COALESCE, OPT_INTERP_WS, OPT_SIDE_SPLIT, OPT_DFT_GEN, OPT_GEN_MIX,
-           OPT_ASYNC_SUMS, OPT_PART_GROUP, OPT_INTERP_PSR, OPT_INTERP_WR)
+           OPT_ASYNC_SUMS, OPT_PART_GROUP, OPT_INTERP_PSR, OPT_INTERP_WR, OPT_INTERP_FUSED)
 K_GEN, K_MIX, K_SYNTH, K_WHITE, K_DENSE, K_GRID = 0, 1, 2, 3, 4, 5
 
 
@@ -122,7 +123,8 @@ def interp_kernel_name(code):
     return {0: f"k_grid_interp_mfma<{white}, {part}, 8>", 1: f"k_grid_interp_ws<{part}>",
             2: f"k_grid_interp_ws2<{part}>", 3: f"k_grid_interp_lds<{white}, {part}>",
             4: f"k_grid_interp_st<{white}, {part}>", 5: f"k_grid_interp_u<{part}>",
-            6: f"k_grid_interp_psr<{part}, 4>", 7: f"k_grid_interp_psr<{part}, 8>", 10: "k_grid_interp_wr"}.get(kind)
+            6: f"k_grid_interp_psr<{part}, 4>", 7: f"k_grid_interp_psr<{part}, 8>", 8: "k_grid_fused<8>", 9: "k_grid_fused<12>",
+            10: "k_grid_interp_wr"}.get(kind)
 BUILD_DEBUG, BUILD_DIAG = 1, 2
 GATHER_AUTO, GATHER_RCCL, GATHER_HOST = 0, 1, 2
 COMM_ID_BYTES = 128

@@ -94,6 +94,13 @@ struct GridPlan {
   int32_t pg_size = 0, n_pg = 0;
   DevBuf pgfirst, psr_pg;
   DevBuf psr_c0;  // device copy of psr_chunk0 (k_grid_interp_psr without partial checksums)
+  // k_grid_fused plan (FPTA_OPT_INTERP_FUSED): every grid signal's grid for kFusedReal realizations in LDS (signal s
+  // at LDS row fused_lrow0[s]), its coefficient staging at fused_stage[s] (doubles; may lie under the grids);
+  // frows [n_chunks][vmax] the LDS row of each band row; fused_lds the workgroup's LDS bytes
+  bool fused_ok = false;
+  size_t fused_lds = 0;
+  std::vector<int32_t> fused_lrow0, fused_stage;
+  DevBuf frows;
   // k_grid_interp_wr plan (GridWindow): <= 2 grid signals, each signal's band rows in a ring of kWrSlots LDS slots by
   // unwrapped row; per chunk the slot of each band row, and the rows to load: all its band rows (full) or those not in
   // the previous chunk's band (new; = full and flagged fresh when the two bands do not fit one ring window)
@@ -143,6 +150,10 @@ struct GridPlan {
     psr_chunk0.clear();
     pg_size = n_pg = 0;
     wr_ok = false;
+    fused_ok = false;
+    fused_lds = 0;
+    fused_lrow0.clear();
+    fused_stage.clear();
     members.clear();
     anchor.clear();
     last.clear();
@@ -222,6 +233,7 @@ struct fpta_ctx {
   int part_group = kPartGroup;  // fused partial checksums: consecutive chunks per partial row (FPTA_OPT_PART_GROUP)
   int interp_psr = 1;  // k_grid_interp_psr where the layout allows it (FPTA_OPT_INTERP_PSR)
   int interp_wr = 0;   // k_grid_interp_wr for plain blocks where the plan allows it (FPTA_OPT_INTERP_WR)
+  int interp_fused = 1;  // k_grid_fused for plain blocks where the plan allows it (FPTA_OPT_INTERP_FUSED)
   // pipelined per-pulsar blocks read their coefficients in the interpolation (ctx stream): two coefficient buffers,
   // coef2 the other one; coef_slot = the grid-buffer index whose block owns c->coef; prev_psr: the last pipelined
   // block ran that way (its draws waited for the interpolation two blocks back, not for the whole ctx stream)
@@ -590,6 +602,18 @@ bool psr_layout(const fpta_ctx* c, const Layout& L) {
   return gs->nf <= 124 && gs->nf % 4 == 0 && gs->ldq == kGridDftRows && G.vmax <= 32 && gs->rowoff == 0;
 }
 
+// The gridded plan of L runs on k_grid_fused (FPTA_OPT_INTERP_FUSED): its grids and coefficient staging for
+// kFusedReal realizations fit in LDS (GridPlan::fused_ok), no per-pulsar (psr) or diagnostic kernel chosen. Blocks
+// with white noise, fused checksums or accumulation take the other kernels (grid_run).
+bool fused_layout(const fpta_ctx* c, const Layout& L) {
+  const GridPlan& G = L.grid;
+  return c->interp_fused && G.built && G.ok && G.fused_ok && (c->grid_mfma & 1) && !c->interp_lds &&
+         c->interp_ws < 4 && !c->interp_wr && !psr_layout(c, L);
+}
+
+// The interpolation kernel reads the block's coefficients (pipelined blocks alternate two coefficient buffers)
+bool coef_in_interp(const fpta_ctx* c, const Layout& L) { return psr_layout(c, L) || fused_layout(c, L); }
+
 // merge: the gridded plan of L coalesces signals (GridPlan::members): after the last member of a grid signal is
 // drawn, k_coef_merge adds the other members' columns into the anchor's. coef_host (optional, with merge): the
 // per-signal coefficients [P][K][R] are downloaded before any merge and *coef_done is set.
@@ -607,7 +631,7 @@ int run_coefficients(fpta_ctx* c, Layout& L, uint64_t seed, int64_t real0, int32
   if (!use_side) c->coef_free_set = false;  // coef is written on the ctx stream from here on
   // a pipelined per-pulsar block draws into the coefficient buffer of its grid-buffer index (the interpolation of the
   // previous block may still read the other one)
-  const bool psr = pipe && use_side && !zin && !x_out && !coef_host && psr_layout(c, L);
+  const bool psr = pipe && use_side && !zin && !x_out && !coef_host && coef_in_interp(c, L);
   if (psr && c->coef_slot != c->gbuf) {
     c->coef.swap(c->coef2);
     c->coef_slot = c->gbuf;
@@ -680,7 +704,8 @@ int run_coefficients(fpta_ctx* c, Layout& L, uint64_t seed, int64_t real0, int32
   std::vector<int32_t> group_of(L.segs.size(), -1);
   for (size_t g = 0; g < G.members.size(); ++g)
     for (int32_t i : G.members[g]) group_of[i] = (int32_t)g;
-  if (pipe && use_side && c->side_split && G.built && G.ok && G.members.size() > 1 && !zin && !x_out && !coef_host) {
+  if (pipe && use_side && c->side_split && G.built && G.ok && G.members.size() > 1 && !zin && !x_out && !coef_host &&
+      !psr) {
     int64_t best = -1;
     for (size_t g = 0; g < G.members.size(); ++g) {
       bool per_pulsar = true;
@@ -1372,6 +1397,38 @@ int grid_build(fpta_ctx* c, Layout& L) {
     G.grid_vals += (double)L.P * gs->nf;
     G.fma_grid = G.fma_dft + G.fma_interp;
   }
+  // k_grid_fused: the grids of kFusedReal realizations (n_seg <= kFusedMaxSig, every 32-row DFT chunk one wave's job,
+  // band steps <= 16) and the coefficient staging each fit in LDS; the staging lies under the grids (the kernel
+  // writes the grids after its last staging read)
+  {
+    int32_t jobs = 0, rows = 0, stage = 0;
+    bool ok = n_seg <= kFusedMaxSig;
+    for (int32_t s = 0; s < n_seg && ok; ++s) {
+      const GridSeg* gs = G.segs[s];
+      ok = gs->nf % 4 == 0 && gs->ldq == (gs->nf / 4 + 32) / 32 * 32;
+      G.fused_lrow0.push_back(rows);
+      G.fused_stage.push_back(stage);
+      jobs += (gs->nf / 4 + 32) / 32;
+      rows += gs->nf;
+      stage += 2 * gs->ntq * kFusedReal * 2;
+    }
+    const size_t lds = sizeof(double) * std::max<size_t>((size_t)rows * kFusedPitch, (size_t)stage);
+    ok = ok && jobs <= kFusedWaves && lds <= (size_t)kFusedLdsMax;
+    if (ok) {
+      std::vector<int32_t> lrt((size_t)n_chunks * vmax);
+      for (int32_t ci = 0; ci < n_chunks; ++ci) {
+        int32_t* r = lrt.data() + (size_t)ci * vmax;
+        int32_t v = 0;
+        for (int32_t s = 0; s < n_seg; ++s)
+          for (int32_t i = 0; i < band_n[s][ci]; ++i)
+            r[v++] = G.fused_lrow0[s] + (int32_t)(((band_lo[s][ci] + i) % nf[s] + nf[s]) % nf[s]);
+        for (; v < vmax; ++v) r[v] = r[0];
+      }
+      if ((rc = upload(c, G.frows, lrt.data(), sizeof(int32_t) * lrt.size(), "fused LDS rows"))) return rc;
+      G.fused_lds = lds;
+    }
+    G.fused_ok = ok;
+  }
   G.ok = true;
   return FPTA_OK;
 }
@@ -1404,7 +1461,14 @@ int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad, bool pipe = fa
   GridSegs gsegs{};
   gsegs.n = (int32_t)G.segs.size();
   const size_t gbytes = sizeof(double) * (size_t)G.grid_rows * R_pad;
-  if (G.g_rpad != R_pad || (pipe && G.g2.cap < gbytes)) {
+  // k_grid_interp_psr: no DFT launch, no grid buffer; in a pipelined block the coefficients drawn on the side stream
+  // into buffer gi are this block's (run_coefficients)
+  const bool psr = psr_layout(c, L) && !a.w_on && !a.accumulate && (!pipe || c->prev_psr);
+  // k_grid_fused: the DFTs run inside the synthesis kernel too (plain blocks: no white epilogue, no partial checksums)
+  const bool fused = !psr && fused_layout(c, L) && !a.w_on && !a.accumulate &&
+                     !(c->fuse_sums && a.out == c->out.as<double>()) && (!pipe || c->prev_psr);
+  // grid buffers only for the kernels that read one (two of 0.41 GB each on C2)
+  if (!psr && !fused && (G.g_rpad != R_pad || (pipe && G.g2.cap < gbytes))) {
     if (c->side) HIPCHK(c, hipStreamSynchronize(c->side), "side sync");  // no reader of a buffer being regrown
     if (c->side2) HIPCHK(c, hipStreamSynchronize(c->side2), "side sync");
     HIPCHK(c, hipStreamSynchronize(c->stream), "grid regrow sync");
@@ -1414,16 +1478,13 @@ int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad, bool pipe = fa
   }
   const int gi = pipe ? c->gbuf : 0;
   double* const gbase = gi ? G.g2.as<double>() : G.g.as<double>();
-  // k_grid_interp_psr: no DFT launch, no grid buffer; in a pipelined block the coefficients drawn on the side stream
-  // into buffer gi are this block's (run_coefficients)
-  const bool psr = psr_layout(c, L) && !a.w_on && !a.accumulate && (!pipe || c->prev_psr);
   if (pipe) {
     for (hipEvent_t* e : {&c->ev_gready, &c->ev_gfree[0], &c->ev_gfree[1]})
       if (!*e) HIPCHK(c, hipEventCreateWithFlags(e, hipEventDisableTiming), "event create");
     // the DFT overwrites buffer gi: the interpolation that last read it (two blocks back) must be done
     if (c->gfree_set[gi]) HIPCHK(c, hipStreamWaitEvent(c->side, c->ev_gfree[gi], 0), "grid buffer wait");
   }
-  if (psr) {
+  if (psr || fused) {
     GridSeg* gs = G.segs[0];
     GridSegDev& g = gsegs.s[0];
     g.g = nullptr;
@@ -1607,6 +1668,50 @@ int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad, bool pipe = fa
     GridWindow wrp{G.wr_meta.as<int4>(), G.wr_list.as<int2>(), G.wr_slot.as<int32_t>()};
     HIPCHK(c, launch_grid_interp_wr(c->stream, a, band, wrp, R_pad), "k_grid_interp_wr launch");
 #endif
+  } else if (fused) {
+    const int32_t nq = G.vmax / 4;
+    kind = nq <= 8 ? 8 : 9;  // launch_grid_fused: NQ = 8 or 12 band steps at a time
+    FusedArgs f{};
+    f.n_sig = (int32_t)G.segs.size();
+    for (int32_t s = 0; s < f.n_sig; ++s) {
+      const GridSeg* gs = G.segs[s];
+      const SegDesc& d = L.segs[G.anchor[s]]->d;
+      FusedSig& fs = f.s[s];
+      fs.tq = gs->tq.as<double>();
+      fs.ldq = gs->ldq;
+      fs.ntq = gs->ntq;
+      fs.nf = gs->nf;
+      fs.nm = d.nm;
+      fs.lrow0 = G.fused_lrow0[s];
+      fs.stage = G.fused_stage[s];
+      fs.n_rc = (gs->nf / 4 + 32) / 32;
+      if (grid_gen_fused(c, L, (size_t)s)) {  // k_grid_dft_gen's terms: the anchor, then the others in layout order
+        std::vector<int32_t> order{G.anchor[s]};
+        for (int32_t i : G.members[s])
+          if (i != G.anchor[s]) order.push_back(i);
+        for (int32_t i : order) {
+          const SegDesc& sd2 = L.segs[i]->d;
+          fs.term_kind[fs.n_terms] = sd2.kind;
+          fs.term_seg[fs.n_terms] = i;
+          fs.term_nm[fs.n_terms] = sd2.nm;
+          fs.term_col0[fs.n_terms] = sd2.col0;
+          fs.term_amp[fs.n_terms] = sd2.amp;
+          ++fs.n_terms;
+        }
+      } else {  // k_grid_dft_mfma's operand: the anchor's (merged) columns of the coefficient buffer
+        fs.term_kind[0] = 1;
+        fs.term_seg[0] = G.anchor[s];
+        fs.term_nm[0] = d.nm;
+        fs.term_col0[0] = d.col0;
+        fs.n_terms = 1;
+      }
+    }
+    f.lrows = G.frows.as<int32_t>();
+    f.psr_c0 = G.psr_c0.as<int32_t>();
+    f.real0 = c->blk_real0;
+    f.k0 = c->blk_k0;
+    f.k1 = c->blk_k1;
+    HIPCHK(c, launch_grid_fused(c->stream, a, band, f, nq, G.fused_lds), "k_grid_fused launch");
   } else if (psr) {
     kind = G.vmax <= 16 ? 6 : 7;  // launch_grid_interp_psr: NQ = 4 or 8 band steps
     HIPCHK(c,
@@ -2044,6 +2149,9 @@ int fpta_set_option(fpta_ctx* c, int32_t key, int64_t value) {
     case FPTA_OPT_INTERP_PSR:
       c->interp_psr = value ? 1 : 0;
       return FPTA_OK;
+    case FPTA_OPT_INTERP_FUSED:
+      c->interp_fused = value ? 1 : 0;
+      return FPTA_OK;
     case FPTA_OPT_INTERP_WR:
 #ifndef FPTA_DIAG_KERNELS
       if (value) return fail(c, FPTA_EINVAL, "interp_wr: k_grid_interp_wr is a diagnostic kernel, not in this build");
@@ -2109,6 +2217,7 @@ int fpta_get_option(fpta_ctx* c, int32_t key, int64_t* value) {
     case FPTA_OPT_PART_GROUP: *value = c->part_group; return FPTA_OK;
     case FPTA_OPT_INTERP_PSR: *value = c->interp_psr; return FPTA_OK;
     case FPTA_OPT_INTERP_WR: *value = c->interp_wr; return FPTA_OK;
+    case FPTA_OPT_INTERP_FUSED: *value = c->interp_fused; return FPTA_OK;
   }
   return fail(c, FPTA_EINVAL, "get_option: unknown key");
 }

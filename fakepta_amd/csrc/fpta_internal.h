@@ -188,6 +188,40 @@ hipError_t launch_grid_interp_wr(hipStream_t st, const SynthArgs& a, const GridB
 // of each pulsar. Bit-identical to k_grid_dft_mfma + k_grid_interp_mfma.
 hipError_t launch_grid_interp_psr(hipStream_t st, const SynthArgs& a, const GridBand& band, const GridSegDev& gs,
                                   const int32_t* psr_grp, int32_t P, int32_t R_pad);
+// Fused per-pulsar synthesis (k_grid_fused, grid_fused.hip): a workgroup owns one pulsar x kFusedReal realizations,
+// draws every grid signal's coefficients into LDS (k_grid_dft_gen's terms and order), runs each signal's quarter-range
+// DFT on fp64 MFMA into an LDS grid (k_grid_dft_gen's steps and butterfly) and interpolates the pulsar's chunks from
+// it (k_grid_interp_ws's MFMA steps): no grid buffer, no DFT launch, bit-identical to the two-kernel path.
+constexpr int kFusedMaxSig = 4;   // grid signals
+constexpr int kFusedReal = 32;    // realizations per workgroup (two 16-realization MFMA tiles)
+constexpr int kFusedWaves = 8;    // waves per workgroup; at most this many DFT jobs (32-row chunks, all signals)
+constexpr int kFusedPitch = 32;   // doubles per LDS grid row
+constexpr int kFusedLdsMax = 160 * 1024;
+struct FusedSig {
+  const double* tq;  // quarter-range tables [4][ntq][ldq] (GridSegDev::tq)
+  int32_t ldq, ntq, nf, nm;  // nm: the anchor's padded modes
+  int32_t lrow0;     // first LDS grid row of the signal
+  int32_t stage;     // LDS offset (doubles) of its coefficients [2 ntq][kFusedReal][cos, sin]
+  int32_t n_rc;      // 32-row chunks of its quarter range (one DFT job each)
+  int32_t n_terms;   // as DftGenArgs: generated (per-pulsar) and loaded (coefficient-buffer) terms, summation order
+  int32_t term_kind[kDftGenTerms];
+  int32_t term_seg[kDftGenTerms];
+  int32_t term_nm[kDftGenTerms];
+  int32_t term_col0[kDftGenTerms];
+  const double* term_amp[kDftGenTerms];
+};
+struct FusedArgs {
+  FusedSig s[kFusedMaxSig];
+  int32_t n_sig;
+  const int32_t* lrows;   // [n_chunks][vmax] LDS grid row of each band row
+  const int32_t* psr_c0;  // [P + 1] first chunk of each pulsar
+  int64_t real0;          // the batch's first realization (Philox counter)
+  uint32_t k0, k1;
+};
+// nq_max: band steps of the widest chunk (vmax / 4; the kernel holds up to 12 steps' operands and takes a wider chunk's
+// in turns); lds_bytes: max(grid rows, coefficient staging) x their sizes
+hipError_t launch_grid_fused(hipStream_t st, const SynthArgs& a, const GridBand& band, const FusedArgs& f,
+                             int32_t nq_max, size_t lds_bytes);
 // Storer-wave variant: compute waves hand finished sums to storer waves through LDS; every block kind (white / ECORR
 // epilogue, partial checksums, accumulate) with R_pad a multiple of 128
 hipError_t launch_grid_interp_st(hipStream_t st, const SynthArgs& a, const GridBand& band, int32_t R_pad);

@@ -10,26 +10,9 @@
 #include <algorithm>
 #include <cstdlib>
 
-#include "device_common.h"
-#include "fpta_internal.h"
-#include "philox.h"
+#include "grid_device.h"
 
 namespace fpta {
-
-typedef double dbl2 __attribute__((ext_vector_type(2)));
-
-// A wave-uniform read of a table the kernel never writes, through the constant address space: a scalar load
-// (lgkmcnt). A plain load of it is a vector load once the kernel has stores the compiler cannot rule out as aliasing,
-// and waiting for it (vmcnt) then also waits for every store issued before it.
-template <class T>
-__device__ __forceinline__ T ld_uniform(const T* p) {
-  return *(const __attribute__((address_space(4))) T*)p;
-}
-typedef int i32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ int4 ld_uniform4(const void* p) {
-  const i32x4 v = ld_uniform((const i32x4*)p);
-  return make_int4(v.x, v.y, v.z, v.w);
-}
 
 // k_grid_interp_mfma: 32 TOAs x 16 kInterpRW realizations per wave, kInterpWPC persistent workgroups per CU
 // (compile-time; tools/interp_variants.sh builds the alternatives it measures into build/diag)
@@ -205,11 +188,6 @@ __global__ __launch_bounds__(256, 3) void k_grid_dft_mfma(GridSegs gsegs, const 
 // D of tile h: lane (lr, lg) register g = grid row j0 + 2 (lg + 4 g) + h, realization r0 + lr (16 consecutive
 // realizations of a row per store instruction). A term's product is rounded before the sum, as k_gen stores it and
 // k_coef_merge adds it.
-__device__ __forceinline__ double opaque(double x) {
-  asm volatile("" : "+v"(x));
-  return x;
-}
-
 constexpr int kDftGenMaxModes = 512;  // LDS: [modes][16 realizations][cos, sin] = 256 B per mode (128 KB at most)
 
 __global__ __launch_bounds__(256, 2) void k_grid_dft_gen(DftGenArgs d) {
@@ -226,45 +204,8 @@ __global__ __launch_bounds__(256, 2) void k_grid_dft_gen(DftGenArgs d) {
   //    Philox call per pair and generated term)
   for (int idx = threadIdx.x; idx < n_modes * 8; idx += nthr) {
     const int m = idx >> 3, rl = 2 * (idx & 7);
-    const int r = r0 + rl;
-    double bc[2] = {0.0, 0.0}, bs[2] = {0.0, 0.0};
-    bool first = true;
-    if (m < gs.nm)
-      for (int i = 0; i < d.n_terms; ++i) {
-        if (m >= d.term_nm[i]) continue;
-        double pc[2], ps[2];
-        if (d.term_kind[i] == 0) {
-          double z[4] = {0.0, 0.0, 0.0, 0.0};
-          const uint64_t g = (uint64_t)(d.real0 + r);
-          if (r < d.n_real) {  // padding realizations: zero, as k_gen writes them
-            if ((g & 1) == 0) {
-              gp_pair2((uint32_t)m, (uint32_t)p, (uint32_t)d.term_seg[i], g, d.k0, d.k1, z);
-            } else {
-              gp_normal2((uint32_t)m, (uint32_t)p, (uint32_t)d.term_seg[i], g, d.k0, d.k1, z[0], z[1]);
-              gp_normal2((uint32_t)m, (uint32_t)p, (uint32_t)d.term_seg[i], g + 1, d.k0, d.k1, z[2], z[3]);
-            }
-            if (r + 1 >= d.n_real) z[2] = z[3] = 0.0;
-          }
-          const double a = d.term_amp[i][(int64_t)p * d.term_nm[i] + m];
-          pc[0] = opaque(a * z[0]);
-          ps[0] = opaque(a * z[1]);
-          pc[1] = opaque(a * z[2]);
-          ps[1] = opaque(a * z[3]);
-        } else {
-          const double* cp = d.coef + ((int64_t)p * d.K + d.term_col0[i] + 2 * m) * d.R_pad + r;
-          const dbl2 vc = *(const dbl2*)cp, vs = *(const dbl2*)(cp + d.R_pad);
-          pc[0] = vc.x;
-          pc[1] = vc.y;
-          ps[0] = vs.x;
-          ps[1] = vs.y;
-        }
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          bc[h] = first ? pc[h] : bc[h] + pc[h];
-          bs[h] = first ? ps[h] : bs[h] + ps[h];
-        }
-        first = false;
-      }
+    double bc[2], bs[2];
+    grid_term_coefs(d, gs.nm, d.coef, d.K, d.R_pad, d.n_real, d.real0, d.k0, d.k1, p, m, r0 + rl, bc, bs);
     *(dbl2*)(Bs + 2 * (m * 16 + rl)) = dbl2{bc[0], bs[0]};
     *(dbl2*)(Bs + 2 * (m * 16 + rl + 1)) = dbl2{bc[1], bs[1]};
   }
@@ -414,17 +355,6 @@ __device__ __forceinline__ void white_quad(int64_t t, int64_t g, uint32_t k0, ui
 // stores the current tile. Loads and stores retire through one in-order counter (vmcnt), so loads issued after
 // the 32 stores of an epilogue would wait for them; issued before, the next tile's first 32 MFMAs run while the
 // stores drain (profiles/r02_interp_diag2.txt: without stores the kernel takes 0.42 ms, with them 0.63).
-template <int RW>
-struct InterpTile {
-  int c, p, r0, nq, cnt, y;
-  // partial-checksum row of the tile's chunk group and the chunk's place in it (first: start the row's sums, last:
-  // store them); the diagnostic kernels take one chunk per row
-  int pg = -1, pfirst = 1, plast = 1;
-  int rr[kGridVMax / 64];
-  const double* G0;
-  const double* Wp;
-};
-
 // White noise + ECORR added to the tile's sums in registers (before the next tile's operands are loaded: the
 // Philox rounds and those operands do not fit in the register budget together).
 template <int RW>
@@ -575,71 +505,6 @@ __device__ __forceinline__ void interp_partials(const SynthArgs& a, const Interp
       const int h = lr & 1, mg = lr >> 1;
       const int rl = 32 * (mg >> 2) + 2 * (lg + 4 * (mg & 3)) + h;
       __builtin_nontemporal_store(dbl2{ps[0], ps[1]}, (dbl2*)(pp + 2 * rl));
-    }
-  }
-}
-
-// PACE > 0 (k_grid_interp_st's storer waves): s_sleep PACE (x 64 cycles) after each 1 KB store of the fast path, so a
-// CU's stores enter the memory pipeline at about the rate the write path drains them. A store that waits at the head
-// of the CU's vector-memory queue holds every load behind it, including the compute waves' operand loads.
-template <int RW, int PACE = 0>
-__device__ __forceinline__ void interp_store_rows(const SynthArgs& a, double* __restrict__ out,
-                                                  const InterpTile<RW>& t, const d4 (&acc)[2][RW]) {
-  const int lane = threadIdx.x & 63;
-  const int lr = lane & 15, lg = lane >> 4;
-  const int tt = 2 * lr;  // this lane's even TOA in the chunk; tt + 1 the odd one
-  if (tt >= t.cnt) return;
-  const int64_t tg = ld_uniform(a.offs + t.p) + t.y + tt;
-  // fast path (full chunk, every realization of the tile stored, no accumulate, 16-byte aligned rows): straight-line
-  // 16-byte stores from a wave-uniform row base plus one 32-bit lane offset, no per-store tests. The general path
-  // below spends ~28 instructions and several branches per store, which held the SIMD's issue while the partner
-  // wave's MFMAs needed it.
-  {
-    const int64_t t0 = tg - tt;  // wave-uniform first sample of the chunk
-    const bool fast = t.cnt == kGridTT && !a.accumulate && t.r0 + 16 * RW <= a.n_real &&
-                      ((((uintptr_t)(out + t0)) | ((uintptr_t)a.ldo << 3)) & 15) == 0 &&
-                      a.ldo < ((int64_t)1 << 26);  // lane offsets (< 6 ldo + 32 doubles) fit 32 bits
-    if (__builtin_amdgcn_readfirstlane(fast ? 1 : 0)) {
-      const uint32_t vo = (uint32_t)(((int64_t)2 * lg * a.ldo + tt) * 8);
-      const char* base = (const char*)(out + t0 + (int64_t)t.r0 * a.ldo);
-#pragma unroll
-      for (int i = 0; i < RW; ++i)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int k = 32 * (i >> 1) + 8 * g + (i & 1);  // row of (tile i, register g) past r0 + 2 lg
-          // non-temporal: the block is never re-read by this kernel, and L2-allocating 1.6 GB of stores would evict
-          // the grid rows the next chunks re-read (they then queue behind the write stream: tools/mfma_store_probe)
-          __builtin_nontemporal_store(dbl2{acc[0][i][g], acc[1][i][g]},
-                                      (dbl2*)((char*)base + (int64_t)k * a.ldo * 8 + vo));
-          if constexpr (PACE > 0) __builtin_amdgcn_s_sleep(PACE);
-        }
-      return;
-    }
-  }
-  // one 16-byte store per (lane, realization) when both TOAs exist and the row offset r * ldo + tg keeps 16-byte
-  // alignment (ldo and tg even), else the pair is stored as two 8-byte stores
-  double* __restrict__ ocol = out + tg;
-  const bool pair = tt + 1 < t.cnt;
-  const bool vec = pair && ((((uintptr_t)ocol) | ((uintptr_t)a.ldo << 3)) & 15) == 0;
-#pragma unroll
-  for (int i = 0; i < RW; ++i) {
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int r = t.r0 + 32 * (i >> 1) + 2 * (lg + 4 * g) + (i & 1);
-      if (r < a.n_real) {
-        double* o = ocol + (int64_t)r * a.ldo;
-        double v0 = acc[0][i][g], v1 = acc[1][i][g];
-        if (a.accumulate) {
-          v0 += o[0];
-          if (pair) v1 += o[1];
-        }
-        if (vec) {
-          *(dbl2*)o = dbl2{v0, v1};
-        } else {
-          o[0] = v0;
-          if (pair) o[1] = v1;
-        }
-      }
     }
   }
 }

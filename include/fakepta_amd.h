@@ -212,7 +212,8 @@ int fpta_batch_info(fpta_ctx* ctx, int64_t* info);
  * mean band rows per chunk (all grid signals, padded to 4), out[15] the interpolation kernel of the last gridded
  * block: 0 none, else 1 + 4 kind + 2 (white / ECORR epilogue) + (fused partial checksums), kind 0
  * k_grid_interp_mfma, 1 k_grid_interp_ws, 2 k_grid_interp_ws2, 3 k_grid_interp_lds, 4 k_grid_interp_st, 5
- * k_grid_interp_u, 6 / 7 k_grid_interp_psr with 4 / 8 band steps.
+ * k_grid_interp_u, 6 / 7 k_grid_interp_psr with 4 / 8 band steps, 8 / 9 k_grid_fused holding 8 / 12 band steps'
+ * operands, 10 k_grid_interp_wr (diagnostic builds only).
  * fpta_batch_grid_info_n writes the first min(n_out, FPTA_GRID_INFO_LEN) values and returns FPTA_GRID_INFO_LEN
  * (negative on error); fpta_batch_grid_info keeps the round-1 contract: out[0..8], host double[9]. */
 #define FPTA_GRID_INFO_LEN 16
@@ -359,6 +360,13 @@ int fpta_comm_gather(fpta_comm* comm, const double* send, int64_t count, double*
                                      (each grid signal's band rows kept in a ring of LDS rows across consecutive chunks:
                                      only the rows the previous chunk did not hold are loaded; measured slower); 0
                                      (default) the other kernels. Results are identical. */
+#define FPTA_OPT_INTERP_FUSED 23  /* gridded plain blocks (no white epilogue, no fused checksums) whose grids for 32
+                                     realizations fit in LDS with at most 8 DFT jobs of 32 quarter-range rows and
+                                     4 grid signals (C2: 129 KB): 1 (default) k_grid_fused (a workgroup draws one
+                                     pulsar's coefficients for 32 realizations, runs every grid signal's DFT into LDS
+                                     and interpolates the pulsar's chunks from it: no grid buffer, no DFT launch;
+                                     pipelined blocks alternate two coefficient buffers); 0 the DFT + interpolation
+                                     kernels. Results are identical. A layout k_grid_interp_psr serves keeps it. */
 int fpta_set_option(fpta_ctx* ctx, int32_t key, int64_t value);
 /* Current value of option `key` (same keys as fpta_set_option). */
 int fpta_get_option(fpta_ctx* ctx, int32_t key, int64_t* value);

@@ -1,0 +1,162 @@
+"""k_grid_fused (FPTA_OPT_INTERP_FUSED): the whole gridded synthesis of one pulsar x 32 realizations in one workgroup
+(coefficient draws, every grid signal's quarter-range DFT into LDS, the interpolation from LDS), against the two-kernel
+path it replaces (k_grid_dft_gen / k_grid_dft_mfma + k_grid_interp_ws) bit for bit, and against the oracle.
+
+Reference loops the kernel evaluates: /root/reference/fakepta/fake_pta.py:372-387 (per-pulsar coefficients and
+F @ c) and correlated_noises.py:153-160 (the ORF-mixed common signal).
+"""
+import numpy as np
+import pytest
+
+from oracle import fakepta_oracle as O
+from tests.conftest import assert_parity, rel_err
+from tests.helpers import common_signal, per_psr_signal, random_layout
+from tests.test_gpu_grid import GRID_TOL, TOL, _flat_layout, _shared_span_layout
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def capi():
+    from fakepta_amd import _capi
+    return _capi
+
+
+@pytest.fixture(scope="module")
+def ctx(capi):
+    c = capi.Context(0)
+    yield c
+    c.close()
+
+
+@pytest.fixture(scope="module")
+def shipped(ctx, capi):
+    opts = ctx.options()
+    assert opts[capi.OPT_INTERP_FUSED] == 1
+    return opts
+
+
+def _c2_like(ctx, rng, P=23, n=(31, 700), unsorted=True):
+    """C2's signal mix on ragged pulsars: RN30 (idx 0), DM100 (idx 2, three radio bands), the HD GWB30; one pulsar's TOAs
+    unsorted, so its chunks' bands jump."""
+    offs, toas, nu = random_layout(rng, P, n)
+    if unsorted:
+        perm = rng.permutation(offs[1] - offs[0])
+        toas[offs[0]:offs[1]] = toas[offs[0]:offs[1]][perm]
+    ctx.batch_set_toas(offs, toas, nu)
+    f1, a1 = per_psr_signal(rng, offs, toas, 30)
+    ctx.batch_add_signal(0, f1, a1, idx=0.0)
+    f2, a2 = per_psr_signal(rng, offs, toas, 100)
+    ctx.batch_add_signal(0, f2, a2, idx=2.0)
+    fc, ac, L, _ = common_signal(rng, offs, toas, 30)
+    ctx.batch_add_signal(1, fc, ac, L=L)
+    segs = [O.Segment(0, 2 * np.pi * f1, a1, 0.0), O.Segment(0, 2 * np.pi * f2, a2, 2.0),
+            O.Segment(1, 2 * np.pi * fc, ac, 0.0, L=L)]
+    return offs, toas, nu, segs
+
+
+def _layout(ctx, rng, layout):
+    if layout == "c2_like":
+        return _c2_like(ctx, rng)
+    if layout in ("coalesced", "masked"):
+        return _shared_span_layout(ctx, rng, nu_const=False, with_masked=layout == "masked")
+    if layout == "one_grid":  # RN + DM + GWB at one radio frequency: a single coalesced grid signal
+        return _shared_span_layout(ctx, rng, nu_const=True)
+    if layout == "dm_only":
+        return _flat_layout(ctx, rng, P=9, n_modes=100)
+    raise ValueError(layout)
+
+
+def _run(ctx, capi, fused, seed, real0, R):
+    ctx.set_option(capi.OPT_INTERP_FUSED, fused)
+    ctx.batch_synth(seed, 0, R, to_host=False)
+    ctx.debug_fill_out(np.nan)
+    out = ctx.batch_synth(seed, real0, R)
+    return out, ctx.batch_grid_info()["interp_kernel"]
+
+
+@pytest.mark.parametrize("layout", ["c2_like", "coalesced", "masked", "one_grid", "dm_only"])
+@pytest.mark.parametrize("dft_gen", [1, 0])
+def test_fused_synthesis_is_bitwise_identical(ctx, capi, shipped, layout, dft_gen):
+    """The fused kernel returns the two-kernel path's block bit for bit: draws inside the kernel (FPTA_OPT_DFT_GEN 1:
+    k_grid_dft_gen's terms) or from the merged coefficient buffer (0: k_grid_dft_mfma's operand), one to three grid
+    signals, a masked (backend) signal, realization counts off every tile multiple and odd first realizations (the
+    Philox pair boundary), every sample written (NaN-poisoned block); the kernel that ran is the fused one. And the
+    block matches the oracle."""
+    rng = np.random.default_rng(211 + len(layout))
+    offs, toas, nu, segs = _layout(ctx, rng, layout)
+    try:
+        ctx.set_option(capi.OPT_SYNTH_PATH, 4)
+        ctx.set_option(capi.OPT_DFT_GEN, dft_gen)
+        for R, real0 in ((333, 5), (1024, 0), (1100, 77), (16, 3)):
+            ref, k0 = _run(ctx, capi, 0, 13, real0, R)
+            got, k1 = _run(ctx, capi, 1, 13, real0, R)
+            assert k1.startswith("k_grid_fused"), k1
+            assert not k0.startswith("k_grid_fused"), k0
+            assert np.all(np.isfinite(got))
+            np.testing.assert_array_equal(ref, got)
+            if R == 333:
+                want = O.batch_synth(offs, toas, nu, segs, 13, real0, R)
+                assert rel_err(got, want) <= GRID_TOL
+                assert_parity(got, want, TOL)
+    finally:
+        ctx.batch_clear()
+        ctx.set_options(shipped)
+
+
+def test_fused_pipelined_blocks(ctx, capi, shipped):
+    """Pipelined blocks (FPTA_OPT_OVERLAP 1) on the fused kernel: the next block's common draws go into the other
+    coefficient buffer on the side stream while this block's kernel reads its own. Blocks queued back to back without a
+    host round trip: the last block equals its one-stream run bit for bit; so does every block of a run of synth calls
+    that each read their block back, and the per-block checksums."""
+    rng = np.random.default_rng(223)
+    _c2_like(ctx, rng, P=40, n=(200, 900), unsorted=False)
+    try:
+        ctx.set_option(capi.OPT_SYNTH_PATH, 4)
+        res = {}
+        for ov in (0, 1):
+            ctx.set_option(capi.OPT_OVERLAP, ov)
+            for b in range(4):
+                ctx.batch_synth(29, 256 * b, 256, to_host=False)
+            res[ov, "last"] = ctx.batch_synth(29, 256 * 4, 256)
+            assert ctx.batch_grid_info()["interp_kernel"].startswith("k_grid_fused")
+            res[ov, "each"] = [(ctx.batch_synth(29, 300 * b + 1, 300), ctx.batch_checksums()) for b in range(3)]
+        np.testing.assert_array_equal(res[0, "last"], res[1, "last"])
+        for (x, xs), (y, ys) in zip(res[0, "each"], res[1, "each"]):
+            np.testing.assert_array_equal(x, y)
+            np.testing.assert_array_equal(xs, ys)
+    finally:
+        ctx.batch_clear()
+        ctx.set_options(shipped)
+
+
+def test_fused_not_taken_outside_its_blocks(ctx, capi, shipped):
+    """Blocks the fused kernel does not serve take the two-kernel path: white / ECORR epilogue, fused partial
+    checksums (streamed jobs), grids too large for LDS (257 modes), and FPTA_OPT_INTERP_FUSED 0."""
+    rng = np.random.default_rng(227)
+    try:
+        offs, toas, nu, segs = _c2_like(ctx, rng, P=12, n=(100, 300))
+        ctx.set_option(capi.OPT_SYNTH_PATH, 4)
+        ctx.batch_synth(3, 0, 256, to_host=False)
+        assert ctx.batch_grid_info()["interp_kernel"].startswith("k_grid_fused")
+        ctx.batch_set_white(np.full(offs[-1], 1e-7), [], [])
+        ctx.batch_synth(3, 0, 256, to_host=False)
+        assert not ctx.batch_grid_info()["interp_kernel"].startswith("k_grid_fused")
+        ctx.batch_set_white()
+        ctx.set_option(capi.OPT_FUSE_CHECKSUMS, 1)
+        ctx.batch_synth(3, 0, 256, to_host=False)
+        assert not ctx.batch_grid_info()["interp_kernel"].startswith("k_grid_fused")
+        ctx.set_option(capi.OPT_FUSE_CHECKSUMS, 0)
+        ctx.set_option(capi.OPT_INTERP_FUSED, 0)
+        ctx.batch_synth(3, 0, 256, to_host=False)
+        assert not ctx.batch_grid_info()["interp_kernel"].startswith("k_grid_fused")
+        ctx.set_options(shipped)
+        ctx.batch_clear()
+        _flat_layout(ctx, rng, P=3, n_modes=257)
+        ctx.set_option(capi.OPT_SYNTH_PATH, 4)
+        ctx.batch_synth(3, 0, 256, to_host=False)
+        assert not ctx.batch_grid_info()["interp_kernel"].startswith("k_grid_fused")
+    finally:
+        ctx.batch_set_white()
+        ctx.batch_clear()
+        ctx.set_options(shipped)
