@@ -294,10 +294,12 @@ def _exchange_unique_id(rank, world, addr, port, make_id, timeout, n_bytes=None)
     the other ranks connect (retrying until `timeout`) and read its bytes. Plain sockets: no torch import, so the
     rank process maps one HIP runtime (the library's).
 
-    Protocol: a rank sends b"FPTA" + its rank (uint32 little-endian), reads the id and answers b"A". Rank 0 keeps
-    accepting until every rank 1 .. world - 1 has acknowledged: a peer with a wrong magic or rank, or one that drops
-    the connection before its acknowledgement, uses up no slot (a rank that failed after connecting retries and is
-    served again). Either side raises TimeoutError past `timeout` seconds."""
+    Protocol: a rank sends b"FPTA" + its rank (uint32 little-endian), reads the id, answers b"A" and returns only once
+    rank 0 has confirmed with b"K". Rank 0 counts a rank as served after reading its b"A" and sending b"K", and keeps
+    accepting until every rank 1 .. world - 1 is served: a peer with a wrong magic or rank, or one that drops the
+    connection before its acknowledgement, uses up no slot; a rank whose acknowledgement rank 0 did not read (timeout,
+    reset) gets no confirmation, connects again and is served again. Either side raises TimeoutError past `timeout`
+    seconds."""
     import socket
     import struct
     import time as _time
@@ -331,9 +333,10 @@ def _exchange_unique_id(rank, world, addr, port, make_id, timeout, n_bytes=None)
                             continue  # a stray or foreign connection: no slot used
                         conn.sendall(uid)
                         if _recv_exact(conn, 1) == b"A":
+                            conn.sendall(b"K")
                             pending.discard(peer)
                     except OSError:
-                        continue  # the peer retries
+                        continue  # no confirmation sent: the peer connects again
         return uid
     hello = _RDZV_MAGIC + struct.pack("<I", rank)
     while True:
@@ -342,11 +345,13 @@ def _exchange_unique_id(rank, world, addr, port, make_id, timeout, n_bytes=None)
                 conn.sendall(hello)
                 buf = _recv_exact(conn, n)
                 conn.sendall(b"A")
-                return buf
+                if _recv_exact(conn, 1) == b"K":  # rank 0 recorded this rank
+                    return buf
         except OSError:
-            if _time.monotonic() > deadline:
-                raise TimeoutError(f"rank {rank}: no RCCL rendezvous at {addr}:{port} within {timeout} s")
-            _time.sleep(0.2)
+            pass  # no rank 0 yet, or no confirmation: connect again
+        if _time.monotonic() > deadline:
+            raise TimeoutError(f"rank {rank}: no RCCL rendezvous at {addr}:{port} within {timeout} s")
+        _time.sleep(0.2)
 
 
 class RcclComm:

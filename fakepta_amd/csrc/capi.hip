@@ -95,11 +95,12 @@ struct GridPlan {
   DevBuf pgfirst, psr_pg;
   DevBuf psr_c0;  // device copy of psr_chunk0 (k_grid_interp_psr without partial checksums)
   // k_grid_fused plan (FPTA_OPT_INTERP_FUSED): every grid signal's grid for kFusedReal realizations in LDS (signal s
-  // at LDS row fused_lrow0[s]), its coefficient staging at fused_stage[s] (doubles; may lie under the grids);
-  // frows [n_chunks][vmax] the LDS row of each band row; fused_lds the workgroup's LDS bytes
+  // at LDS row fused_lrow0[s]), the draw ring after them; frows [n_chunks][vmax] the LDS row of each band row;
+  // fused_lds the workgroup's LDS bytes
   bool fused_ok = false;
   size_t fused_lds = 0;
-  std::vector<int32_t> fused_lrow0, fused_stage;
+  int32_t fused_fq = 0;  // band steps per (chunk, lane group) in frows
+  std::vector<int32_t> fused_lrow0;
   DevBuf frows;
   // k_grid_interp_wr plan (GridWindow): <= 2 grid signals, each signal's band rows in a ring of kWrSlots LDS slots by
   // unwrapped row; per chunk the slot of each band row, and the rows to load: all its band rows (full) or those not in
@@ -153,7 +154,6 @@ struct GridPlan {
     fused_ok = false;
     fused_lds = 0;
     fused_lrow0.clear();
-    fused_stage.clear();
     members.clear();
     anchor.clear();
     last.clear();
@@ -1065,8 +1065,9 @@ int grid_build(fpta_ctx* c, Layout& L) {
     return rc0;
   const int32_t n_chunks = G.n_chunks;
   // band rows of a chunk: every signal's band back to back (virtual rows voff_s ..), padded to a multiple of
-  // 4 once per chunk (k_grid_interp_mfma: 4 rows per MFMA step; pad rows re-read a valid row at weight 0), and to at
-  // least kGridMinV rows (k_grid_interp_st's operand lookahead never passes the next chunk)
+  // 4 once per chunk (k_grid_interp_mfma: 4 rows per MFMA step; pad rows re-read a valid row at weight 0), and in
+  // diagnostic builds to at least kGridMinV rows (k_grid_interp_st's operand lookahead never passes the next chunk; the
+  // product kernels would only run zero-weight steps on them)
   std::vector<int32_t> voff((size_t)n_seg * n_chunks);
   int32_t vmax = 4;
   for (int32_t ci = 0; ci < n_chunks; ++ci) {
@@ -1075,7 +1076,11 @@ int grid_build(fpta_ctx* c, Layout& L) {
       voff[(size_t)s * n_chunks + ci] = v;
       v += band_n[s][ci];
     }
+#ifdef FPTA_DIAG_KERNELS
     chunks[ci].w = std::max(kGridMinV, (v + 3) & ~3);
+#else
+    chunks[ci].w = (v + 3) & ~3;
+#endif
     vmax = std::max(vmax, chunks[ci].w);
   }
   if (vmax > kGridVMax) {
@@ -1327,7 +1332,8 @@ int grid_build(fpta_ctx* c, Layout& L) {
   if ((rc = upload(c, d_chunk_of, chunk_of.data(), sizeof(int32_t) * N, "grid chunk_of")) ||
       (rc = upload(c, d_tt_of, tt_of.data(), sizeof(int32_t) * N, "grid tt_of")))
     return rc;
-  const size_t wbytes = sizeof(double) * (size_t)n_chunks * vmax * kGridTT;
+  // + kFusedWdPad band rows after the last chunk: k_grid_fused loads NQ band steps' weights of every chunk unclamped
+  const size_t wbytes = sizeof(double) * ((size_t)n_chunks * vmax + kFusedWdPad) * kGridTT;
   HIPCHK(c, G.wd.ensure(wbytes), "grid weights alloc");
   HIPCHK(c, hipMemsetAsync(G.wd.p, 0, wbytes, c->stream), "grid weights memset");
   std::vector<double> gx, gw;
@@ -1397,34 +1403,39 @@ int grid_build(fpta_ctx* c, Layout& L) {
     G.grid_vals += (double)L.P * gs->nf;
     G.fma_grid = G.fma_dft + G.fma_interp;
   }
-  // k_grid_fused: the grids of kFusedReal realizations (n_seg <= kFusedMaxSig, every 32-row DFT chunk one wave's job,
-  // band steps <= 16) and the coefficient staging each fit in LDS; the staging lies under the grids (the kernel
-  // writes the grids after its last staging read)
+  // k_grid_fused: the grids of kFusedReal realizations plus the draw ring fit in LDS, n_seg <= kFusedMaxSig, and every
+  // 32-row DFT chunk is one DFT wave's job
   {
-    int32_t jobs = 0, rows = 0, stage = 0;
+    int32_t jobs = 0, rows = 0;
     bool ok = n_seg <= kFusedMaxSig;
     for (int32_t s = 0; s < n_seg && ok; ++s) {
       const GridSeg* gs = G.segs[s];
       ok = gs->nf % 4 == 0 && gs->ldq == (gs->nf / 4 + 32) / 32 * 32;
       G.fused_lrow0.push_back(rows);
-      G.fused_stage.push_back(stage);
       jobs += (gs->nf / 4 + 32) / 32;
       rows += gs->nf;
-      stage += 2 * gs->ntq * kFusedReal * 2;
     }
-    const size_t lds = sizeof(double) * std::max<size_t>((size_t)rows * kFusedPitch, (size_t)stage);
-    ok = ok && jobs <= kFusedWaves && lds <= (size_t)kFusedLdsMax;
+    const size_t lds = sizeof(double) * ((size_t)rows * kFusedPitch + 2 * kFusedMaxSig * kFusedSlot) + 16;
+    for (const std::vector<int32_t>& m : G.members) ok = ok && m.size() <= (size_t)kDftGenTerms;
+    ok = ok && jobs <= kFusedDW && lds <= (size_t)kFusedLdsMax;
     if (ok) {
-      std::vector<int32_t> lrt((size_t)n_chunks * vmax);
+      // [n_chunks][4][fq]: band row 4 q + j of a chunk at [j][q] (a lane's rows of consecutive steps contiguous: 16-byte
+      // loads), fq = the band steps rounded up to 4 and at least kFusedNQ; steps past the chunk's repeat its first row
+      const int32_t fq = std::max(kFusedNQ, (vmax / 4 + 3) & ~3);
+      std::vector<int32_t> band_row(vmax);
+      std::vector<int32_t> lrt((size_t)n_chunks * 4 * fq);
       for (int32_t ci = 0; ci < n_chunks; ++ci) {
-        int32_t* r = lrt.data() + (size_t)ci * vmax;
         int32_t v = 0;
         for (int32_t s = 0; s < n_seg; ++s)
           for (int32_t i = 0; i < band_n[s][ci]; ++i)
-            r[v++] = G.fused_lrow0[s] + (int32_t)(((band_lo[s][ci] + i) % nf[s] + nf[s]) % nf[s]);
-        for (; v < vmax; ++v) r[v] = r[0];
+            band_row[v++] = G.fused_lrow0[s] + (int32_t)(((band_lo[s][ci] + i) % nf[s] + nf[s]) % nf[s]);
+        for (; v < vmax; ++v) band_row[v] = band_row[0];
+        int32_t* r = lrt.data() + (size_t)ci * 4 * fq;
+        for (int32_t j = 0; j < 4; ++j)
+          for (int32_t q = 0; q < fq; ++q) r[j * fq + q] = 4 * q + j < vmax ? band_row[4 * q + j] : band_row[0];
       }
       if ((rc = upload(c, G.frows, lrt.data(), sizeof(int32_t) * lrt.size(), "fused LDS rows"))) return rc;
+      G.fused_fq = fq;
       G.fused_lds = lds;
     }
     G.fused_ok = ok;
@@ -1683,7 +1694,6 @@ int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad, bool pipe = fa
       fs.nf = gs->nf;
       fs.nm = d.nm;
       fs.lrow0 = G.fused_lrow0[s];
-      fs.stage = G.fused_stage[s];
       fs.n_rc = (gs->nf / 4 + 32) / 32;
       if (grid_gen_fused(c, L, (size_t)s)) {  // k_grid_dft_gen's terms: the anchor, then the others in layout order
         std::vector<int32_t> order{G.anchor[s]};
@@ -1706,11 +1716,18 @@ int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad, bool pipe = fa
         fs.n_terms = 1;
       }
     }
+    f.ring_off = (G.fused_lrow0.back() + G.segs.back()->nf) * kFusedPitch;
     f.lrows = G.frows.as<int32_t>();
+    f.fq = G.fused_fq;
     f.psr_c0 = G.psr_c0.as<int32_t>();
     f.real0 = c->blk_real0;
     f.k0 = c->blk_k0;
     f.k1 = c->blk_k1;
+#ifdef FPTA_FUSED_PROF
+    HIPCHK(c, c->dbg_a.ensure(sizeof(unsigned long long) * 8 * 8 * 4096), "fused profile alloc");
+    HIPCHK(c, hipMemsetAsync(c->dbg_a.p, 0, sizeof(unsigned long long) * 8 * 8 * 4096, c->stream), "profile memset");
+    f.prof = c->dbg_a.as<unsigned long long>();
+#endif
     HIPCHK(c, launch_grid_fused(c->stream, a, band, f, nq, G.fused_lds), "k_grid_fused launch");
   } else if (psr) {
     kind = G.vmax <= 16 ? 6 : 7;  // launch_grid_interp_psr: NQ = 4 or 8 band steps
@@ -2794,6 +2811,16 @@ int fpta_batch_grid_info(fpta_ctx* c, double* out) {
 }
 
 const char* fpta_batch_path_reason(const fpta_ctx* c) { return c ? c->path_reason.c_str() : ""; }
+
+#ifdef FPTA_FUSED_PROF
+// k_grid_fused's per-wave cycle counters of the last fused block ([4096 workgroups][8 waves][8]; -DFPTA_FUSED_PROF
+// variant builds only, tools/fused_prof.py)
+extern "C" int fpta_debug_fused_prof(fpta_ctx* c, unsigned long long* host, int64_t n) {
+  if (!c || !host || n <= 0 || !c->dbg_a.p || (size_t)n * 8 > c->dbg_a.cap) return FPTA_EINVAL;
+  HIPCHK(c, hipMemcpy(host, c->dbg_a.p, (size_t)n * 8, hipMemcpyDeviceToHost), "profile download");
+  return FPTA_OK;
+}
+#endif
 
 int fpta_debug_fill_out(fpta_ctx* c, double value) {
   if (!c) return fail(nullptr, FPTA_EINVAL, "null ctx");

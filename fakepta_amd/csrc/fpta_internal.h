@@ -188,20 +188,28 @@ hipError_t launch_grid_interp_wr(hipStream_t st, const SynthArgs& a, const GridB
 // of each pulsar. Bit-identical to k_grid_dft_mfma + k_grid_interp_mfma.
 hipError_t launch_grid_interp_psr(hipStream_t st, const SynthArgs& a, const GridBand& band, const GridSegDev& gs,
                                   const int32_t* psr_grp, int32_t P, int32_t R_pad);
-// Fused per-pulsar synthesis (k_grid_fused, grid_fused.hip): a workgroup owns one pulsar x kFusedReal realizations,
-// draws every grid signal's coefficients into LDS (k_grid_dft_gen's terms and order), runs each signal's quarter-range
-// DFT on fp64 MFMA into an LDS grid (k_grid_dft_gen's steps and butterfly) and interpolates the pulsar's chunks from
-// it (k_grid_interp_ws's MFMA steps): no grid buffer, no DFT launch, bit-identical to the two-kernel path.
-constexpr int kFusedMaxSig = 4;   // grid signals
-constexpr int kFusedReal = 32;    // realizations per workgroup (two 16-realization MFMA tiles)
-constexpr int kFusedWaves = 8;    // waves per workgroup; at most this many DFT jobs (32-row chunks, all signals)
-constexpr int kFusedPitch = 32;   // doubles per LDS grid row
+// Fused per-pulsar synthesis (k_grid_fused, grid_fused.hip): persistent workgroups, each walking items = (pulsar,
+// kFusedReal realizations). Per item, kFusedDW DFT waves draw every grid signal's coefficients (k_grid_dft_gen's terms
+// and order) through a two-slot LDS ring and run the signal's quarter-range DFT on fp64 MFMA into registers (one
+// 32-row chunk each); kFusedIW interpolation waves meanwhile interpolate the previous item's chunks from its LDS grid
+// (k_grid_interp_ws's MFMA steps). At the item boundary the DFT waves write the next grid. No grid buffer, no DFT
+// launch; bit-identical to the two-kernel path.
+constexpr int kFusedMaxSig = 2;    // grid signals (the draw ring holds a group of each)
+constexpr int kFusedReal = 32;     // realizations per item (two 16-realization MFMA tiles)
+constexpr int kFusedPitch = 32;    // doubles per LDS grid row
+constexpr int kFusedIW = 4;        // interpolation waves per workgroup
+constexpr int kFusedDW = 4;        // DFT waves per workgroup = DFT jobs (32-row quarter-range chunks) at most
+constexpr int kFusedGroupModes = 16;  // modes per draw group: two 4-mode k-steps of both parities
+constexpr int kFusedSlot = kFusedGroupModes * kFusedReal * 2;  // doubles per signal of a ring slot [16 modes][32][cos, sin]
 constexpr int kFusedLdsMax = 160 * 1024;
+constexpr int kFusedNQ = 12;       // band steps whose operands an interpolation wave holds (a wider chunk: the rest one
+                                   // step at a time)
+constexpr int kFusedWdPad = 4 * kFusedNQ;  // band rows of zero weights past the last chunk (GridPlan::wd)
+constexpr int kFusedTerms = 2;     // members of a grid signal whose inputs the DFT waves prefetch (the others: inline)
 struct FusedSig {
   const double* tq;  // quarter-range tables [4][ntq][ldq] (GridSegDev::tq)
   int32_t ldq, ntq, nf, nm;  // nm: the anchor's padded modes
   int32_t lrow0;     // first LDS grid row of the signal
-  int32_t stage;     // LDS offset (doubles) of its coefficients [2 ntq][kFusedReal][cos, sin]
   int32_t n_rc;      // 32-row chunks of its quarter range (one DFT job each)
   int32_t n_terms;   // as DftGenArgs: generated (per-pulsar) and loaded (coefficient-buffer) terms, summation order
   int32_t term_kind[kDftGenTerms];
@@ -213,13 +221,16 @@ struct FusedSig {
 struct FusedArgs {
   FusedSig s[kFusedMaxSig];
   int32_t n_sig;
-  const int32_t* lrows;   // [n_chunks][vmax] LDS grid row of each band row
+  int32_t ring_off;       // LDS offset (doubles) of the draw ring (past the grids); a sync word follows it
+  const int32_t* lrows;   // [n_chunks][4][fq] LDS grid row of band row 4 q + j at [j][q]
+  int32_t fq;             // band steps per (chunk, j) in lrows (a multiple of 4, >= kFusedNQ)
   const int32_t* psr_c0;  // [P + 1] first chunk of each pulsar
   int64_t real0;          // the batch's first realization (Philox counter)
   uint32_t k0, k1;
+  unsigned long long* prof;  // -DFPTA_FUSED_PROF builds only: per-wave cycle counters [gridDim][8 waves][8]; else null
 };
 // nq_max: band steps of the widest chunk (vmax / 4; the kernel holds up to 12 steps' operands and takes a wider chunk's
-// in turns); lds_bytes: max(grid rows, coefficient staging) x their sizes
+// in turns); lds_bytes: grids + ring + sync word
 hipError_t launch_grid_fused(hipStream_t st, const SynthArgs& a, const GridBand& band, const FusedArgs& f,
                              int32_t nq_max, size_t lds_bytes);
 // Storer-wave variant: compute waves hand finished sums to storer waves through LDS; every block kind (white / ECORR

@@ -19,6 +19,12 @@ template <class T>
 __device__ __forceinline__ T ld_uniform(const T* p) {
   return *(const __attribute__((address_space(4))) T*)p;
 }
+// A per-lane read through the global address space: a pointer chosen among several (a select or a branch) is generic,
+// and a generic (flat) load counts on both vmcnt and lgkmcnt, so every LDS wait after it would also wait for it.
+template <class T>
+__device__ __forceinline__ T ld_global(const T* p) {
+  return *(const __attribute__((address_space(1))) T*)p;
+}
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ int4 ld_uniform4(const void* p) {
   const i32x4 v = ld_uniform((const i32x4*)p);

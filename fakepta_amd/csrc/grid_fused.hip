@@ -1,25 +1,29 @@
-// k_grid_fused: the whole gridded synthesis of one pulsar x kFusedReal realizations in one workgroup (C2: RN + GWB in
-// one grid signal of nf = 124 points, DM in one of nf = 380; 129 KB of LDS grid for 32 realizations).
+// k_grid_fused: the whole gridded synthesis of items = (pulsar, kFusedReal realizations) in persistent workgroups (C2:
+// RN + GWB in one grid signal of nf = 124 points, DM in one of nf = 380; 129 KB of LDS grid per item).
 //
 // The two-kernel path writes every grid (C2: 0.41 GB per block of 1024 realizations) to HBM from k_grid_dft_gen and
 // reads it back in k_grid_interp_ws: with the 1.64 GB of residuals, 2.5 GB of HBM traffic per block, and the DFTs of
 // block b + 1 co-run beside the interpolation of block b on the leftover registers of one wave slot per SIMD. Here the
-// grid lives in LDS only; HBM sees the residual stores, the interpolation weights (read once per pulsar per XCD, the
-// 32 realization blocks of a pulsar run side by side on one XCD) and the mixed common coefficients.
+// grid lives in LDS only; HBM sees the residual stores, the interpolation weights (read once per pulsar per XCD: the 32
+// items of a pulsar run side by side on one XCD) and the mixed common coefficients.
 //
-// Phases of a workgroup (8 waves, one workgroup per CU):
-//  1. draws: every thread makes (mode, realization pair) coefficient pairs of every grid signal into LDS staging,
-//     [2 ntq][32 realizations][cos, sin] per signal, with grid_term_coefs (k_grid_dft_gen's terms and order);
-//  2. DFT: wave w takes job w = (grid signal, 32-row chunk rc of its quarter range) for both 16-realization tiles:
-//     k_grid_dft_gen's MFMA k-steps per parity (A = table row pairs from global / L2, B = the (cos, sin) pair of a
-//     realization from LDS), the accumulators kept in registers; a barrier (the staging may lie under the grids), then
-//     k_grid_dft_gen's butterfly writes grid rows j, H + j, H - j, nf - j into LDS row lrow0 + j;
-//  3. interpolation: wave w takes the pulsar's chunks c0 + w, c0 + w + 8, ...: per band step A = the dbl2 pair of
-//     realizations (2 lr, 2 lr + 1) of LDS row lrows[c][4 q + lg] (one ds_read_b128), B = the weight pair of TOAs
-//     (2 lr, 2 lr + 1) from global memory, four MFMAs (even / odd TOA x realization tile) as k_grid_interp_ws; the next
-//     chunk's weights are loaded before this chunk's eight 16-byte stores enter the vmcnt queue.
+// A workgroup (one per CU) has two roles, one wave of each per SIMD:
+//  * DFT waves (kFusedDW): build item k + 1's grids while item k is interpolated. The coefficients of a grid signal are
+//    drawn in groups of 16 modes x 32 realizations (one (mode, realization pair) per lane, grid_term_coefs:
+//    k_grid_dft_gen's terms and order) into a two-slot LDS ring: while every wave's MFMAs read group g, the waves draw
+//    group g + 1 into the other slot; the DFT waves meet at an LDS counter after each group (the interpolation waves
+//    take no part). Wave d's job is the d-th 32-row chunk of the quarter ranges: k_grid_dft_gen's MFMA k-steps for both
+//    realization tiles (A = table row pairs from global memory / L2, B = the (cos, sin) pair of a realization from the
+//    ring), the accumulators kept in registers until the item boundary, then k_grid_dft_gen's butterfly writes grid rows
+//    j, H + j, H - j, nf - j into LDS.
+//  * interpolation waves (kFusedIW): the item's chunks c0 + w, c0 + w + kFusedIW, ...: per band step A = the dbl2 pair
+//    of realizations (2 lr, 2 lr + 1) of LDS row lrows[c][4 q + lg] (one ds_read_b128), B = the weight pair of TOAs
+//    (2 lr, 2 lr + 1) from global memory, four MFMAs (even / odd TOA x realization tile) as k_grid_interp_ws; the next
+//    chunk's weights are loaded before this chunk's eight 16-byte stores enter the vmcnt queue.
+// Two s_barriers per item separate the roles: A (item k interpolated, item k + 1's accumulators ready), after which the
+// DFT waves overwrite the grids, and B (the new grids written).
 // Every value is made by the same operations in the same order as k_grid_dft_gen (or k_grid_dft_mfma from the merged
-// anchor columns) + k_grid_interp_ws: the block is bit-identical to theirs (tests/test_gpu_grid.py).
+// anchor columns) + k_grid_interp_ws: the block is bit-identical to theirs (tests/test_gpu_fused.py).
 #include <hip/hip_runtime.h>
 #include <algorithm>
 
@@ -27,168 +31,443 @@
 
 namespace fpta {
 
-template <int NQ>
-__global__ __launch_bounds__(64 * kFusedWaves, 1) void k_grid_fused(SynthArgs a, GridBand band, FusedArgs f,
-                                                                    int32_t n_rb, int32_t n_items) {
-  static_assert(kFusedReal == 32 && kFusedPitch == 32, "two realization tiles per LDS grid row");
-  extern __shared__ __attribute__((aligned(16))) double lds[];
-  const int per = (n_items + 7) >> 3;
-  const int item = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);  // a pulsar's blocks on one XCD
-  if (item >= n_items) return;  // the whole workgroup, before its first barrier
-  const int p = item / n_rb, rb = item - p * n_rb;
-  const int r0 = rb * kFusedReal;
+#ifndef FPTA_FUSED_CUT
+#define FPTA_FUSED_CUT 0  // diagnostic variant builds only (make variant DEFS=-DFPTA_FUSED_CUT=n): 1 no DFT builds, 2 no interpolation
+#endif
+
+namespace {
+
+// -DFPTA_FUSED_PROF (make variant; tools/fused_prof.py): per-wave cycle counters of the kernel's phases
+#ifdef FPTA_FUSED_PROF
+struct Prof {
+  unsigned long long v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long t = 0;
+  __device__ __forceinline__ void start() { t = clock64(); }
+  __device__ __forceinline__ void lap(int i) {
+    const unsigned long long n = clock64();
+    v[i] += n - t;
+    t = n;
+  }
+  __device__ __forceinline__ void count(int i) { ++v[i]; }
+  __device__ __forceinline__ void flush(unsigned long long* out, int wave) {
+    if (out && (threadIdx.x & 63) == 0)
+      for (int i = 0; i < 8; ++i) out[((int64_t)blockIdx.x * 8 + wave) * 8 + i] = v[i];
+  }
+};
+#else
+struct Prof {
+  __device__ __forceinline__ void start() {}
+  __device__ __forceinline__ void lap(int) {}
+  __device__ __forceinline__ void count(int) {}
+  __device__ __forceinline__ void flush(unsigned long long*, int) {}
+};
+#endif
+
+__device__ __forceinline__ void fused_barrier() { asm volatile("s_barrier" ::: "memory"); }  // no vmcnt(0) fence
+__device__ __forceinline__ void fused_wait_lgkm0() { __builtin_amdgcn_s_waitcnt(15 | (3 << 14) | (7 << 4)); }
+
+// A workgroup's items: those of XCD x (workgroup b runs on XCD b % 8) are a contiguous range, strided over its
+// workgroups, so the items of one pulsar run side by side on one XCD
+struct FusedItems {
+  int first, stride, count;
+  __device__ __forceinline__ explicit FusedItems(int n_items) {
+    const int per = (n_items + 7) >> 3;
+    const int x = blockIdx.x & 7;
+    stride = gridDim.x >> 3;
+    first = x * per + (int)(blockIdx.x >> 3);
+    const int end = min(n_items, (x + 1) * per);
+    count = first < end ? (end - first + stride - 1) / stride : 0;
+  }
+  __device__ __forceinline__ int item(int k) const { return first + k * stride; }
+};
+
+}  // namespace
+
+template <int NQ, bool ODD>
+__global__ __launch_bounds__(64 * (kFusedIW + kFusedDW), 1) void k_grid_fused(SynthArgs a, GridBand band, FusedArgs f,
+                                                                             int32_t n_rb, int32_t n_items) {
+  static_assert(kFusedReal == 32 && kFusedPitch == 32 && kFusedGroupModes * kFusedReal / 2 == 64 * kFusedDW,
+                "two realization tiles; one (mode, realization pair) of a 16-mode group per DFT lane");
+  extern __shared__ __attribute__((aligned(16))) double lds[];  // [grid rows][32] | ring [2][kFusedSlot] | sync word
+  const FusedItems items(n_items);
+  if (items.count == 0) return;  // the whole workgroup, before its first barrier
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const int lr = lane & 15, lg = lane >> 4;
-
-  // 1. coefficients of every grid signal, a realization pair per thread and mode
-  for (int s = 0; s < f.n_sig; ++s) {
-    const FusedSig& fs = f.s[s];
-    double* __restrict__ bs_lds = lds + fs.stage;
-    const int n_items_s = 2 * fs.ntq * (kFusedReal / 2);
-    for (int idx = threadIdx.x; idx < n_items_s; idx += 64 * kFusedWaves) {
-      const int m = idx >> 4, rl = 2 * (idx & 15);
-      double bc[2], bs[2];
-      grid_term_coefs(fs, fs.nm, a.coef, a.K, a.R_pad, a.n_real, f.real0, f.k0, f.k1, p, m, r0 + rl, bc, bs);
-      *(dbl2*)(bs_lds + 2 * (m * kFusedReal + rl)) = dbl2{bc[0], bs[0]};
-      *(dbl2*)(bs_lds + 2 * (m * kFusedReal + rl + 1)) = dbl2{bc[1], bs[1]};
-    }
-  }
+  double* __restrict__ ring = lds + f.ring_off;
+  uint32_t* sync = (uint32_t*)(ring + 2 * kFusedMaxSig * kFusedSlot);
+  if (threadIdx.x == 0) *sync = 0u;
   __syncthreads();
 
-  // 2. DFT job of this wave: grid signal js, quarter-range rows 32 jrc .. 32 jrc + 31, both realization tiles
-  int js = -1, jrc = 0;
-  {
-    int j = wave;
-    for (int s = 0; s < f.n_sig; ++s) {
-      if (js < 0 && j < f.s[s].n_rc) {
-        js = s;
-        jrc = j;
-      }
-      j -= f.s[s].n_rc;
-    }
-  }
-  js = __builtin_amdgcn_readfirstlane(js);
-  jrc = __builtin_amdgcn_readfirstlane(jrc);
-  d4 C[2][2][2], S[2][2][2];  // [parity: 0 odd k, 1 even k][row tile h: rows 2 i + h][realization tile t]
-  if (js >= 0) {
-    const FusedSig& fs = f.s[js];
-    const int j0 = 32 * jrc;
-    const double* __restrict__ bsrc = lds + fs.stage;
-    const int64_t tstride = (int64_t)fs.ntq * fs.ldq;
-    const int n_par[2] = {(fs.nm + 1) >> 1, fs.nm >> 1};  // modes of odd k (m = 2 t) and of even k (m = 2 t + 1)
+  if (wave >= kFusedIW) {
+    // ---------------------------------------------------------------- DFT waves
+    const int dw = wave - kFusedIW;
+    int js = -1, jrc = 0;  // this wave's job: grid signal js, quarter-range rows 32 jrc .. 32 jrc + 31
+    {
+      int j = dw;
 #pragma unroll
-    for (int par = 0; par < 2; ++par) {
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int t = 0; t < 2; ++t) C[par][h][t] = S[par][h][t] = d4{0.0, 0.0, 0.0, 0.0};
-      const double* __restrict__ tc = fs.tq + (int64_t)(2 * par) * tstride + (int64_t)lg * fs.ldq + j0 + 2 * lr;
-      const double* __restrict__ ts = tc + tstride;
-      const int nq = (n_par[par] + 3) >> 2;
-      // operands of step q + 1 in flight while step q's MFMAs run (two sets, alternating)
-      struct Ops {
-        dbl2 ac, as, b[2];
-      };
-      auto fetch = [&](int q, Ops& o) {
-        const int qq = min(q, nq - 1);
-        o.ac = *(const dbl2*)(tc + (int64_t)(4 * qq) * fs.ldq);
-        o.as = *(const dbl2*)(ts + (int64_t)(4 * qq) * fs.ldq);
-        const double* bm = bsrc + 2 * ((2 * (4 * qq + lg) + par) * kFusedReal + lr);
-        o.b[0] = *(const dbl2*)bm;
-        o.b[1] = *(const dbl2*)(bm + 2 * 16);
-      };
-      auto mfma = [&](const Ops& o) {
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-          C[par][0][t] = __builtin_amdgcn_mfma_f64_16x16x4f64(o.ac.x, o.b[t].x, C[par][0][t], 0, 0, 0);
-          C[par][1][t] = __builtin_amdgcn_mfma_f64_16x16x4f64(o.ac.y, o.b[t].x, C[par][1][t], 0, 0, 0);
-          S[par][0][t] = __builtin_amdgcn_mfma_f64_16x16x4f64(o.as.x, o.b[t].y, S[par][0][t], 0, 0, 0);
-          S[par][1][t] = __builtin_amdgcn_mfma_f64_16x16x4f64(o.as.y, o.b[t].y, S[par][1][t], 0, 0, 0);
+      for (int s = 0; s < kFusedMaxSig; ++s) {
+        if (s < f.n_sig && js < 0 && j < f.s[s].n_rc) {
+          js = s;
+          jrc = j;
         }
+        if (s < f.n_sig) j -= f.s[s].n_rc;
+      }
+    }
+    js = __builtin_amdgcn_readfirstlane(js);
+    jrc = __builtin_amdgcn_readfirstlane(jrc);
+    Prof pf;  // DFT waves: 0 loads issue, 1 MFMA steps, 2 ring sync, 3 grid writes, 4 barriers, 5 iterations, 6 normals,
+              // 7 draw stores
+    pf.start();
+    uint32_t epoch = 0;
+    // every DFT wave's ring writes and reads so far are done (an LDS counter; the interpolation waves run on)
+    auto dsync = [&]() {
+      fused_wait_lgkm0();
+      if (lane == 0) __hip_atomic_fetch_add(sync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      epoch += kFusedDW;
+      while ((uint32_t)__builtin_amdgcn_readfirstlane(
+                 (int)__hip_atomic_load(sync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) < epoch)
+        __builtin_amdgcn_s_sleep(1);
+    };
+    // groups of 16 modes (two 4-mode k-steps of both parities) of grid signal s
+    auto n_groups = [&](int nm) { return (((((nm + 1) >> 1) + 3) >> 2) + 1) >> 1; };
+    int ng[kFusedMaxSig];
+    int n_it = 0;  // iterations per item: iteration g draws group g + 1 of every signal and runs group g's steps
+#pragma unroll
+    for (int s = 0; s < kFusedMaxSig; ++s) {
+      ng[s] = s < f.n_sig ? n_groups(f.s[s].nm) : 0;
+      n_it = max(n_it, ng[s]);
+    }
+    // this wave's job, hoisted: its table rows (parity 0 cos, t = lg, rows 32 jrc + 2 lr) and k-steps per parity
+    const FusedSig& jf = f.s[js < 0 ? 0 : js];
+    const int64_t jts = (int64_t)jf.ntq * jf.ldq, jld4 = 4 * (int64_t)jf.ldq;
+    const double* __restrict__ jtq = jf.tq + (int64_t)lg * jf.ldq + 32 * jrc + 2 * lr;
+    const int jnq0 = (((jf.nm + 1) >> 1) + 3) >> 2, jnq1 = ((jf.nm >> 1) + 3) >> 2;
+    const int jng = js < 0 ? 0 : (jnq0 + 1) >> 1;
+    // [parity: 0 odd k, 1 even k][row tile h: rows 2 i + h][realization tile t]
+    d4 C[2][2][2], S[2][2][2];
+    // Group g of signal s: modes 16 g .. 16 g + 15 x realizations r0 .. r0 + 31, one (mode m, realization pair r) per
+    // lane, k_grid_dft_gen's coefficient (grid_term_coefs: the same operations) in three parts:
+    //  draw_load: every term slot's inputs, two 16-byte loads each whatever the term (a fixed count keeps the compiler's
+    //             vmcnt waits for the table operands exact): a generated term's amplitude, a loaded term's columns;
+    //             issued with the tables of the steps before them, so the latencies overlap;
+    //  draw_normals: the generated terms' normals (no memory);
+    //  draw_store: amp * z (rounded) and the loaded values summed in the terms' order, into the ring.
+    // The signal index is a constant wherever these run (loops over kFusedMaxSig unrolled): the descriptor's fields are
+    // scalar loads at fixed kernel-argument offsets, not re-read by computed index in every group.
+    const int didx = dw * 64 + lane;
+    const int dmm = didx >> 4, drl = 2 * (didx & 15);
+    struct DrawIn {
+      dbl2 x0[kFusedTerms], x1[kFusedTerms];  // generated: x0.x amplitude pair; loaded: x0 cos pair, x1 sin pair
+    };
+    auto draw_load = [&](const FusedSig& fs, int g, int p, int r0, DrawIn& in) {
+      const int m = kFusedGroupModes * g + dmm, r = r0 + drl;
+#pragma unroll
+      for (int i = 0; i < kFusedTerms; ++i) {
+        const bool on = i < fs.n_terms;
+        const int nmi = on ? fs.term_nm[i] : 2;
+        const int mi = min(m, nmi - 1);  // clamped: a mode past the term's is never used
+        const double* src0;
+        int64_t step;
+        if (on && fs.term_kind[i] == 1) {
+          src0 = a.coef + ((int64_t)p * a.K + fs.term_col0[i] + 2 * mi) * a.R_pad + r;
+          step = a.R_pad;
+        } else {  // the amplitude pair (mi, mi + 1) of a generated term: .x is amp[mi] (rows are padded to even nm)
+          src0 = (on ? fs.term_amp[i] : a.coef) + (int64_t)p * nmi + (mi & ~1);
+          step = 0;
+        }
+        in.x0[i] = ld_global((const dbl2*)src0);
+        in.x1[i] = ld_global((const dbl2*)(src0 + step));
+      }
+    };
+    auto draw_finish = [&](const FusedSig& fs, int g, int p, int r0, double* __restrict__ slot_s, const DrawIn& in) {
+      const int m = kFusedGroupModes * g + dmm, r = r0 + drl;
+      const uint64_t gr = (uint64_t)(f.real0 + r);
+      double bc[2] = {0.0, 0.0}, bs[2] = {0.0, 0.0};
+      bool first = true;
+      auto add = [&](bool use, const double (&pc)[2], const double (&ps)[2]) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          bc[h] = use ? (first ? pc[h] : bc[h] + pc[h]) : bc[h];
+          bs[h] = use ? (first ? ps[h] : bs[h] + ps[h]) : bs[h];
+        }
+        first = first && !use;
       };
-      if (nq > 0) {
-        Ops o0, o1;
-        fetch(0, o0);
-        for (int q = 0; q < nq; q += 2) {
-          fetch(q + 1, o1);
-          mfma(o0);
-          if (q + 1 < nq) {
-            fetch(q + 2, o0);
-            mfma(o1);
+      const bool ok0 = r < a.n_real, ok1 = r + 1 < a.n_real;  // padding realizations: zero, as k_gen writes them
+      auto normals = [&](int seg, double (&z)[4]) {
+        if (!ODD) {  // r0 and r are even: the first realization's parity is the launch's
+          gp_pair2((uint32_t)m, (uint32_t)p, (uint32_t)seg, gr, f.k0, f.k1, z);
+        } else {
+          gp_normal2((uint32_t)m, (uint32_t)p, (uint32_t)seg, gr, f.k0, f.k1, z[0], z[1]);
+          gp_normal2((uint32_t)m, (uint32_t)p, (uint32_t)seg, gr + 1, f.k0, f.k1, z[2], z[3]);
+        }
+        z[0] = ok0 ? z[0] : 0.0;
+        z[1] = ok0 ? z[1] : 0.0;
+        z[2] = ok1 ? z[2] : 0.0;
+        z[3] = ok1 ? z[3] : 0.0;
+      };
+#pragma unroll
+      for (int i = 0; i < kFusedTerms; ++i) {
+        if (i >= fs.n_terms) continue;
+        double pc[2], ps[2];
+        if (fs.term_kind[i] == 0) {
+          double z[4];
+          normals(fs.term_seg[i], z);
+          const double amp = (m & 1) ? in.x0[i].y : in.x0[i].x;
+          pc[0] = opaque(amp * z[0]);
+          ps[0] = opaque(amp * z[1]);
+          pc[1] = opaque(amp * z[2]);
+          ps[1] = opaque(amp * z[3]);
+        } else {
+          pc[0] = in.x0[i].x;
+          pc[1] = in.x0[i].y;
+          ps[0] = in.x1[i].x;
+          ps[1] = in.x1[i].y;
+        }
+        add(m < fs.nm && m < fs.term_nm[i], pc, ps);
+      }
+      // members past kFusedTerms (a grid signal of three or more, e.g. coalesced RN + DM + GWB at one radio frequency):
+      // loaded and drawn here, in order, with the same operations
+      for (int i = kFusedTerms; i < fs.n_terms; ++i) {
+        const int mi = min(m, fs.term_nm[i] - 1);
+        double pc[2], ps[2];
+        if (fs.term_kind[i] == 0) {
+          double z[4];
+          normals(fs.term_seg[i], z);
+          const double amp = ld_global(fs.term_amp[i] + (int64_t)p * fs.term_nm[i] + mi);
+          pc[0] = opaque(amp * z[0]);
+          ps[0] = opaque(amp * z[1]);
+          pc[1] = opaque(amp * z[2]);
+          ps[1] = opaque(amp * z[3]);
+        } else {
+          const double* cp = a.coef + ((int64_t)p * a.K + fs.term_col0[i] + 2 * mi) * a.R_pad + r;
+          const dbl2 vc = ld_global((const dbl2*)cp), vs = ld_global((const dbl2*)(cp + a.R_pad));
+          pc[0] = vc.x;
+          pc[1] = vc.y;
+          ps[0] = vs.x;
+          ps[1] = vs.y;
+        }
+        add(m < fs.nm && m < fs.term_nm[i], pc, ps);
+      }
+      double* __restrict__ dst = slot_s + 2 * (dmm * kFusedReal + drl);
+      *(dbl2*)dst = dbl2{bc[0], bs[0]};
+      *(dbl2*)(dst + 2) = dbl2{bc[1], bs[1]};
+    };
+    // ring slot k: [signal][16 modes][32 realizations][cos, sin]
+    auto slot_of = [&](int k, int s) { return ring + ((k & 1) * kFusedMaxSig + s) * kFusedSlot; };
+    // the table operands of this wave's k-steps q = 2 g, 2 g + 1 (clamped: a step past the parity's is never used)
+    struct Tabs {
+      dbl2 ac[2][2], as[2][2];  // [k-step h2][parity]
+    };
+    auto tables = [&](int g, Tabs& tb) {
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2) {
+        const int q = max(0, min(2 * g + h2, jnq0 - 1));
+#pragma unroll
+        for (int par = 0; par < 2; ++par) {
+          const double* __restrict__ tc = jtq + (int64_t)(2 * par) * jts + q * jld4;
+          tb.ac[h2][par] = ld_global((const dbl2*)tc);
+          tb.as[h2][par] = ld_global((const dbl2*)(tc + jts));
+        }
+      }
+    };
+    // k_grid_dft_gen's MFMA k-steps q = 2 g, 2 g + 1 of the job on the job signal's group g in ring slot g
+    auto steps = [&](int g, const Tabs& tb) {
+      const double* __restrict__ bsrc = slot_of(g, js);
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2) {
+        const int q = 2 * g + h2;
+#pragma unroll
+        for (int par = 0; par < 2; ++par) {
+          if (q >= (par ? jnq1 : jnq0)) continue;
+          const dbl2 ac = tb.ac[h2][par], as = tb.as[h2][par];
+          // mode 16 g + 2 (4 h2 + lg) + par = 2 (4 q + lg) + par, realizations lr and 16 + lr
+          const double* bm = bsrc + 2 * ((2 * (4 * h2 + lg) + par) * kFusedReal + lr);
+          const dbl2 b[2] = {*(const dbl2*)bm, *(const dbl2*)(bm + 2 * 16)};
+#pragma unroll
+          for (int t = 0; t < 2; ++t) {
+            C[par][0][t] = __builtin_amdgcn_mfma_f64_16x16x4f64(ac.x, b[t].x, C[par][0][t], 0, 0, 0);
+            C[par][1][t] = __builtin_amdgcn_mfma_f64_16x16x4f64(ac.y, b[t].x, C[par][1][t], 0, 0, 0);
+            S[par][0][t] = __builtin_amdgcn_mfma_f64_16x16x4f64(as.x, b[t].y, S[par][0][t], 0, 0, 0);
+            S[par][1][t] = __builtin_amdgcn_mfma_f64_16x16x4f64(as.y, b[t].y, S[par][1][t], 0, 0, 0);
           }
         }
       }
-    }
-  }
-  __syncthreads();  // every staging read is done: the grids may overlay the staging
-  if (js >= 0) {
-    const FusedSig& fs = f.s[js];
-    const int j0 = 32 * jrc;
-    const int nf = fs.nf, Q = nf >> 2, H = nf >> 1;
-    double* __restrict__ gcol = lds + (int64_t)fs.lrow0 * kFusedPitch + lr;
+    };
+    // item k's accumulators of this wave's job: iteration g draws group g + 1 of every signal into ring slot g + 1 and
+    // runs the job signal's group g from slot g; all loads of an iteration are issued before its steps
+    auto build = [&](int k) {
+      const int item = items.item(k);
+      const int p = item / n_rb, r0 = (item - p * n_rb) * kFusedReal;
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
+      for (int par = 0; par < 2; ++par)
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int j = j0 + 2 * (lg + 4 * g) + h;
-        if (j > Q) continue;
+        for (int h = 0; h < 2; ++h)
 #pragma unroll
-        for (int t = 0; t < 2; ++t) {
-          const double oc = C[0][h][t][g], os = S[0][h][t][g], ec = C[1][h][t][g], es = S[1][h][t][g];
-          const double pe = ec + es, me = ec - es, po = oc + os, mo = oc - os;
-          gcol[j * kFusedPitch + 16 * t] = pe + po;
-          gcol[(H + j) * kFusedPitch + 16 * t] = pe - po;
-          if (j > 0 && j < Q) {
-            gcol[(H - j) * kFusedPitch + 16 * t] = me - mo;
-            gcol[(nf - j) * kFusedPitch + 16 * t] = me + mo;
-          }
-        }
+          for (int t = 0; t < 2; ++t) C[par][h][t] = S[par][h][t] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int s = 0; s < kFusedMaxSig; ++s) {
+        if (s >= f.n_sig) continue;
+        DrawIn in;
+        draw_load(f.s[s], 0, p, r0, in);
+        draw_finish(f.s[s], 0, p, r0, slot_of(0, s), in);
       }
+      pf.lap(7);
+      dsync();
+      pf.lap(2);
+      for (int g = 0; g < n_it; ++g) {
+        Tabs tb;
+        tables(g, tb);
+        DrawIn in[kFusedMaxSig];
+#pragma unroll
+        for (int s = 0; s < kFusedMaxSig; ++s)
+          draw_load(f.s[s], min(g + 1, max(ng[s], 1) - 1), p, r0, in[s]);  // an unused descriptor is a copy of the first
+        pf.lap(0);
+        if (g < jng) steps(g, tb);
+        pf.lap(1);
+#pragma unroll
+        for (int s = 0; s < kFusedMaxSig; ++s)
+          if (g + 1 < ng[s]) draw_finish(f.s[s], g + 1, p, r0, slot_of(g + 1, s), in[s]);
+        pf.lap(6);
+        dsync();
+        pf.lap(2);
+        pf.count(5);
+      }
+    };
+    auto write_grid = [&]() {
+      if (js >= 0) {
+        const int j0 = 32 * jrc;
+        const int nf = jf.nf, Q = nf >> 2, H = nf >> 1;
+        double* __restrict__ gcol = lds + (int64_t)jf.lrow0 * kFusedPitch + lr;
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int gg = 0; gg < 4; ++gg) {
+            const int j = j0 + 2 * (lg + 4 * gg) + h;
+            if (j > Q) continue;
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+              const double oc = C[0][h][t][gg], os = S[0][h][t][gg], ec = C[1][h][t][gg], es = S[1][h][t][gg];
+              const double pe = ec + es, me = ec - es, po = oc + os, mo = oc - os;
+              gcol[j * kFusedPitch + 16 * t] = pe + po;
+              gcol[(H + j) * kFusedPitch + 16 * t] = pe - po;
+              if (j > 0 && j < Q) {
+                gcol[(H - j) * kFusedPitch + 16 * t] = me - mo;
+                gcol[(nf - j) * kFusedPitch + 16 * t] = me + mo;
+              }
+            }
+          }
+      }
+      fused_wait_lgkm0();
+    };
+    // item k + 1's draws and steps run while the interpolation waves read item k's grids (one build site: the
+    // draws are most of the kernel's code)
+    for (int k = -1; k < items.count; ++k) {
+      const bool next = k + 1 < items.count;
+      if (next && !(FPTA_FUSED_CUT & 1)) build(k + 1);
+      if (k >= 0) {
+        fused_barrier();  // A(k): item k is interpolated
+        pf.lap(4);
+      }
+      if (next) write_grid();
+      pf.lap(3);
+      fused_barrier();  // B(k): item k + 1's grids are written
+      pf.lap(4);
+    }
+    pf.flush(f.prof, wave);
+    return;
   }
-  __syncthreads();
 
-  // 3. the pulsar's chunks, wave w: c0 + w, c0 + w + kFusedWaves, ...
-  const int c_end = ld_uniform(f.psr_c0 + p + 1);
-  int c = ld_uniform(f.psr_c0 + p) + wave;
-  if (c >= c_end) return;
-  struct Ops {
-    int4 ci;
-    int nq;
-    dbl2 b[NQ];
-    int row[NQ];  // LDS offset (doubles) of band row 4 (q0 + q) + lg, realization pair 2 lr
+  // ------------------------------------------------------------------ interpolation waves
+  // Every operand of a chunk's band steps comes through vector loads (vmcnt): a scalar load waits lgkmcnt(0) (scalar
+  // loads return out of order), which also waits for the LDS grid reads, and a lane select of four scalar rows
+  // compiles to divergent branches. The chunk table entries {first TOA, count, band rows} of an item's chunks for this
+  // wave sit in the lanes of one VGPR quad (ItemInfo::civ, lane i = the wave's i-th chunk, loaded one item ahead) and
+  // are read with readlane.
+  struct ItemInfo {
+    int p, r0, c0, n;  // pulsar, first realization, the wave's first chunk, the wave's chunks in the item
+    int64_t toa0;      // the pulsar's first TOA (residual column)
+    int4 civ;          // lane i: band.chunks[c0 + kFusedIW i] (i < min(n, 64))
   };
-  // operands of band steps q0 .. q0 + NQ - 1 of chunk cc (steps past nq re-load the last one, never used)
-  auto load = [&](int cc, int q0, Ops& o) {
-    o.ci = ld_uniform4(band.chunks + cc);
-    o.nq = __builtin_amdgcn_readfirstlane(o.ci.w) >> 2;
+  auto item_info = [&](int k, ItemInfo& it) {  // the loads of civ are left in flight
+    it.n = 0;
+    it.c0 = 0;
+    it.p = it.r0 = 0;
+    it.toa0 = 0;
+    if (k < items.count) {
+      const int item = items.item(k);
+      it.p = item / n_rb;
+      it.r0 = (item - it.p * n_rb) * kFusedReal;
+      const int cb = ld_uniform(f.psr_c0 + it.p) + wave, ce = ld_uniform(f.psr_c0 + it.p + 1);
+      it.toa0 = ld_uniform(a.offs + it.p);
+      it.c0 = cb;
+      it.n = cb < ce ? (ce - cb + kFusedIW - 1) / kFusedIW : 0;
+    }
+    const int cl = it.n > 0 ? it.c0 + kFusedIW * min(lane, it.n - 1) : 0;
+    const i32x4 v = *(const i32x4*)(band.chunks + cl);
+    it.civ = make_int4(v.x, v.y, v.z, v.w);
+  };
+  // {pulsar, first TOA, count, band rows} of the wave's i-th chunk of the item
+  auto chunk_info = [&](const ItemInfo& it, int i) {
+    if (i < 64)
+      return make_int4(it.p, __builtin_amdgcn_readlane(it.civ.y, i), __builtin_amdgcn_readlane(it.civ.z, i),
+                       __builtin_amdgcn_readlane(it.civ.w, i));
+    return ld_uniform4(band.chunks + it.c0 + kFusedIW * i);  // a pulsar of more than 256 chunks
+  };
+  struct Ops {
+    int4 ci;      // {pulsar, first TOA, count, band rows} (wave-uniform)
+    int c, nq;    // chunk, band steps (wave-uniform)
+    dbl2 b[NQ];   // weights of TOAs (2 lr, 2 lr + 1) at band row 4 (q0 + q) + lg
+    int row[NQ];  // LDS grid row of band row 4 (q0 + q) + lg
+  };
+  // operands of band steps 0 .. NQ - 1 of chunk cc, at constant offsets from two addresses (steps past nq read the
+  // next chunk's or the tables' padding rows: never used)
+  auto load = [&](int cc, int4 ci, Ops& o) {
+    o.ci = ci;
+    o.c = cc;
+    o.nq = ci.w >> 2;
     FPTA_DCHECK(o.nq > 0, "k_grid_fused band steps", o.nq, 1 << 20);
-    const int32_t* __restrict__ rt = f.lrows + (int64_t)cc * band.vmax;
+    const i32x4* __restrict__ rt = (const i32x4*)(f.lrows + ((int64_t)cc * 4 + lg) * f.fq);
     const double* __restrict__ wp = band.wd + ((int64_t)cc * band.vmax + lg) * kGridTT + 2 * lr;
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      const int qq = min(q0 + q, o.nq - 1);
-      const int4 r4 = ld_uniform4(rt + 4 * qq);
-      o.row[q] = (lg == 0 ? r4.x : lg == 1 ? r4.y : lg == 2 ? r4.z : r4.w) * kFusedPitch + 2 * lr;
-      o.b[q] = *(const dbl2*)(wp + 4 * kGridTT * qq);
+    for (int q4 = 0; q4 < NQ / 4; ++q4) {
+      const i32x4 r4 = rt[q4];
+      o.row[4 * q4] = r4.x;
+      o.row[4 * q4 + 1] = r4.y;
+      o.row[4 * q4 + 2] = r4.z;
+      o.row[4 * q4 + 3] = r4.w;
     }
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) o.b[q] = *(const dbl2*)(wp + 4 * kGridTT * q);
   };
-  Ops cur, nxt;
-  load(c, 0, cur);
-  d4 acc[2][2];  // [TOA parity][realization tile]
-  while (true) {
+  const int lds_lane = 2 * lr;  // this lane's realization pair in an LDS grid row
+  Prof pf;  // interpolation waves: 0 next-chunk loads, 1 MFMA steps, 2 stores, 3 barriers, 4 wide-chunk reloads, 5 chunks
+  pf.start();
+  // The chunk in cur (of the item at pulsar p, realizations r0 ..); the next one's operands (this item's, or the next
+  // item's first) are loaded into nxt first, so their latency hides behind this chunk's MFMAs and they precede this
+  // chunk's stores in the vmcnt queue.
+  // Loads are never conditional: a load on one side of a branch makes the compiler's vmcnt wait after the join count
+  // from the side without it, i.e. wait for nearly every load in flight (the next chunk's included). Without a next
+  // chunk the current one's operands are loaded again (never used).
+  auto chunk = [&](int p, int r0, int64_t toa0, Ops& cur, bool has_next, int c_next, int4 ci_next, Ops& nxt) {
+    if (FPTA_FUSED_CUT & 2) return;
+    pf.lap(6);
+    load(has_next ? c_next : cur.c, has_next ? ci_next : cur.ci, nxt);
+    pf.lap(0);
+    pf.count(5);
+    d4 acc[2][2];  // [TOA parity][realization tile]
 #pragma unroll
     for (int e = 0; e < 2; ++e)
 #pragma unroll
       for (int i = 0; i < 2; ++i) acc[e][i] = d4{0.0, 0.0, 0.0, 0.0};
-    for (int q0 = 0;; q0 += NQ) {
+    {
       // step q's A operand is read from LDS ahead of step q - 1's MFMAs (rows past nq are valid clamped rows)
-      dbl2 an = *(const dbl2*)(lds + cur.row[0]);
+      dbl2 an = *(const dbl2*)(lds + cur.row[0] * kFusedPitch + lds_lane);
 #pragma unroll
       for (int q = 0; q < NQ; ++q) {
-        if (q0 + q < cur.nq) {
+        if (q < cur.nq) {
           const dbl2 av = an;
-          if (q + 1 < NQ) an = *(const dbl2*)(lds + cur.row[q + 1]);
+          if (q + 1 < NQ) an = *(const dbl2*)(lds + cur.row[q + 1] * kFusedPitch + lds_lane);
           const dbl2 bv = cur.b[q];
           acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(av.x, bv.x, acc[0][0], 0, 0, 0);
           acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(av.y, bv.x, acc[0][1], 0, 0, 0);
@@ -196,63 +475,161 @@ __global__ __launch_bounds__(64 * kFusedWaves, 1) void k_grid_fused(SynthArgs a,
           acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(av.y, bv.y, acc[1][1], 0, 0, 0);
         }
       }
-      if (q0 + NQ >= cur.nq) break;
-      load(c, q0 + NQ, cur);  // a chunk wider than NQ steps (sparse pulsars): its next steps' operands
     }
-    InterpTile<2> t;
-    t.c = c;
-    t.p = p;
-    t.r0 = r0;
-    t.y = cur.ci.y;
-    t.cnt = cur.ci.z;
-    t.nq = cur.nq;
-    // next chunk: its operands are in flight before this chunk's stores enter the vmcnt queue
-    c += kFusedWaves;
-    const bool more = c < c_end;
-    if (more) load(c, 0, nxt);
+    pf.lap(1);
+    // a chunk wider than NQ steps (sparse pulsars): its further steps one at a time, each operand loaded and waited for
+    // here (off the common path, whose operands all arrive one chunk ahead)
+    for (int q = NQ; q < cur.nq; ++q) {
+      const int v = 4 * q + lg;
+      const int row = f.lrows[((int64_t)cur.c * 4 + lg) * f.fq + q];
+      const dbl2 bv = *(const dbl2*)(band.wd + ((int64_t)cur.c * band.vmax + v) * kGridTT + 2 * lr);
+      const dbl2 av = *(const dbl2*)(lds + row * kFusedPitch + lds_lane);
+      acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(av.x, bv.x, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(av.y, bv.x, acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(av.x, bv.y, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(av.y, bv.y, acc[1][1], 0, 0, 0);
+    }
+    pf.lap(4);
     __builtin_amdgcn_sched_barrier(0);
-    interp_store_rows<2>(a, a.out, t, acc);
-    if (!more) break;
-    cur = nxt;
+    // interp_store_rows' fast path from the item's first TOA (toa0, a scalar of the item): a full chunk, every
+    // realization of the item stored, 16-byte aligned rows: eight 16-byte non-temporal stores from one row base
+    const int64_t t0 = toa0 + cur.ci.y;
+    if (cur.ci.z == kGridTT && r0 + kFusedReal <= a.n_real && ((t0 | a.ldo) & 1) == 0 && a.ldo < ((int64_t)1 << 26)) {
+      const uint32_t vo = (uint32_t)(((int64_t)2 * lg * a.ldo + 2 * lr) * 8);
+      const char* base = (const char*)(a.out + t0 + (int64_t)r0 * a.ldo);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          __builtin_nontemporal_store(dbl2{acc[0][i][g], acc[1][i][g]},
+                                      (dbl2*)((char*)base + (int64_t)(8 * g + i) * a.ldo * 8 + vo));
+    } else {
+      InterpTile<2> t;
+      t.c = cur.c;
+      t.p = p;
+      t.r0 = r0;
+      t.y = cur.ci.y;
+      t.cnt = cur.ci.z;
+      t.nq = cur.nq;
+      interp_store_rows<2>(a, a.out, t, acc);
+    }
+    pf.lap(2);
+  };
+  // The wave's chunks of all its items as one stream: after chunk i of item k (it0) the next one is chunk i + 1, or the
+  // first chunk of the next item that has one for this wave (it1: item k + 1's table, loaded one item ahead); every item
+  // boundary crossed is a barrier pair A / B (item k interpolated / item k + 1's grids written), which the DFT waves
+  // pass once per item as well.
+  ItemInfo it0, it1;
+  int k = 0;
+  item_info(0, it0);
+  item_info(1, it1);
+  auto boundaries = [&](int nb) {
+    if (nb > 0) fused_wait_lgkm0();  // every grid read of the item is done
+    for (int i = 0; i < nb; ++i) {
+      fused_barrier();  // A
+      fused_barrier();  // B
+    }
+    pf.lap(3);
+  };
+  // move to the next item that has a chunk for this wave (or past the last): the barrier pairs of the items left
+  auto advance_item = [&]() {
+    int nb = 0;
+    do {
+      ++nb;
+      ++k;
+      it0 = it1;
+      item_info(k + 1, it1);
+    } while (k < items.count && it0.n == 0);
+    return nb;
+  };
+  fused_barrier();  // B(-1)
+  pf.lap(3);
+  if (it0.n == 0) boundaries(advance_item());
+  Ops o0, o1;  // operand sets in turn (chunks two at a time: no register copies; only o0 lives across iterations)
+  int i = 0;   // the chunk in o0: the wave's i-th chunk of item k
+  if (k < items.count) load(it0.c0, chunk_info(it0, 0), o0);
+  // the chunk after chunk i of item k: (same item, i + 1) or (it1's first chunk, crossing one item); an item of no
+  // chunk for the wave is crossed without a chunk (advance_item)
+  while (k < items.count) {
+    const bool same1 = i + 1 < it0.n;
+    const bool next1 = same1 || it1.n > 0;
+    chunk(it0.p, it0.r0, it0.toa0, o0, next1, same1 ? it0.c0 + kFusedIW * (i + 1) : it1.c0,
+          same1 ? chunk_info(it0, i + 1) : chunk_info(it1, 0), o1);
+    if (same1) {
+      ++i;
+    } else {
+      boundaries(advance_item());
+      i = 0;
+      if (!next1) {  // item k had no chunk for this wave: its first chunk is not in o1
+        if (k < items.count) load(it0.c0, chunk_info(it0, 0), o0);
+        continue;
+      }
+    }
+    if (k >= items.count) break;
+    const bool same2 = i + 1 < it0.n;
+    const bool next2 = same2 || it1.n > 0;
+    chunk(it0.p, it0.r0, it0.toa0, o1, next2, same2 ? it0.c0 + kFusedIW * (i + 1) : it1.c0,
+          same2 ? chunk_info(it0, i + 1) : chunk_info(it1, 0), o0);
+    if (same2) {
+      ++i;
+    } else {
+      boundaries(advance_item());
+      i = 0;
+      if (!next2 && k < items.count) load(it0.c0, chunk_info(it0, 0), o0);
+    }
   }
+  pf.flush(f.prof, wave);
 }
 
 hipError_t launch_grid_fused(hipStream_t st, const SynthArgs& a, const GridBand& band, const FusedArgs& f,
                              int32_t nq_max, size_t lds_bytes) {
   if (band.n_chunks <= 0 || band.vmax < 4 || band.vmax % 4 != 0 || a.R_pad % kFusedReal != 0 || a.w_on ||
       a.accumulate || a.part || !f.lrows || !f.psr_c0 || f.n_sig <= 0 || f.n_sig > kFusedMaxSig ||
-      lds_bytes > (size_t)kFusedLdsMax || nq_max <= 0)
+      lds_bytes > (size_t)kFusedLdsMax || nq_max <= 0 || f.ring_off < 0 || f.fq < kFusedNQ || f.fq % 4 != 0 ||
+      (size_t)(f.ring_off + 2 * kFusedMaxSig * kFusedSlot) * sizeof(double) + sizeof(uint32_t) > lds_bytes)
     return hipErrorInvalidValue;
   int jobs = 0;
   for (int s = 0; s < f.n_sig; ++s) {
     const FusedSig& fs = f.s[s];
-    if (fs.nf % 4 != 0 || !fs.tq || fs.n_rc != (fs.nf / 4 + 32) / 32 || fs.ldq < 32 * fs.n_rc ||
-        fs.ntq < ((((fs.nm + 1) >> 1) + 3) & ~3) || fs.n_terms <= 0 || fs.n_terms > kDftGenTerms ||
-        fs.lrow0 < 0 || fs.stage < 0 ||
-        (size_t)(fs.stage + 2 * fs.ntq * kFusedReal * 2) * sizeof(double) > lds_bytes ||
-        (size_t)(fs.lrow0 + fs.nf) * kFusedPitch * sizeof(double) > lds_bytes)
+    const int nq = ((((fs.nm + 1) >> 1) + 3) >> 2);  // k-steps of the odd-k parity (the larger)
+    if (fs.nf % 4 != 0 || !fs.tq || fs.n_rc != (fs.nf / 4 + 32) / 32 || fs.ldq < 32 * fs.n_rc || 4 * nq > fs.ntq ||
+        fs.n_terms <= 0 || fs.n_terms > kDftGenTerms || fs.lrow0 < 0 || (fs.lrow0 + fs.nf) * kFusedPitch > f.ring_off)
       return hipErrorInvalidValue;
     for (int i = 0; i < fs.n_terms; ++i)
-      if (fs.term_nm[i] <= 0 || fs.term_nm[i] > fs.nm || (fs.term_kind[i] == 0 && !fs.term_amp[i]) ||
+      if (fs.term_nm[i] <= 0 || fs.term_nm[i] > fs.nm || (fs.term_kind[i] == 0 && (!fs.term_amp[i] || fs.term_nm[i] % 2)) ||
           (fs.term_kind[i] == 1 && (!a.coef || fs.term_col0[i] < 0 || fs.term_col0[i] + 2 * fs.term_nm[i] > a.K)))
         return hipErrorInvalidValue;
     jobs += fs.n_rc;
   }
-  if (jobs > kFusedWaves) return hipErrorInvalidValue;
+  if (jobs > kFusedDW) return hipErrorInvalidValue;
   const int32_t n_rb = a.R_pad / kFusedReal;
   const int64_t items = (int64_t)a.P * n_rb;
   if (items > 0x7FFFFFFF || items <= 0) return hipErrorInvalidValue;
-  const int64_t grid = (items + 7) / 8 * 8;
-  // NQ: band steps whose operands a wave holds (a wider chunk takes them NQ at a time)
-  auto kernel = nq_max <= 8 ? k_grid_fused<8> : k_grid_fused<12>;
-  static bool attr_set[2] = {false, false};
-  const int ki = nq_max <= 8 ? 0 : 1;
+  static int n_cu = 0;
+  if (!n_cu) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0)
+      n_cu = 256;
+  }
+  // persistent: one workgroup per CU (the grids take most of the LDS)
+  const int64_t grid = std::min<int64_t>((items + 7) / 8 * 8, ((int64_t)n_cu + 7) / 8 * 8);
+  // NQ: band steps whose operands an interpolation wave holds (a wider chunk takes them NQ at a time)
+  // ODD: the first realization is odd, so no lane's realization pair is one Philox pair (the draws take two)
+  const bool odd = f.real0 & 1;
+  auto kernel = nq_max <= 8 ? (odd ? k_grid_fused<8, true> : k_grid_fused<8, false>)
+                            : (odd ? k_grid_fused<12, true> : k_grid_fused<12, false>);
+  static bool attr_set[4] = {false, false, false, false};
+  const int ki = (nq_max <= 8 ? 0 : 2) + odd;
   if (!attr_set[ki]) {  // dynamic LDS beyond 64 KB
     hipError_t e = hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, kFusedLdsMax);
     if (e != hipSuccess) return e;
     attr_set[ki] = true;
   }
-  hipLaunchKernelGGL(kernel, dim3((unsigned)grid), dim3(64 * kFusedWaves), lds_bytes, st, a, band, f, n_rb,
+  // unused descriptors are copies of the first: the kernel's unconditional draw loads read valid memory through them
+  FusedArgs fa = f;
+  for (int s = f.n_sig; s < kFusedMaxSig; ++s) fa.s[s] = f.s[0];
+  hipLaunchKernelGGL(kernel, dim3((unsigned)grid), dim3(64 * (kFusedIW + kFusedDW)), lds_bytes, st, a, band, fa, n_rb,
                      (int32_t)items);
   return hipGetLastError();
 }

@@ -37,29 +37,40 @@ def shipped(ctx, capi):
 
 
 def _c2_like(ctx, rng, P=23, n=(31, 700), unsorted=True):
-    """C2's signal mix on ragged pulsars: RN30 (idx 0), DM100 (idx 2, three radio bands), the HD GWB30; one pulsar's TOAs
-    unsorted, so its chunks' bands jump."""
-    offs, toas, nu = random_layout(rng, P, n)
+    """C2's signal mix on ragged pulsars over one common span T (make_fake_array with equal Tobs): RN30 (idx 0), DM100
+    (idx 2, three radio bands) and the HD GWB30 on f_k = k / T, so RN and the GWB coalesce into one grid signal (two grid
+    signals, four 32-row DFT chunks); a pulsar of 31 TOAs (wide bands) and one pulsar's TOAs unsorted (bands jump)."""
+    counts = rng.integers(n[0], n[1], size=P)
+    counts[1] = 31
+    offs = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
+    t0, t1 = 4.4e9, 4.4e9 + 3.15e8
+    toas = np.concatenate([np.concatenate([[t0], np.sort(rng.uniform(t0, t1, k - 2)), [t1]]) for k in counts])
     if unsorted:
         perm = rng.permutation(offs[1] - offs[0])
         toas[offs[0]:offs[1]] = toas[offs[0]:offs[1]][perm]
+    nu = rng.choice([800.0, 1400.0, 2500.0], size=offs[-1])
+    T = t1 - t0
     ctx.batch_set_toas(offs, toas, nu)
-    f1, a1 = per_psr_signal(rng, offs, toas, 30)
-    ctx.batch_add_signal(0, f1, a1, idx=0.0)
-    f2, a2 = per_psr_signal(rng, offs, toas, 100)
-    ctx.batch_add_signal(0, f2, a2, idx=2.0)
-    fc, ac, L, _ = common_signal(rng, offs, toas, 30)
+    segs = []
+    for nm, idx in ((30, 0.0), (100, 2.0)):
+        f = np.tile(np.arange(1, nm + 1) / T, (P, 1))
+        a = np.sqrt(O.powerlaw(f, rng.uniform(-14.5, -13.5, (P, 1)), 3.0) / T)
+        ctx.batch_add_signal(0, f, a, idx=idx)
+        segs.append(O.Segment(0, 2 * np.pi * f, a, idx))
+    fc = np.arange(1, 31) / T
+    ac = np.sqrt(O.powerlaw(fc, -14.0, 13 / 3) / T)
+    v = rng.normal(size=(P, 3))
+    L = O.mvn_factor(O.orf_hd(v / np.linalg.norm(v, axis=1)[:, None]))
     ctx.batch_add_signal(1, fc, ac, L=L)
-    segs = [O.Segment(0, 2 * np.pi * f1, a1, 0.0), O.Segment(0, 2 * np.pi * f2, a2, 2.0),
-            O.Segment(1, 2 * np.pi * fc, ac, 0.0, L=L)]
+    segs.append(O.Segment(1, 2 * np.pi * fc, ac, 0.0, L=L))
     return offs, toas, nu, segs
 
 
 def _layout(ctx, rng, layout):
     if layout == "c2_like":
         return _c2_like(ctx, rng)
-    if layout in ("coalesced", "masked"):
-        return _shared_span_layout(ctx, rng, nu_const=False, with_masked=layout == "masked")
+    if layout == "coalesced":
+        return _shared_span_layout(ctx, rng, nu_const=False)
     if layout == "one_grid":  # RN + DM + GWB at one radio frequency: a single coalesced grid signal
         return _shared_span_layout(ctx, rng, nu_const=True)
     if layout == "dm_only":
@@ -75,12 +86,12 @@ def _run(ctx, capi, fused, seed, real0, R):
     return out, ctx.batch_grid_info()["interp_kernel"]
 
 
-@pytest.mark.parametrize("layout", ["c2_like", "coalesced", "masked", "one_grid", "dm_only"])
+@pytest.mark.parametrize("layout", ["c2_like", "coalesced", "one_grid", "dm_only"])
 @pytest.mark.parametrize("dft_gen", [1, 0])
 def test_fused_synthesis_is_bitwise_identical(ctx, capi, shipped, layout, dft_gen):
     """The fused kernel returns the two-kernel path's block bit for bit: draws inside the kernel (FPTA_OPT_DFT_GEN 1:
-    k_grid_dft_gen's terms) or from the merged coefficient buffer (0: k_grid_dft_mfma's operand), one to three grid
-    signals, a masked (backend) signal, realization counts off every tile multiple and odd first realizations (the
+    k_grid_dft_gen's terms) or from the merged coefficient buffer (0: k_grid_dft_mfma's operand), one or two grid
+    signals (one to four DFT waves with a job), realization counts off every tile multiple and odd first realizations (the
     Philox pair boundary), every sample written (NaN-poisoned block); the kernel that ran is the fused one. And the
     block matches the oracle."""
     rng = np.random.default_rng(211 + len(layout))
@@ -132,7 +143,8 @@ def test_fused_pipelined_blocks(ctx, capi, shipped):
 
 def test_fused_not_taken_outside_its_blocks(ctx, capi, shipped):
     """Blocks the fused kernel does not serve take the two-kernel path: white / ECORR epilogue, fused partial
-    checksums (streamed jobs), grids too large for LDS (257 modes), and FPTA_OPT_INTERP_FUSED 0."""
+    checksums (streamed jobs), more than four 32-row DFT chunks (a masked backend signal: a third grid signal), grids
+    too large for LDS (600 modes: 1,804 grid rows), and FPTA_OPT_INTERP_FUSED 0."""
     rng = np.random.default_rng(227)
     try:
         offs, toas, nu, segs = _c2_like(ctx, rng, P=12, n=(100, 300))
@@ -150,12 +162,14 @@ def test_fused_not_taken_outside_its_blocks(ctx, capi, shipped):
         ctx.set_option(capi.OPT_INTERP_FUSED, 0)
         ctx.batch_synth(3, 0, 256, to_host=False)
         assert not ctx.batch_grid_info()["interp_kernel"].startswith("k_grid_fused")
-        ctx.set_options(shipped)
-        ctx.batch_clear()
-        _flat_layout(ctx, rng, P=3, n_modes=257)
-        ctx.set_option(capi.OPT_SYNTH_PATH, 4)
-        ctx.batch_synth(3, 0, 256, to_host=False)
-        assert not ctx.batch_grid_info()["interp_kernel"].startswith("k_grid_fused")
+        for build in (lambda: _shared_span_layout(ctx, rng, nu_const=False, with_masked=True),
+                      lambda: _flat_layout(ctx, rng, P=3, n_modes=600)):
+            ctx.set_options(shipped)
+            ctx.batch_clear()
+            build()
+            ctx.set_option(capi.OPT_SYNTH_PATH, 4)
+            ctx.batch_synth(3, 0, 256, to_host=False)
+            assert not ctx.batch_grid_info()["interp_kernel"].startswith("k_grid_fused")
     finally:
         ctx.batch_set_white()
         ctx.batch_clear()
