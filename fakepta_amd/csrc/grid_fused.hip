@@ -102,6 +102,9 @@ __global__ __launch_bounds__(64 * (kFusedIW + kFusedDW), 1) void k_grid_fused(Sy
   if (wave >= kFusedIW) {
     // ---------------------------------------------------------------- DFT waves
     const int dw = wave - kFusedIW;
+    // the DFT waves are the item's critical path (the interpolation waves wait at barrier A): first claim on the SIMD's
+    // issue slots, the interpolation waves fill the gaps (C2 kernel -3%)
+    __builtin_amdgcn_s_setprio(3);
     int js = -1, jrc = 0;  // this wave's job: grid signal js, quarter-range rows 32 jrc .. 32 jrc + 31
     {
       int j = dw;
@@ -116,8 +119,8 @@ __global__ __launch_bounds__(64 * (kFusedIW + kFusedDW), 1) void k_grid_fused(Sy
     }
     js = __builtin_amdgcn_readfirstlane(js);
     jrc = __builtin_amdgcn_readfirstlane(jrc);
-    Prof pf;  // DFT waves: 0 loads issue, 1 MFMA steps, 2 ring sync, 3 grid writes, 4 barriers, 5 iterations, 6 normals,
-              // 7 draw stores
+    Prof pf;  // DFT waves: 0 loads issue, 1 MFMA steps, 2 ring sync, 3 grid writes, 4 barriers, 5 iterations, 6 draws,
+              // 7 the first item's first draws
     pf.start();
     uint32_t epoch = 0;
     // every DFT wave's ring writes and reads so far are done (an LDS counter; the interpolation waves run on)
@@ -271,9 +274,9 @@ __global__ __launch_bounds__(64 * (kFusedIW + kFusedDW), 1) void k_grid_fused(Sy
         }
       }
     };
-    // k_grid_dft_gen's MFMA k-steps q = 2 g, 2 g + 1 of the job on the job signal's group g in ring slot g
-    auto steps = [&](int g, const Tabs& tb) {
-      const double* __restrict__ bsrc = slot_of(g, js);
+    // k_grid_dft_gen's MFMA k-steps q = 2 g, 2 g + 1 of the job on the job signal's group g in ring slot `slot`
+    auto steps = [&](int slot, int g, const Tabs& tb) {
+      const double* __restrict__ bsrc = slot_of(slot, js);
 #pragma unroll
       for (int h2 = 0; h2 < 2; ++h2) {
         const int q = 2 * g + h2;
@@ -294,45 +297,57 @@ __global__ __launch_bounds__(64 * (kFusedIW + kFusedDW), 1) void k_grid_fused(Sy
         }
       }
     };
-    // item k's accumulators of this wave's job: iteration g draws group g + 1 of every signal into ring slot g + 1 and
-    // runs the job signal's group g from slot g; all loads of an iteration are issued before its steps
+    // Item k's accumulators of this wave's job. Iteration g runs the job signal's group g from ring slot sb + g and
+    // draws group g + 1 of every signal into slot sb + g + 1; the last iteration draws group 0 of item k + 1 instead
+    // (its MFMA steps have no draws of their own to overlap), so only the first item's group 0 is drawn alone. All
+    // loads of an iteration are issued before its steps.
+    int sb = 0;  // ring slot of the item's group 0
     auto build = [&](int k) {
       const int item = items.item(k);
       const int p = item / n_rb, r0 = (item - p * n_rb) * kFusedReal;
+      const bool nx = k + 1 < items.count;
+      const int item1 = nx ? items.item(k + 1) : item;
+      const int p1 = item1 / n_rb, r1 = (item1 - p1 * n_rb) * kFusedReal;
 #pragma unroll
       for (int par = 0; par < 2; ++par)
 #pragma unroll
         for (int h = 0; h < 2; ++h)
 #pragma unroll
           for (int t = 0; t < 2; ++t) C[par][h][t] = S[par][h][t] = d4{0.0, 0.0, 0.0, 0.0};
+      if (k == 0) {
 #pragma unroll
-      for (int s = 0; s < kFusedMaxSig; ++s) {
-        if (s >= f.n_sig) continue;
-        DrawIn in;
-        draw_load(f.s[s], 0, p, r0, in);
-        draw_finish(f.s[s], 0, p, r0, slot_of(0, s), in);
+        for (int s = 0; s < kFusedMaxSig; ++s) {
+          if (s >= f.n_sig) continue;
+          DrawIn in;
+          draw_load(f.s[s], 0, p, r0, in);
+          draw_finish(f.s[s], 0, p, r0, slot_of(sb, s), in);
+        }
+        pf.lap(7);
+        dsync();
+        pf.lap(2);
       }
-      pf.lap(7);
-      dsync();
-      pf.lap(2);
       for (int g = 0; g < n_it; ++g) {
+        const bool last = g + 1 == n_it;
+        const int dp = last ? p1 : p, dr = last ? r1 : r0;
         Tabs tb;
         tables(g, tb);
         DrawIn in[kFusedMaxSig];
 #pragma unroll
-        for (int s = 0; s < kFusedMaxSig; ++s)
-          draw_load(f.s[s], min(g + 1, max(ng[s], 1) - 1), p, r0, in[s]);  // an unused descriptor is a copy of the first
+        for (int s = 0; s < kFusedMaxSig; ++s)  // an unused descriptor is a copy of the first
+          draw_load(f.s[s], last ? 0 : min(g + 1, max(ng[s], 1) - 1), dp, dr, in[s]);
         pf.lap(0);
-        if (g < jng) steps(g, tb);
+        if (g < jng) steps(sb + g, g, tb);
         pf.lap(1);
 #pragma unroll
         for (int s = 0; s < kFusedMaxSig; ++s)
-          if (g + 1 < ng[s]) draw_finish(f.s[s], g + 1, p, r0, slot_of(g + 1, s), in[s]);
+          if (last ? nx && s < f.n_sig : g + 1 < ng[s])
+            draw_finish(f.s[s], last ? 0 : g + 1, dp, dr, slot_of(sb + g + 1, s), in[s]);
         pf.lap(6);
         dsync();
         pf.lap(2);
         pf.count(5);
       }
+      sb = (sb + n_it) & 1;
     };
     auto write_grid = [&]() {
       if (js >= 0) {
