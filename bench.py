@@ -452,7 +452,9 @@ def main():
         grid_avg_s = dft_ms / 1e3 / n_steps
         dft_flops = 2.0 * gi["fma_dft"] * R_pad
         # grid signals with a per-pulsar member draw their coefficients inside the DFT (FPTA_OPT_DFT_GEN, C2)
-        dft_kernel = ("k_grid_dft_gen" if args.config == "c2" and ctx.get_option(_capi.OPT_DFT_GEN)
+        fused = kernel.startswith("k_grid_fused")
+        dft_kernel = ("inside " + kernel if fused else
+                      "k_grid_dft_gen" if args.config == "c2" and ctx.get_option(_capi.OPT_DFT_GEN)
                       and gi["grid_mfma"] & 1 else GRID_DFT[bool(gi["grid_mfma"] & 1)])
         roofline = {"bound": "hbm", "pipe": pipe, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": kernel,
@@ -461,13 +463,20 @@ def main():
                     "traffic_source": traffic_src,
                     "implementation_bytes_per_launch": impl_bytes,
                     "interp_fp64_TFLOPs": 2.0 * gi["fma_interp"] * R_pad / synth_avg_s / 1e12,
+                    # k_grid_fused also runs the block's DFTs on the same fp64 pipe (one launch, no DFT kernel): its
+                    # interpolation + DFT MFMA FLOPs against the 78.6 TF FP64 peak beside the HBM fraction
+                    "fp64_pipe": ({"flops_per_launch": 2.0 * (gi["fma_interp"] + gi["fma_dft"]) * R_pad,
+                                   "TFLOPs": 2.0 * (gi["fma_interp"] + gi["fma_dft"]) * R_pad / synth_avg_s / 1e12,
+                                   "frac": 2.0 * (gi["fma_interp"] + gi["fma_dft"]) * R_pad / synth_avg_s / 1e12
+                                   / FP64_PEAK_TFLOPS} if fused else None),
                     "grid": {"width": gi["width"], "sigma": gi["sigma"], "err_bound": gi["err_bound"],
                              "signals": gi["signals"], "grid_signals": gi["grid_signals"],
                              "band_rows_per_chunk": gi["band_rows_per_chunk"]},
                     "dft": {"kernel": dft_kernel, "launches_per_step": n_dft / n_steps,
                             "co_running_span_ms_per_step": grid_avg_s * 1e3,
-                            "note": "HIP-event spans of one block's DFT launches on the side streams, beside the "
-                                    "previous block's interpolation (not kernel durations; see isolated)",
+                            "note": ("the DFTs run inside the synthesis kernel (no DFT launch)" if fused else
+                                     "HIP-event spans of one block's DFT launches on the side streams, beside the "
+                                     "previous block's interpolation (not kernel durations; see isolated)"),
                             "flops_per_block": dft_flops}}
     else:
         # exact paths: FP64-bound, 2K FLOP per 8-byte sample (80 FLOP/B at K = 320)

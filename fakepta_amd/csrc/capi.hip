@@ -1,323 +1,13 @@
-// C-ABI of libfakepta_amd.so (declared in include/fakepta_amd.h).
-// Host-side orchestration only: argument checking, device buffers, layout tables,
-// kernel dispatch on the context's stream, HIP-event timing. All arithmetic on the
-// path runs in kernels.hip.
-#include <hip/hip_runtime.h>
-#include <rccl/rccl.h>
+// C-ABI of libfakepta_amd.so (declared in include/fakepta_amd.h): contexts and options, the drop-in entry points, the
+// batch entry points and path selection, dense covariance. The gridded plan is grid_host.hip, several devices and RCCL
+// ranks multi.hip; host-side orchestration only (argument checking, device buffers, layout tables, kernel dispatch on
+// the context's stream, HIP-event timing).
+#include "capi_host.h"
 
-#include <algorithm>
-#include <cmath>
-#include <cstdio>
-#include <cstdlib>
-#include <cstring>
-#include <string>
-#include <vector>
-
-#include "../../include/fakepta_amd.h"
-#include "fpta_internal.h"
-
-using namespace fpta;
-
-namespace {
+namespace __attribute__((visibility("hidden"))) capi {  // library-internal: not exported
 
 thread_local std::string g_err;
 
-struct DevBuf {
-  void* p = nullptr;
-  size_t cap = 0;
-  DevBuf() = default;
-  DevBuf(const DevBuf&) = delete;
-  DevBuf& operator=(const DevBuf&) = delete;
-  ~DevBuf() { release(); }
-  void release() {
-    if (p) (void)hipFree(p);
-    p = nullptr;
-    cap = 0;
-  }
-  void swap(DevBuf& o) {
-    std::swap(p, o.p);
-    std::swap(cap, o.cap);
-  }
-  hipError_t ensure(size_t bytes) {
-    if (bytes <= cap && p) return hipSuccess;
-    release();
-    size_t want = std::max<size_t>(bytes, 256);
-    hipError_t e = hipMalloc(&p, want);
-    if (e != hipSuccess) {
-      p = nullptr;
-      return e;
-    }
-    cap = want;
-    return hipSuccess;
-  }
-  template <class T>
-  T* as() const {
-    return static_cast<T*>(p);
-  }
-};
-
-struct Seg {
-  SegDesc d{};
-  int32_t nm_orig = 0;
-  std::vector<double> h_w0;  // first angular frequency per row ([P] for kind 0, [1] for kind 1)
-  std::vector<uint8_t> h_mask;  // host copy of the TOA mask (empty: none), for grid coalescing
-  DevBuf w, amp, L, LT, mask;
-};
-
-// Gridded-synthesis tables of one signal (grid.hip): real-DFT table E; its grid block starts at row rowoff of
-// the plan's grid buffer.
-struct GridSeg {
-  int32_t nf = 0, half = 0, lde = 0, ntab = 0;
-  int64_t rowoff = 0;
-  DevBuf ecos, esin;  // half-range tables (k_grid_dft)
-  int32_t ldq = 0, ntq = 0;
-  DevBuf tq;          // quarter-range tables by mode parity (k_grid_dft_mfma)
-};
-
-// Gridded-synthesis plan of a layout (built once per layout, reused by every batch).
-struct GridPlan {
-  bool built = false;
-  bool ok = false;           // usable for this layout (harmonic, <= kGridMaxSeg signals)
-  std::string why;           // reason when !ok
-  int32_t w = 0;             // kernel width (grid cells)
-  double sigma = 0.0;        // oversampling
-  int32_t n_chunks = 0;
-  DevBuf chunks;             // int4 {pulsar, first TOA (pulsar-local), count, band rows V (multiple of 4)}
-  int32_t vmax = 0;          // largest V: row pitch of the row-index and weight tables
-  int64_t grid_rows = 0;     // rows of the grid buffer: sum over signals of P nf
-  DevBuf rows;               // [n_chunks][vmax] int32 grid-buffer row of each band row (all signals back to back)
-  DevBuf wd;                 // [n_chunks][vmax][kGridTT] interpolation weights (chromatic factor, mask folded in)
-  DevBuf g, g2;              // [grid_rows][R_pad] grid values of the batch (two buffers when pipelined)
-  std::vector<int32_t> psr_chunk0;  // [P + 1] first chunk of each pulsar (chunks are pulsar-major)
-  // partial-checksum groups (FPTA_OPT_FUSE_CHECKSUMS): <= pg_size consecutive chunks of one pulsar each; pgfirst
-  // [n_pg + 1] the first chunk of each group, psr_pg [P + 1] the first group of each pulsar
-  int32_t pg_size = 0, n_pg = 0;
-  DevBuf pgfirst, psr_pg;
-  DevBuf psr_c0;  // device copy of psr_chunk0 (k_grid_interp_psr without partial checksums)
-  // k_grid_fused plan (FPTA_OPT_INTERP_FUSED): every grid signal's grid for kFusedReal realizations in LDS (signal s
-  // at LDS row fused_lrow0[s]), the draw ring after them; frows [n_chunks][vmax] the LDS row of each band row;
-  // fused_lds the workgroup's LDS bytes
-  bool fused_ok = false;
-  size_t fused_lds = 0;
-  int32_t fused_fq = 0;  // band steps per (chunk, lane group) in frows
-  std::vector<int32_t> fused_lrow0;
-  DevBuf frows;
-  // k_grid_interp_wr plan (GridWindow): <= 2 grid signals, each signal's band rows in a ring of kWrSlots LDS slots by
-  // unwrapped row; per chunk the slot of each band row, and the rows to load: all its band rows (full) or those not in
-  // the previous chunk's band (new; = full and flagged fresh when the two bands do not fit one ring window)
-  bool wr_ok = false;
-  DevBuf wr_meta, wr_list, wr_slot;
-  // k_grid_interp_lds plan: groups int4 {first chunk, chunks, union rows U, offset into urows}; urows the grid-
-  // buffer rows of each group's union; lrows [n_chunks][vmax] the union slot of each band row
-  bool lds_ok = false;
-  int32_t n_groups = 0, lds_rows = 0;
-  DevBuf groups, urows, lrows;
-  // k_grid_interp_u plan (GridUnion): groups of <= kUnionGroup chunks with <= kUnionRowsMax union rows; per chunk the
-  // signals' band offsets and union bases; per (chunk, signal, TOA slot) the window's first band row and {d, ch}
-  bool u_ok = false;
-  int32_t u_groups = 0, u_sig = 0;
-  DevBuf ugroups, uurows, ucbase, udch, uwrow;
-  int32_t u_w[kUnionSigMax] = {0, 0};
-  double u_hw[kUnionSigMax] = {0.0, 0.0}, u_beta[kUnionSigMax] = {0.0, 0.0};
-  std::vector<GridSeg*> segs;  // one per grid signal
-  // grid signals (FPTA_OPT_GRID_COALESCE): members (layout signal indices, ascending), the anchor (the member with
-  // the most modes: its coefficient columns receive the others' and its grid/weights serve the group) and the last
-  // member (the group's coefficients are complete once it is drawn)
-  std::vector<std::vector<int32_t>> members;
-  std::vector<int32_t> anchor, last;
-  bool merges = false;       // some grid signal has > 1 member
-  double mean_v = 0.0;       // mean band rows per chunk
-  double fma_grid = 0.0;     // FMAs per realization: DFT + interpolation
-  double fma_dft = 0.0;      // FMAs per realization in k_grid_dft
-  double fma_interp = 0.0;   // FMAs per realization in k_grid_interp (dense band, padded TOA slots)
-  double grid_vals = 0.0;    // grid values per realization (sum over signals of P nf)
-  double weight_bytes = 0.0; // interpolation weight tables
-  double fma_direct = 0.0;   // FMAs per realization of the direct contraction
-  double err_bound = 1.0;    // a-priori relative aliasing bound of the ES kernel, exp(-pi w sqrt(1 - 1/sigma))
-  int64_t g_rpad = 0;        // R_pad the grid buffers are sized for
-  ~GridPlan() { clear(); }
-  void clear() {
-    for (GridSeg* g : segs) delete g;
-    segs.clear();
-    built = ok = false;
-    n_chunks = 0;
-    vmax = 0;
-    lds_ok = false;
-    n_groups = lds_rows = 0;
-    u_ok = false;
-    u_groups = u_sig = 0;
-    grid_rows = 0;
-    g_rpad = 0;
-    psr_chunk0.clear();
-    pg_size = n_pg = 0;
-    wr_ok = false;
-    fused_ok = false;
-    fused_lds = 0;
-    fused_lrow0.clear();
-    members.clear();
-    anchor.clear();
-    last.clear();
-    merges = false;
-    mean_v = 0.0;
-    // the plan figures accumulate over signals in grid_build: a rebuilt plan must start from zero
-    fma_grid = fma_dft = fma_interp = grid_vals = weight_bytes = fma_direct = 0.0;
-    err_bound = 1.0;
-    why.clear();
-  }
-};
-
-// A device-resident pulsar array plus its GP signals.
-struct Layout {
-  int32_t P = 0;
-  int64_t n_toa = 0;
-  int64_t max_np = 0;
-  std::vector<int64_t> h_offs;
-  std::vector<double> h_toas, h_nu;
-  DevBuf offs, toas, nu, psr_of;
-  std::vector<Seg*> segs;
-  DevBuf segdesc;
-  int32_t K = 0;
-  bool dirty = true;
-  // recurrence seeds [n_seg][n_toa] (double4), valid when every segment is harmonic
-  DevBuf seeds;
-  bool all_harmonic = false;
-  // tile table cache of the tiled synthesis kernels: valid for (tiles_toa, tiles_real, tiles_n_real)
-  DevBuf tiles;
-  int32_t n_tiles = 0;
-  int32_t tiles_toa = 0, tiles_real = 0;
-  int64_t tiles_n_real = -1;
-  GridPlan grid;
-  ~Layout() { clear_signals(); }
-  void clear_signals() {
-    for (Seg* s : segs) delete s;
-    segs.clear();
-    K = 0;
-    dirty = true;
-    tiles_n_real = -1;
-    grid.clear();
-  }
-};
-
-}  // namespace
-
-struct fpta_ctx {
-  int device = 0;
-  hipStream_t stream = nullptr;
-  std::string err;
-  Layout batch, scratch;
-  // batch white noise
-  DevBuf sigma, block_of, esig, zb_epochs, corr_autos, corr_parts, corr_dst;
-  bool has_sigma = false, has_blocks = false;
-  int64_t n_blocks = 0;
-  // work buffers
-  DevBuf coef, zbuf, out, sums, zin, xout, hostz, scratch_out, scratch_z, scratch_zb, scratch_sigma,
-      scratch_block_of, scratch_esig, dbg_a, dbg_b;
-  int32_t out_R = 0;
-  int64_t out_ld = 0;
-  // options
-  int synth_path = 0;
-  int mfma_min_real = 16;
-  int profile = 0;
-  int anchor = 0;  // 0: phasor recurrence anchored once per segment
-  int valu_variant = 1;  // seeded (MT 2, NT 16): fastest on C2 (profiles/r01_sweep_*.txt)
-  int fuse_white = 1;    // add white/ECORR in the seeded kernel's epilogue
-  int fuse_sums = 0;     // gridded path: interpolation writes partial checksums (FPTA_OPT_FUSE_CHECKSUMS)
-  int mix_mfma = 1;      // ORF mixing of large arrays on fp64 MFMA (k_mix_mfma) or VALU (k_mix_tiled)
-  // batch coefficients on a side stream (FPTA_OPT_OVERLAP): gen / mix of signal i run there and signal i's
-  // consumer on the ctx stream waits for ev_sig[i] only, so the gridded DFT of one signal overlaps the draws of
-  // the next (VALU Philox beside fp64 MFMA). ev_begin orders the side stream after everything queued before.
-  int overlap = 1;
-  int interp_ws = 1;      // gridded interpolation on the warp-specialised kernel (FPTA_OPT_INTERP_WS)
-  int last_interp = 0;    // interpolation kernel of the last gridded block: 1 + 4 kind + 2 white + part (0: none)
-  int grid_coalesce = 1;  // gridded path: signals sharing w0 and the chromatic weight share one grid (FPTA_OPT_GRID_COALESCE)
-  int part_group = kPartGroup;  // fused partial checksums: consecutive chunks per partial row (FPTA_OPT_PART_GROUP)
-  int interp_psr = 1;  // k_grid_interp_psr where the layout allows it (FPTA_OPT_INTERP_PSR)
-  int interp_wr = 0;   // k_grid_interp_wr for plain blocks where the plan allows it (FPTA_OPT_INTERP_WR)
-  int interp_fused = 1;  // k_grid_fused for plain blocks where the plan allows it (FPTA_OPT_INTERP_FUSED)
-  // pipelined per-pulsar blocks read their coefficients in the interpolation (ctx stream): two coefficient buffers,
-  // coef2 the other one; coef_slot = the grid-buffer index whose block owns c->coef; prev_psr: the last pipelined
-  // block ran that way (its draws waited for the interpolation two blocks back, not for the whole ctx stream)
-  DevBuf coef2;
-  int coef_slot = 0;
-  bool prev_psr = false;
-  int async_sums = 0;    // streamed jobs: partial-checksum reductions on their own stream (FPTA_OPT_ASYNC_SUMS; measured
-                         // no faster on C3, profiles/r03h_ab_c3_async_sums.txt: the reductions then compete with the interpolation)
-  int gen_mix = 2;       // common signals of 64..256 pulsars: draws and ORF mixing in one kernel (k_gen_mix,
-                         // FPTA_OPT_GEN_MIX; 2: 16-realization waves, C3 -3.7 % vs 1, profiles/r03z_gen_mix_waves.txt);
-                         // 0 k_gen into zbuf, then k_mix_mfma
-  int dft_gen = 1;       // gridded path: grid signals with a per-pulsar member draw their coefficients inside the DFT
-                         // (k_grid_dft_gen, FPTA_OPT_DFT_GEN): no k_gen launch, no coefficient round trip for them
-  bool gen_fused = false;  // the current block runs k_grid_dft_gen for those grid signals (set by batch_common)
-  int64_t blk_real0 = 0;   // the current block's first realization and Philox key (k_grid_dft_gen draws)
-  uint32_t blk_k0 = 0, blk_k1 = 0;
-  int interp_lds = 0;    // gridded interpolation with the grid rows staged in LDS where the plan allows (measured
-                         // slower on C2: 0.745 vs 0.67 ms, profiles/r02g_*; kept as an option)
-  hipStream_t side = nullptr;
-  hipEvent_t ev_begin = nullptr;
-  std::vector<hipEvent_t> ev_sig;
-  bool coef_side = false;  // the last coefficients were made on the side stream and are not all waited for
-  // recorded on the ctx stream right after the last reader of the coefficient buffer was queued (the gridded
-  // DFT, or the coefficient download): the next block's draws wait for it instead of for the whole previous
-  // block, so they overlap that block's interpolation
-  hipEvent_t ev_coef_free = nullptr;
-  bool coef_free_set = false;
-  // pipelined gridded batches (FPTA_OPT_OVERLAP, path 4): the draws, merges and DFT of a block all run on the side
-  // stream, into one of two grid buffers, so they overlap the previous block's interpolation on the ctx stream.
-  // ev_gready: the block's DFT is done (its interpolation waits); ev_gfree[i]: the interpolation reading grid
-  // buffer i is done (the DFT that next writes buffer i waits); coef_last_side: the last reader of coef was a
-  // side-stream DFT, so the next block's draws need no ctx-stream wait.
-  hipEvent_t ev_gready = nullptr;
-  hipEvent_t ev_gfree[2] = {nullptr, nullptr};
-  bool gfree_set[2] = {false, false};
-  int gbuf = 0;
-  bool coef_last_side = false;
-  // FPTA_OPT_SIDE_SPLIT: grid signal split_g (per-pulsar members only) of the current pipelined block runs its draws
-  // and DFT on side2. At each block start side waits for side2's previous work (ev_s2done) and side2 for side's
-  // (ev_s2begin), so a layout change never lets one stream write columns the other still reads; ev_gready2: side2's
-  // DFT is done. side_split 2: side2's DFT also waits for the common signals' draws queued on side before it
-  // (ev_s2mix), so those draws get the room beside the previous block's interpolation first.
-  int side_split = 2;
-  hipStream_t side2 = nullptr;
-  hipEvent_t ev_s2begin = nullptr, ev_s2done = nullptr, ev_gready2 = nullptr, ev_s2mix = nullptr;
-  bool s2done_set = false;
-  int32_t split_g = -1;
-  bool coef_copy_pending = false;  // the block's coefficients are still to be downloaded after the synthesis
-  DevBuf part[2], part_tmp; // partial checksums [n_chunks][R_pad][2] (two buffers, by block), reduction scratch
-  bool part_ready = false;  // part[part_cur] holds the partials of the current block (c->out, out_R)
-  int32_t part_chunks = 0, part_rpad = 0;
-  int part_cur = 0, part_next = 0;
-  // streamed jobs reduce a block's partials on their own stream (red), beside the next block's interpolation, which
-  // writes the other partials buffer; ev_pfree[i]: the reduction reading part[i] is done (the interpolation that next
-  // writes part[i] waits for it); red_pending: red has work the ctx stream has not joined
-  hipStream_t red = nullptr;
-  hipEvent_t ev_pready = nullptr, ev_pfree[2] = {nullptr, nullptr}, ev_red = nullptr;
-  bool pfree_set[2] = {false, false};
-  bool red_pending = false;
-  int last_path = 0;     // synthesis path of the last batch (1 direct, 2 MFMA, 3 VALU, 4 gridded)
-  std::string path_reason;  // why the last batch did not take the gridded path (empty if it did)
-  // gridded path defaults: w = 15 at sigma = 1.5 (a-priori bound 1.5e-12). The measured flat-spectrum worst case at
-  // real-MJD epochs is <= ~6e-12 relative (tests/test_gpu_grid.py at the shipped defaults; the numpy model of
-  // oracle.grid_synth and the GPU agree); w = 14 (bound 9.4e-12) is refused by the auto path. sigma = 1.5 keeps the
-  // grid (DFT) a quarter smaller than sigma = 2 (tools/sweep_grid.py --params, profiles/r01_sweep_wsig.txt)
-  int grid_w = 15;       // gridded path: kernel width in grid cells
-  int grid_sigma100 = 150;  // gridded path: oversampling x 100
-  int grid_mfma = 1;     // gridded path: bit 0 k_grid_dft_mfma (else k_grid_dft); the interpolation is always on
-                         // MFMA (k_grid_interp_ws / k_grid_interp_mfma)
-  // profiling
-  struct Pending {
-    int which;
-    hipEvent_t a, b;
-  };
-  std::vector<Pending> pending;
-  std::vector<hipEvent_t> pool;
-  int64_t kcount[FPTA_K_N] = {};
-  double kms[FPTA_K_N] = {};
-  // dense-covariance path: inputs, basis G^T [k_pad][n_pad], matrix C [n_pad][n_pad], panel, draws
-  DevBuf dn_toas, dn_nu, dn_f, dn_sw, dn_segof, dn_segidx, dn_segff, dn_white, dn_GT, dn_C, dn_PT, dn_info, dn_r,
-      dn_y, dn_out, dn_Z;
-};
-
-namespace {
 
 int fail(fpta_ctx* c, int code, const std::string& msg) {
   if (c) c->err = msg;
@@ -330,23 +20,6 @@ int hip_fail(fpta_ctx* c, hipError_t e, const char* what) {
   return fail(c, e == hipErrorOutOfMemory ? FPTA_ENOMEM : FPTA_EDEVICE, m);
 }
 
-// Debug build (make debug, -DFPTA_DEBUG): synchronize after every launch so a device fault is
-// reported by the launch that caused it, and the kernels' FPTA_DCHECK bounds checks are compiled in.
-// Release builds read no environment variable and never add work or synchronisation.
-#ifdef FPTA_DEBUG
-constexpr bool debug_sync() { return true; }
-#else
-constexpr bool debug_sync() { return false; }
-#endif
-
-#define HIPCHK(ctx, expr, what)                                                           \
-  do {                                                                                    \
-    hipError_t _e = (expr);                                                               \
-    if (_e == hipSuccess && debug_sync() && std::strstr(what, "launch"))                  \
-      _e = hipStreamSynchronize((ctx)->stream);                                           \
-    if (_e != hipSuccess) return hip_fail(ctx, _e, what);                                 \
-  } while (0)
-
 hipEvent_t get_event(fpta_ctx* c) {
   if (!c->pool.empty()) {
     hipEvent_t e = c->pool.back();
@@ -358,26 +31,6 @@ hipEvent_t get_event(fpta_ctx* c) {
   return e;
 }
 
-// Bracket a launch with HIP events on the ctx stream when profiling is on.
-struct KTimer {
-  fpta_ctx* c;
-  int which;
-  hipStream_t st;
-  hipEvent_t a = nullptr, b = nullptr;
-  KTimer(fpta_ctx* c_, int w, hipStream_t s = nullptr) : c(c_), which(w), st(s ? s : c_->stream) {
-    if (c->profile) {
-      a = get_event(c);
-      b = get_event(c);
-      if (a) (void)hipEventRecord(a, st);
-    }
-  }
-  ~KTimer() {
-    if (c->profile && a && b) {
-      (void)hipEventRecord(b, st);
-      c->pending.push_back({which, a, b});
-    }
-  }
-};
 
 // The ctx stream waits for everything queued on the red stream (partial-checksum reductions of streamed jobs).
 int join_red(fpta_ctx* c) {
@@ -847,926 +500,6 @@ int check_tiles(fpta_ctx* c, const Layout& L, int32_t R, int32_t tile_toa, int32
 }
 
 
-// ------------------------------------------------------------------------------- gridded plan
-// Gauss-Legendre nodes/weights on [-1, 1] (Newton on P_n; host, once per plan).
-void gauss_legendre(int n, std::vector<double>& x, std::vector<double>& wt) {
-  x.assign(n, 0.0);
-  wt.assign(n, 0.0);
-  for (int i = 0; i < (n + 1) / 2; ++i) {
-    double z = std::cos(M_PI * (i + 0.75) / (n + 0.5)), dp = 1.0;
-    for (int it = 0; it < 100; ++it) {
-      double p0 = 1.0, p1 = z;
-      for (int k = 2; k <= n; ++k) {
-        const double p2 = ((2.0 * k - 1.0) * z * p1 - (k - 1.0) * p0) / k;
-        p0 = p1;
-        p1 = p2;
-      }
-      dp = n * (z * p1 - p0) / (z * z - 1.0);
-      const double dz = p1 / dp;
-      z -= dz;
-      if (std::fabs(dz) < 1e-16) break;
-    }
-    x[i] = -z;
-    x[n - 1 - i] = z;
-    wt[i] = wt[n - 1 - i] = 2.0 / ((1.0 - z * z) * dp * dp);
-  }
-}
-
-// Build the gridded plan (grid.hip) of layout L: per signal the grid size nf, the deconvolved real-DFT
-// table, the chunking of every pulsar's TOAs into runs of <= kGridTT whose interpolation rows span at
-// most kGridRowCap cells, and the dense banded weights (device). Not usable -> ok = false + why.
-constexpr int kGridRowCap = 48;
-constexpr double kGridAutoRatio = 0.5;  // auto path: gridded when it needs < half the direct FMAs
-// auto path: gridded only when the a-priori bound exp(-pi w sqrt(1 - 1/sigma)) of the width/oversampling pair is
-// within this. The measured flat-spectrum worst case is ~3-4x the bound (w = 16, sigma = 1.5: bound 2.5e-13,
-// measured <= 3.6e-12; w = 15: 1.5e-12 / 6e-12; w = 14: 9.4e-12 / 3.2e-11, refused). A forced path 4 runs any
-// accepted pair: the caller opted in, and fpta_batch_grid_info reports the bound.
-constexpr double kGridAutoMaxErr = 2e-12;
-int grid_build(fpta_ctx* c, Layout& L) {
-  GridPlan& G = L.grid;
-  if (G.built && G.w == c->grid_w && G.sigma == c->grid_sigma100 / 100.0) return FPTA_OK;
-  G.clear();
-  G.built = true;
-  G.w = c->grid_w;
-  G.sigma = c->grid_sigma100 / 100.0;
-  G.err_bound = std::exp(-M_PI * G.w * std::sqrt(1.0 - 1.0 / G.sigma));
-  if (L.segs.empty()) {
-    G.why = "gridded path: no signals";
-    return FPTA_OK;
-  }
-  for (Seg* sg : L.segs)
-    if (!sg->d.harmonic) {
-      G.why = "gridded path: every signal needs a harmonic grid f_k = k f_1";
-      return FPTA_OK;
-    }
-  // grid signals: with FPTA_OPT_GRID_COALESCE, a signal joins the first earlier grid signal with the same base
-  // frequency w0 on every pulsar and the same chromatic weight (factor x mask) on every TOA. Their sums
-  // ch(t) sum_k c_k cos(k w0 t) + s_k sin(k w0 t) then add in coefficient space (k_coef_merge): one DFT, one band.
-  {
-    const int32_t n_layout = (int32_t)L.segs.size();
-    std::vector<std::vector<double>> chv(n_layout);
-    auto ch_of = [&](int32_t i) -> const std::vector<double>& {
-      if (chv[i].empty()) {
-        const SegDesc& d = L.segs[i]->d;
-        const std::vector<uint8_t>& m = L.segs[i]->h_mask;
-        chv[i].resize(L.n_toa);
-        for (int64_t t = 0; t < L.n_toa; ++t) {
-          double ch = 1.0;  // chrom_factor (device_common.h), same operations
-          if (d.idx != 0.0) {
-            const double x = d.freqf / L.h_nu[t];
-            ch = d.idx == 2.0 ? x * x : d.idx == 1.0 ? x : std::pow(x, d.idx);
-          }
-          chv[i][t] = (!m.empty() && !m[t]) ? 0.0 : ch;
-        }
-      }
-      return chv[i];
-    };
-    auto w0_of = [&](int32_t i, int32_t p) { return L.segs[i]->h_w0[L.segs[i]->d.kind == 0 ? p : 0]; };
-    for (int32_t i = 0; i < n_layout; ++i) {
-      int32_t join = -1;
-      for (size_t g = 0; c->grid_coalesce && g < G.members.size() && join < 0; ++g) {
-        // a grid signal merges at most kGridMaxSeg other members (CoefMerge::src): a full group starts a new one
-        if (G.members[g].size() > (size_t)kGridMaxSeg) continue;
-        const int32_t f = G.members[g][0];
-        bool same = true;
-        for (int32_t p = 0; p < L.P && same; ++p) same = w0_of(i, p) == w0_of(f, p);
-        if (same) same = ch_of(i) == ch_of(f);
-        if (same) join = (int32_t)g;
-      }
-      if (join < 0) {
-        G.members.push_back({i});
-      } else {
-        G.members[join].push_back(i);
-        G.merges = true;
-      }
-    }
-    for (const std::vector<int32_t>& m : G.members) {
-      int32_t a = m[0];
-      for (int32_t i : m)
-        if (L.segs[i]->d.nm > L.segs[a]->d.nm) a = i;
-      G.anchor.push_back(a);
-      G.last.push_back(m.back());
-    }
-  }
-  const int32_t n_seg = (int32_t)G.members.size();  // grid signals from here on
-  if (n_seg > kGridMaxSeg) {
-    G.why = "gridded path: needs 1.." + std::to_string(kGridMaxSeg) + " grid signals (after coalescing)";
-    return FPTA_OK;
-  }
-  const int64_t N = L.n_toa;
-  // per (segment, TOA): first interpolation row J (unwrapped) and offset d = u - J, u = theta / h
-  std::vector<std::vector<int64_t>> J(n_seg, std::vector<int64_t>(N));
-  std::vector<std::vector<double>> D(n_seg, std::vector<double>(N));
-  std::vector<int32_t> nf(n_seg), ws(n_seg);
-  std::vector<double> betas(n_seg);
-  // Per grid signal: the options' (w, sigma) give nf0 = sigma (2 N + 1) grid points, a multiple of 4 (the MFMA DFT
-  // runs on the quarter range); it computes whole blocks of kGridDftRows rows of the quarter range, so nf1 = 4 (rows
-  // of those blocks - 1) points cost it nothing more. The larger effective oversampling sigma1 = nf1 / (2 N + 1)
-  // reaches the options' a-priori bound with a narrower kernel w1; the signal takes (nf1, w1) when its interpolation
-  // band (w + the cells a 32-TOA chunk spans) is estimated narrower.
-  const double bound_target = G.err_bound;
-  G.err_bound = 0.0;
-  for (int32_t s = 0; s < n_seg; ++s) {
-    const Seg* sg = L.segs[G.anchor[s]];
-    const SegDesc& d = sg->d;
-    int32_t n = (int32_t)std::ceil(G.sigma * (2.0 * d.nm + 1.0));
-    int32_t n0 = (std::max(n, 2 * G.w + 2) + 3) / 4 * 4, w0 = G.w;
-    // grid cells per TOA per grid point: mean over pulsars of w0 dt / (2 pi), dt the mean TOA spacing
-    double rho = 0.0;
-    for (int32_t p = 0; p < L.P; ++p) {
-      const int64_t a0 = L.h_offs[p], a1 = L.h_offs[p + 1];
-      double tmin = L.h_toas[a0], tmax = L.h_toas[a0];
-      for (int64_t t = a0; t < a1; ++t) {
-        tmin = std::min(tmin, L.h_toas[t]);
-        tmax = std::max(tmax, L.h_toas[t]);
-      }
-      if (a1 - a0 > 1) rho += sg->h_w0[d.kind == 0 ? p : 0] * (tmax - tmin) / (double)(a1 - a0 - 1) / (2.0 * M_PI);
-    }
-    rho /= L.P;
-    const int32_t blocks = (n0 / 4 + kGridDftRows) / kGridDftRows;  // ceil((nf / 4 + 1) / rows per block)
-    const int32_t n1 = 4 * (blocks * kGridDftRows - 1);
-    const double sig1 = n1 / (2.0 * d.nm + 1.0);
-    int32_t w1 = G.w;
-    while (w1 > 4 && std::exp(-M_PI * (w1 - 1) * std::sqrt(1.0 - 1.0 / sig1)) <= bound_target) --w1;
-    const bool fill = n1 > n0 && 2 * w1 + 2 <= n1 && w1 + kGridTT * n1 * rho < w0 + kGridTT * n0 * rho - 0.25;
-    nf[s] = fill ? n1 : n0;
-    ws[s] = fill ? w1 : w0;
-    const double sig = nf[s] / (2.0 * d.nm + 1.0);
-    // shape parameter of the exponential-of-semicircle kernel for oversampling sigma (2.31 w at sigma = 2)
-    betas[s] = 0.98 * M_PI * ws[s] * (1.0 - 0.5 / sig);
-    G.err_bound = std::max(G.err_bound, std::exp(-M_PI * ws[s] * std::sqrt(1.0 - 1.0 / sig)));
-    const double hw = 0.5 * ws[s];
-    const double h = 2.0 * M_PI / nf[s];
-    for (int32_t p = 0; p < L.P; ++p) {
-      const double w0 = sg->h_w0[d.kind == 0 ? p : 0];
-      for (int64_t t = L.h_offs[p]; t < L.h_offs[p + 1]; ++t) {
-        const double u = (w0 * L.h_toas[t]) / h;
-        if (!std::isfinite(u) || std::fabs(u) > 1e15) {
-          G.why = "gridded path: phase out of range";
-          return FPTA_OK;
-        }
-        const int64_t j = (int64_t)std::floor(u - hw) + 1;
-        J[s][t] = j;
-        D[s][t] = u - (double)j;
-      }
-    }
-  }
-  // chunks: <= kGridTT consecutive TOAs of one pulsar, every signal's band <= kGridRowCap rows
-  std::vector<int4> chunks;
-  std::vector<int32_t> chunk_of(N), tt_of(N);
-  std::vector<std::vector<int64_t>> band_lo(n_seg);  // per chunk: first grid row (unwrapped) of each signal
-  std::vector<std::vector<int32_t>> band_n(n_seg);   // per chunk: band rows of each signal (span + w)
-  std::vector<int64_t> lo(n_seg), hi(n_seg);
-  for (int32_t p = 0; p < L.P; ++p) {
-    int64_t t = L.h_offs[p];
-    const int64_t t_end = L.h_offs[p + 1];
-    while (t < t_end) {
-      const int64_t t0 = t;
-      for (int32_t s = 0; s < n_seg; ++s) lo[s] = hi[s] = J[s][t];
-      ++t;
-      // chunks end on multiples of kGridTT in the global TOA index: every full chunk then writes whole
-      // 256-byte runs of each realization row
-      const int64_t t_lim = std::min(t_end, (t0 / kGridTT + 1) * kGridTT);
-      while (t < t_lim) {
-        bool fits = true;
-        for (int32_t s = 0; s < n_seg && fits; ++s)
-          fits = std::max(hi[s], J[s][t]) - std::min(lo[s], J[s][t]) + ws[s] + 1 <= kGridRowCap;
-        if (!fits) break;
-        for (int32_t s = 0; s < n_seg; ++s) {
-          lo[s] = std::min(lo[s], J[s][t]);
-          hi[s] = std::max(hi[s], J[s][t]);
-        }
-        ++t;
-      }
-      const int32_t ci = (int32_t)chunks.size();
-      chunks.push_back(make_int4(p, (int)(t0 - L.h_offs[p]), (int)(t - t0), 0));
-      for (int64_t u = t0; u < t; ++u) {
-        chunk_of[u] = ci;
-        tt_of[u] = (int32_t)(u - t0);
-      }
-      for (int32_t s = 0; s < n_seg; ++s) {
-        band_lo[s].push_back(lo[s]);
-        band_n[s].push_back((int32_t)(hi[s] - lo[s]) + ws[s]);
-        for (int64_t u = t0; u < t; ++u) J[s][u] -= lo[s];  // row of the TOA's first weight in its band
-      }
-    }
-  }
-  if (chunks.size() > (size_t)0x7FFFFFFF / 8) {
-    G.why = "gridded path: too many chunks";
-    return FPTA_OK;
-  }
-  G.n_chunks = (int32_t)chunks.size();
-  G.psr_chunk0.assign((size_t)L.P + 1, 0);
-  for (int32_t ci = (int32_t)chunks.size() - 1; ci >= 0; --ci) G.psr_chunk0[chunks[ci].x] = ci;
-  G.psr_chunk0[L.P] = G.n_chunks;
-  for (int32_t p = L.P - 1; p >= 0; --p)  // a pulsar without TOAs has no chunk: it starts where the next one does
-    if (L.h_offs[p + 1] == L.h_offs[p]) G.psr_chunk0[p] = G.psr_chunk0[p + 1];
-  if (int rc0 = upload(c, G.psr_c0, G.psr_chunk0.data(), sizeof(int32_t) * G.psr_chunk0.size(), "pulsar chunks"))
-    return rc0;
-  const int32_t n_chunks = G.n_chunks;
-  // band rows of a chunk: every signal's band back to back (virtual rows voff_s ..), padded to a multiple of
-  // 4 once per chunk (k_grid_interp_mfma: 4 rows per MFMA step; pad rows re-read a valid row at weight 0), and in
-  // diagnostic builds to at least kGridMinV rows (k_grid_interp_st's operand lookahead never passes the next chunk; the
-  // product kernels would only run zero-weight steps on them)
-  std::vector<int32_t> voff((size_t)n_seg * n_chunks);
-  int32_t vmax = 4;
-  for (int32_t ci = 0; ci < n_chunks; ++ci) {
-    int32_t v = 0;
-    for (int32_t s = 0; s < n_seg; ++s) {
-      voff[(size_t)s * n_chunks + ci] = v;
-      v += band_n[s][ci];
-    }
-#ifdef FPTA_DIAG_KERNELS
-    chunks[ci].w = std::max(kGridMinV, (v + 3) & ~3);
-#else
-    chunks[ci].w = (v + 3) & ~3;
-#endif
-    vmax = std::max(vmax, chunks[ci].w);
-  }
-  if (vmax > kGridVMax) {
-    G.why = "gridded path: a chunk's band rows over all signals exceed " + std::to_string(kGridVMax);
-    return FPTA_OK;
-  }
-  G.vmax = vmax;
-  std::vector<int64_t> rowoff(n_seg);
-  int64_t grid_rows = 0;
-  for (int32_t s = 0; s < n_seg; ++s) {
-    rowoff[s] = grid_rows;
-    grid_rows += (int64_t)L.P * nf[s];
-  }
-  if (grid_rows > 0x7FFFFFFF) {
-    G.why = "gridded path: grid too large";
-    return FPTA_OK;
-  }
-  G.grid_rows = grid_rows;
-  std::vector<int32_t> rt((size_t)n_chunks * vmax);
-  for (int32_t ci = 0; ci < n_chunks; ++ci) {
-    int32_t* r = rt.data() + (size_t)ci * vmax;
-    const int32_t p = chunks[ci].x;
-    int32_t v = 0;
-    for (int32_t s = 0; s < n_seg; ++s)
-      for (int32_t i = 0; i < band_n[s][ci]; ++i) {
-        const int64_t j = ((band_lo[s][ci] + i) % nf[s] + nf[s]) % nf[s];
-        r[v++] = (int32_t)(rowoff[s] + (int64_t)p * nf[s] + j);
-      }
-    for (; v < vmax; ++v) r[v] = r[0];
-  }
-  // k_grid_interp_wr (diagnostic kernel): ring slot kWrSlots s + (unwrapped row mod kWrSlots) per band row; load
-  // lists per chunk
-  std::vector<int4> wr_meta;
-  std::vector<int2> wr_list;
-  std::vector<int32_t> wr_slot;
-#ifdef FPTA_DIAG_KERNELS
-  bool wr_ok = n_seg <= kWrMaxSig && vmax <= kWrVMax;
-#else
-  bool wr_ok = false;
-#endif
-  for (int32_t s = 0; s < n_seg && wr_ok; ++s)
-    for (int32_t ci = 0; ci < n_chunks && wr_ok; ++ci) wr_ok = band_n[s][ci] <= kWrSlots;
-  if (wr_ok) {
-    wr_meta.resize(n_chunks);
-    wr_slot.assign((size_t)n_chunks * vmax, 0);
-    for (int32_t ci = 0; ci < n_chunks; ++ci) {
-      const int32_t p = chunks[ci].x;
-      int32_t* sl = wr_slot.data() + (size_t)ci * vmax;
-      int32_t v = 0;
-      for (int32_t s = 0; s < n_seg; ++s)
-        for (int32_t i = 0; i < band_n[s][ci]; ++i)
-          sl[v++] = kWrSlots * s + (int32_t)((band_lo[s][ci] + i) & (kWrSlots - 1));
-      for (; v < vmax; ++v) sl[v] = sl[0];
-      // the bands of chunks ci - back .. ci (same pulsar) in one ring window per signal: compat (back 1) = only the rows
-      // the previous band does not hold load, after the chunk before has been computed; near (back 2) = they may load
-      // while the chunk two back is computed
-      auto window = [&](int32_t back) {
-        if (ci < back) return false;
-        for (int32_t b = 1; b <= back; ++b)
-          if (chunks[ci - b].x != p) return false;
-        for (int32_t s = 0; s < n_seg; ++s) {
-          int64_t lo = band_lo[s][ci], hi = band_lo[s][ci] + band_n[s][ci];
-          for (int32_t b = 1; b <= back; ++b) {
-            lo = std::min(lo, band_lo[s][ci - b]);
-            hi = std::max(hi, band_lo[s][ci - b] + (int64_t)band_n[s][ci - b]);
-          }
-          if (hi - lo > kWrSlots) return false;
-        }
-        return true;
-      };
-      const bool compat = window(1), near = compat && window(2);
-      auto add_rows = [&](bool only_new) {
-        int32_t n = 0;
-        for (int32_t s = 0; s < n_seg; ++s)
-          for (int32_t i = 0; i < band_n[s][ci]; ++i) {
-            const int64_t u = band_lo[s][ci] + i;
-            if (only_new && u >= band_lo[s][ci - 1] && u < band_lo[s][ci - 1] + band_n[s][ci - 1]) continue;
-            const int64_t j = (u % nf[s] + nf[s]) % nf[s];
-            wr_list.push_back(make_int2(kWrSlots * s + (int32_t)(u & (kWrSlots - 1)),
-                                        (int32_t)(rowoff[s] + (int64_t)p * nf[s] + j)));
-            ++n;
-          }
-        return n;
-      };
-      const int32_t full_off = (int32_t)wr_list.size();
-      const int32_t full_n = add_rows(false);
-      int32_t new_off = full_off, new_n = full_n;
-      if (compat) {
-        new_off = (int32_t)wr_list.size();
-        new_n = add_rows(true);
-      }
-      wr_meta[ci] = make_int4(full_off, full_n, new_off, new_n | (compat ? 0 : kWrFresh) | (near ? 0 : kWrFar));
-    }
-  }
-  // LDS-staged interpolation (k_grid_interp_lds): groups of <= kLdsGroup consecutive chunks of one pulsar whose
-  // bands, over all signals, unite to <= kLdsRowsMax rows. Per group the union's grid-buffer rows (signal by
-  // signal, each signal's rows one contiguous unwrapped range), per chunk the union slot of each band row.
-  std::vector<int4> groups;
-  std::vector<int32_t> urows, lrt((size_t)n_chunks * vmax);
-  int32_t umax = 0;
-  bool lds_ok = true;
-  for (int32_t ci = 0; ci < n_chunks && lds_ok;) {
-    const int32_t p = chunks[ci].x;
-    auto union_rows = [&](int32_t n) {
-      int64_t u = 0;
-      for (int32_t s = 0; s < n_seg; ++s) {
-        int64_t lo = band_lo[s][ci], end = band_lo[s][ci] + band_n[s][ci];
-        for (int32_t k = 1; k < n; ++k) {
-          lo = std::min(lo, band_lo[s][ci + k]);
-          end = std::max(end, band_lo[s][ci + k] + (int64_t)band_n[s][ci + k]);
-        }
-        u += end - lo;
-      }
-      return u;
-    };
-    int32_t n = 1;
-    while (n < kLdsGroup && ci + n < n_chunks && chunks[ci + n].x == p && union_rows(n + 1) <= kLdsRowsMax) ++n;
-    const int64_t U = union_rows(n);
-    if (U > kLdsRowsMax) {
-      lds_ok = false;  // one chunk's bands alone exceed the LDS budget: the register-tiled kernel serves the layout
-      break;
-    }
-    groups.push_back(make_int4(ci, n, (int32_t)U, (int32_t)urows.size()));
-    umax = std::max(umax, (int32_t)U);
-    int32_t uoff = 0;
-    for (int32_t s = 0; s < n_seg; ++s) {
-      int64_t lo = band_lo[s][ci], end = band_lo[s][ci] + band_n[s][ci];
-      for (int32_t k = 1; k < n; ++k) {
-        lo = std::min(lo, band_lo[s][ci + k]);
-        end = std::max(end, band_lo[s][ci + k] + (int64_t)band_n[s][ci + k]);
-      }
-      for (int64_t j = lo; j < end; ++j)
-        urows.push_back((int32_t)(rowoff[s] + (int64_t)p * nf[s] + ((j % nf[s]) + nf[s]) % nf[s]));
-      for (int32_t k = 0; k < n; ++k) {  // chunk ci + k: signal s's band rows start at slot uoff + (its lo - lo)
-        int32_t v = 0;
-        for (int32_t s2 = 0; s2 < s; ++s2) v += band_n[s2][ci + k];
-        for (int32_t i = 0; i < band_n[s][ci + k]; ++i)
-          lrt[(size_t)(ci + k) * vmax + v + i] = uoff + (int32_t)(band_lo[s][ci + k] - lo) + i;
-      }
-      uoff += (int32_t)(end - lo);
-    }
-    for (int32_t k = 0; k < n; ++k) {  // pad rows: any valid slot (weight 0)
-      int32_t* r = lrt.data() + (size_t)(ci + k) * vmax;
-      int32_t v = 0;
-      for (int32_t s = 0; s < n_seg; ++s) v += band_n[s][ci + k];
-      for (; v < vmax; ++v) r[v] = r[0];
-    }
-    ci += n;
-  }
-  G.lds_ok = lds_ok && !groups.empty();
-  G.n_groups = (int32_t)groups.size();
-  G.lds_rows = umax;
-  // k_grid_interp_u plan (diagnostic builds): the same grouping under the tighter LDS budget of two workgroups per CU
-  std::vector<int4> ug;
-  std::vector<int32_t> uur, ucb, uwr;
-#ifdef FPTA_DIAG_KERNELS
-  bool u_ok = n_seg <= kUnionSigMax;
-#else
-  bool u_ok = false;
-#endif
-  for (int32_t ci = 0; ci < n_chunks && u_ok;) {
-    const int32_t p = chunks[ci].x;
-    auto span = [&](int32_t s, int32_t n, int64_t& lo, int64_t& end) {
-      lo = band_lo[s][ci];
-      end = band_lo[s][ci] + band_n[s][ci];
-      for (int32_t k = 1; k < n; ++k) {
-        lo = std::min(lo, band_lo[s][ci + k]);
-        end = std::max(end, band_lo[s][ci + k] + (int64_t)band_n[s][ci + k]);
-      }
-    };
-    auto union_rows = [&](int32_t n) {
-      int64_t u = 0, lo, end;
-      for (int32_t s = 0; s < n_seg; ++s) {
-        span(s, n, lo, end);
-        u += end - lo;
-      }
-      return u;
-    };
-    int32_t n = 1;
-    while (n < kUnionGroup && ci + n < n_chunks && chunks[ci + n].x == p && union_rows(n + 1) <= kUnionRowsMax) ++n;
-    const int64_t U = union_rows(n);
-    if (U > kUnionRowsMax) {
-      u_ok = false;
-      break;
-    }
-    ug.push_back(make_int4(ci, n, (int32_t)U, (int32_t)uur.size()));
-    int32_t uoff = 0;
-    std::vector<int32_t> cb((size_t)n * 2 * kUnionSigMax, 0);
-    for (int32_t s = 0; s < n_seg; ++s) {
-      int64_t lo, end;
-      span(s, n, lo, end);
-      for (int64_t j = lo; j < end; ++j)
-        uur.push_back((int32_t)(rowoff[s] + (int64_t)p * nf[s] + ((j % nf[s]) + nf[s]) % nf[s]));
-      for (int32_t k = 0; k < n; ++k) {
-        const int32_t vo = voff[(size_t)s * n_chunks + ci + k];
-        cb[(size_t)k * 2 * kUnionSigMax + s] = vo;
-        cb[(size_t)k * 2 * kUnionSigMax + kUnionSigMax + s] = uoff + (int32_t)(band_lo[s][ci + k] - lo) - vo;
-      }
-      uoff += (int32_t)(end - lo);
-    }
-    for (int32_t k = 0; k < n; ++k)
-      for (int32_t s = n_seg; s < kUnionSigMax; ++s) {  // absent signals: never selected (offset past every row)
-        cb[(size_t)k * 2 * kUnionSigMax + s] = 1 << 20;
-        cb[(size_t)k * 2 * kUnionSigMax + kUnionSigMax + s] = 0;
-      }
-    ucb.insert(ucb.end(), cb.begin(), cb.end());
-    ci += n;
-  }
-  G.u_ok = u_ok && !ug.empty();
-  G.u_groups = (int32_t)ug.size();
-  G.u_sig = n_seg;
-  if (G.u_ok) {
-    uwr.assign((size_t)n_chunks * n_seg * kGridTT, -(1 << 20));  // empty TOA slots: every weight 0
-    for (int32_t s = 0; s < n_seg; ++s)
-      for (int64_t t = 0; t < N; ++t)
-        uwr[((size_t)chunk_of[t] * n_seg + s) * kGridTT + tt_of[t]] =
-            (int32_t)J[s][t] + voff[(size_t)s * n_chunks + chunk_of[t]];
-    for (int32_t s = 0; s < n_seg; ++s) {
-      G.u_w[s] = ws[s];
-      G.u_hw[s] = 0.5 * (double)ws[s];
-      G.u_beta[s] = betas[s];
-    }
-  }
-  int rc;
-  G.wr_ok = wr_ok;
-  if (wr_ok && ((rc = upload(c, G.wr_meta, wr_meta.data(), sizeof(int4) * wr_meta.size(), "window plan")) ||
-                (rc = upload(c, G.wr_list, wr_list.data(), sizeof(int2) * std::max<size_t>(wr_list.size(), 1),
-                             "window rows")) ||
-                (rc = upload(c, G.wr_slot, wr_slot.data(), sizeof(int32_t) * wr_slot.size(), "window slots"))))
-    return rc;
-  if ((rc = upload(c, G.chunks, chunks.data(), sizeof(int4) * chunks.size(), "grid chunks")) ||
-      (rc = upload(c, G.rows, rt.data(), sizeof(int32_t) * rt.size(), "grid band rows")))
-    return rc;
-  if (G.lds_ok && ((rc = upload(c, G.groups, groups.data(), sizeof(int4) * groups.size(), "grid groups")) ||
-                   (rc = upload(c, G.urows, urows.data(), sizeof(int32_t) * urows.size(), "grid union rows")) ||
-                   (rc = upload(c, G.lrows, lrt.data(), sizeof(int32_t) * lrt.size(), "grid LDS rows"))))
-    return rc;
-  if (G.u_ok) {
-    if ((rc = upload(c, G.ugroups, ug.data(), sizeof(int4) * ug.size(), "union groups")) ||
-        (rc = upload(c, G.uurows, uur.data(), sizeof(int32_t) * uur.size(), "union rows")) ||
-        (rc = upload(c, G.ucbase, ucb.data(), sizeof(int32_t) * ucb.size(), "union bases")) ||
-        (rc = upload(c, G.uwrow, uwr.data(), sizeof(int32_t) * uwr.size(), "union window rows")))
-      return rc;
-    const size_t dbytes = sizeof(double) * 2 * (size_t)n_chunks * n_seg * kGridTT;
-    HIPCHK(c, G.udch.ensure(dbytes), "union weight parameters alloc");
-    HIPCHK(c, hipMemsetAsync(G.udch.p, 0, dbytes, c->stream), "union weight parameters memset");
-  }
-  DevBuf d_chunk_of, d_tt_of, d_row, d_d;
-  if ((rc = upload(c, d_chunk_of, chunk_of.data(), sizeof(int32_t) * N, "grid chunk_of")) ||
-      (rc = upload(c, d_tt_of, tt_of.data(), sizeof(int32_t) * N, "grid tt_of")))
-    return rc;
-  // + kFusedWdPad band rows after the last chunk: k_grid_fused loads NQ band steps' weights of every chunk unclamped
-  const size_t wbytes = sizeof(double) * ((size_t)n_chunks * vmax + kFusedWdPad) * kGridTT;
-  HIPCHK(c, G.wd.ensure(wbytes), "grid weights alloc");
-  HIPCHK(c, hipMemsetAsync(G.wd.p, 0, wbytes, c->stream), "grid weights memset");
-  std::vector<double> gx, gw;
-  gauss_legendre(256, gx, gw);
-  G.fma_direct = 0.0;
-  G.fma_grid = 0.0;
-  G.fma_interp = 0.0;
-  G.fma_dft = 0.0;
-  G.grid_vals = 0.0;
-  for (int32_t ci = 0; ci < n_chunks; ++ci) G.fma_interp += (double)chunks[ci].w * kGridTT;
-  G.mean_v = G.fma_interp / kGridTT / std::max(n_chunks, 1);
-  G.weight_bytes = (double)wbytes;
-  for (Seg* sg : L.segs) G.fma_direct += 2.0 * sg->d.nm * (double)N;
-  for (int32_t s = 0; s < n_seg; ++s) {
-    const SegDesc& d = L.segs[G.anchor[s]]->d;
-    GridSeg* gs = new GridSeg();
-    G.segs.push_back(gs);
-    gs->nf = nf[s];
-    gs->half = nf[s] / 2;
-    gs->lde = (gs->half + kGridDftRows) / kGridDftRows * kGridDftRows;  // row blocks of k_grid_dft_mfma and k_grid_dft
-    gs->ntab = (d.nm + 7) / 8 * 8;         // whole pairs of 4-mode MFMA k-steps (zero rows)
-    gs->rowoff = rowoff[s];
-    // q_k = (2 pi / nf) / phi_hat(k), phi_hat(k) = alpha int_{-1}^{1} phi(z) cos(k alpha z) dz, alpha = pi w / nf
-    const double alpha = M_PI * ws[s] / nf[s], beta = betas[s];
-    std::vector<double> ec((size_t)gs->ntab * gs->lde, 0.0), es((size_t)gs->ntab * gs->lde, 0.0);
-    for (int32_t m = 0; m < d.nm; ++m) {
-      const int64_t k = m + 1;
-      double ph = 0.0;
-      for (size_t q = 0; q < gx.size(); ++q)
-        ph += gw[q] * std::exp(beta * (std::sqrt(1.0 - gx[q] * gx[q]) - 1.0)) * std::cos(k * alpha * gx[q]);
-      const double qk = (2.0 * M_PI / nf[s]) / (alpha * ph);
-      for (int32_t j = 0; j <= gs->half; ++j) {
-        const double a = 2.0 * M_PI * (double)((k * j) % nf[s]) / nf[s];  // exact argument reduction
-        ec[(size_t)m * gs->lde + j] = qk * std::cos(a);
-        es[(size_t)m * gs->lde + j] = qk * std::sin(a);
-      }
-    }
-    if ((rc = upload(c, gs->ecos, ec.data(), sizeof(double) * ec.size(), "grid ecos")) ||
-        (rc = upload(c, gs->esin, es.data(), sizeof(double) * es.size(), "grid esin")))
-      return rc;
-    // quarter-range tables by parity: [0] cos / [1] sin of odd k = 2 t + 1 (m = 2 t), [2] / [3] of even k = 2 t + 2
-    gs->ldq = (nf[s] / 4 + kGridDftRows) / kGridDftRows * kGridDftRows;
-    gs->ntq = ((d.nm + 1) / 2 + 7) / 8 * 8;
-    std::vector<double> tq((size_t)4 * gs->ntq * gs->ldq, 0.0);
-    for (int32_t m = 0; m < d.nm; ++m) {
-      const int32_t par = m & 1, t = m >> 1;
-      for (int32_t j = 0; j <= nf[s] / 4; ++j) {
-        tq[((size_t)(2 * par) * gs->ntq + t) * gs->ldq + j] = ec[(size_t)m * gs->lde + j];
-        tq[((size_t)(2 * par + 1) * gs->ntq + t) * gs->ldq + j] = es[(size_t)m * gs->lde + j];
-      }
-    }
-    if ((rc = upload(c, gs->tq, tq.data(), sizeof(double) * tq.size(), "grid quarter tables"))) return rc;
-    // weight rows of signal s: its band's virtual offset in the chunk + the TOA's first row in the band
-    std::vector<int32_t> row(N);
-    for (int64_t t = 0; t < N; ++t) row[t] = (int32_t)J[s][t] + voff[(size_t)s * n_chunks + chunk_of[t]];
-    if ((rc = upload(c, d_row, row.data(), sizeof(int32_t) * N, "grid rows")) ||
-        (rc = upload(c, d_d, D[s].data(), sizeof(double) * N, "grid offsets")))
-      return rc;
-    HIPCHK(c,
-           launch_grid_weights(c->stream, d, N, L.nu.as<double>(), d_chunk_of.as<int32_t>(), d_tt_of.as<int32_t>(),
-                               d_row.as<int32_t>(), d_d.as<double>(), ws[s], beta, vmax, G.wd.as<double>(),
-                               G.u_ok ? G.udch.as<double>() : nullptr, s, n_seg),
-           "k_grid_weights launch");
-    HIPCHK(c, hipStreamSynchronize(c->stream), "grid weights sync");  // d_row / d_d are reused
-    // multiply-adds per realization: quarter range by parity on MFMA, half range on VALU
-    G.fma_dft += (double)L.P * ((c->grid_mfma & 1) ? (gs->nf / 4 + 1) * 2.0 * d.nm : (gs->half + 1) * 2.0 * d.nm);
-    G.grid_vals += (double)L.P * gs->nf;
-    G.fma_grid = G.fma_dft + G.fma_interp;
-  }
-  // k_grid_fused: the grids of kFusedReal realizations plus the draw ring fit in LDS, n_seg <= kFusedMaxSig, and every
-  // 32-row DFT chunk is one DFT wave's job
-  {
-    int32_t jobs = 0, rows = 0;
-    bool ok = n_seg <= kFusedMaxSig;
-    for (int32_t s = 0; s < n_seg && ok; ++s) {
-      const GridSeg* gs = G.segs[s];
-      ok = gs->nf % 4 == 0 && gs->ldq == (gs->nf / 4 + 32) / 32 * 32;
-      G.fused_lrow0.push_back(rows);
-      jobs += (gs->nf / 4 + 32) / 32;
-      rows += gs->nf;
-    }
-    const size_t lds = sizeof(double) * ((size_t)rows * kFusedPitch + 2 * kFusedMaxSig * kFusedSlot) + 16;
-    for (const std::vector<int32_t>& m : G.members) ok = ok && m.size() <= (size_t)kDftGenTerms;
-    ok = ok && jobs <= kFusedDW && lds <= (size_t)kFusedLdsMax;
-    if (ok) {
-      // [n_chunks][4][fq]: band row 4 q + j of a chunk at [j][q] (a lane's rows of consecutive steps contiguous: 16-byte
-      // loads), fq = the band steps rounded up to 4 and at least kFusedNQ; steps past the chunk's repeat its first row
-      const int32_t fq = std::max(kFusedNQ, (vmax / 4 + 3) & ~3);
-      std::vector<int32_t> band_row(vmax);
-      std::vector<int32_t> lrt((size_t)n_chunks * 4 * fq);
-      for (int32_t ci = 0; ci < n_chunks; ++ci) {
-        int32_t v = 0;
-        for (int32_t s = 0; s < n_seg; ++s)
-          for (int32_t i = 0; i < band_n[s][ci]; ++i)
-            band_row[v++] = G.fused_lrow0[s] + (int32_t)(((band_lo[s][ci] + i) % nf[s] + nf[s]) % nf[s]);
-        for (; v < vmax; ++v) band_row[v] = band_row[0];
-        int32_t* r = lrt.data() + (size_t)ci * 4 * fq;
-        for (int32_t j = 0; j < 4; ++j)
-          for (int32_t q = 0; q < fq; ++q) r[j * fq + q] = 4 * q + j < vmax ? band_row[4 * q + j] : band_row[0];
-      }
-      if ((rc = upload(c, G.frows, lrt.data(), sizeof(int32_t) * lrt.size(), "fused LDS rows"))) return rc;
-      G.fused_fq = fq;
-      G.fused_lds = lds;
-    }
-    G.fused_ok = ok;
-  }
-  G.ok = true;
-  return FPTA_OK;
-}
-
-// Partial-checksum groups of G: each pulsar's chunks cut into runs of <= size consecutive chunks (a group never spans
-// two pulsars, so a workgroup that owns a pulsar owns its groups), uploaded once per (plan, size).
-int grid_part_groups(fpta_ctx* c, GridPlan& G, int32_t P, int32_t size) {
-  if (G.pg_size == size) return FPTA_OK;
-  std::vector<int32_t> first, psr((size_t)P + 1);
-  for (int32_t p = 0; p < P; ++p) {
-    psr[p] = (int32_t)first.size();
-    for (int32_t ci = G.psr_chunk0[p]; ci < G.psr_chunk0[p + 1]; ci += size) first.push_back(ci);
-  }
-  psr[P] = (int32_t)first.size();
-  first.push_back(G.n_chunks);
-  int rc;
-  if ((rc = upload(c, G.pgfirst, first.data(), sizeof(int32_t) * first.size(), "partial groups")) ||
-      (rc = upload(c, G.psr_pg, psr.data(), sizeof(int32_t) * psr.size(), "partial groups of pulsars")))
-    return rc;
-  G.n_pg = (int32_t)first.size() - 1;
-  G.pg_size = size;
-  return FPTA_OK;
-}
-
-// Run the gridded synthesis: one DFT launch per grid signal, then one interpolation launch for all.
-// pipe (run_coefficients drew this block on the side stream in pipelined mode): the DFTs follow there, into grid
-// buffer c->gbuf, and the interpolation on the ctx stream waits only for them.
-int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad, bool pipe = false) {
-  GridPlan& G = L.grid;
-  GridSegs gsegs{};
-  gsegs.n = (int32_t)G.segs.size();
-  const size_t gbytes = sizeof(double) * (size_t)G.grid_rows * R_pad;
-  // k_grid_interp_psr: no DFT launch, no grid buffer; in a pipelined block the coefficients drawn on the side stream
-  // into buffer gi are this block's (run_coefficients)
-  const bool psr = psr_layout(c, L) && !a.w_on && !a.accumulate && (!pipe || c->prev_psr);
-  // k_grid_fused: the DFTs run inside the synthesis kernel too (plain blocks: no white epilogue, no partial checksums)
-  const bool fused = !psr && fused_layout(c, L) && !a.w_on && !a.accumulate &&
-                     !(c->fuse_sums && a.out == c->out.as<double>()) && (!pipe || c->prev_psr);
-  // grid buffers only for the kernels that read one (two of 0.41 GB each on C2)
-  if (!psr && !fused && (G.g_rpad != R_pad || (pipe && G.g2.cap < gbytes))) {
-    if (c->side) HIPCHK(c, hipStreamSynchronize(c->side), "side sync");  // no reader of a buffer being regrown
-    if (c->side2) HIPCHK(c, hipStreamSynchronize(c->side2), "side sync");
-    HIPCHK(c, hipStreamSynchronize(c->stream), "grid regrow sync");
-    HIPCHK(c, G.g.ensure(gbytes), "grid alloc");
-    if (pipe) HIPCHK(c, G.g2.ensure(gbytes), "grid alloc");
-    G.g_rpad = R_pad;
-  }
-  const int gi = pipe ? c->gbuf : 0;
-  double* const gbase = gi ? G.g2.as<double>() : G.g.as<double>();
-  if (pipe) {
-    for (hipEvent_t* e : {&c->ev_gready, &c->ev_gfree[0], &c->ev_gfree[1]})
-      if (!*e) HIPCHK(c, hipEventCreateWithFlags(e, hipEventDisableTiming), "event create");
-    // the DFT overwrites buffer gi: the interpolation that last read it (two blocks back) must be done
-    if (c->gfree_set[gi]) HIPCHK(c, hipStreamWaitEvent(c->side, c->ev_gfree[gi], 0), "grid buffer wait");
-  }
-  if (psr || fused) {
-    GridSeg* gs = G.segs[0];
-    GridSegDev& g = gsegs.s[0];
-    g.g = nullptr;
-    g.nf = gs->nf;
-    g.half = gs->half;
-    g.nm = L.segs[G.anchor[0]]->d.nm;
-    g.col0 = L.segs[G.anchor[0]]->d.col0;
-    g.tq = gs->tq.as<double>();
-    g.ldq = gs->ldq;
-    g.ntq = gs->ntq;
-    if (pipe) {
-      HIPCHK(c, hipEventRecord(c->ev_gready, c->side), "event record");
-      c->coef_last_side = false;  // the interpolation on the ctx stream reads the coefficients
-    } else {
-      int rc = wait_coef_all(c);
-      if (rc) return rc;
-    }
-  } else {
-    KTimer kt(c, FPTA_K_GRID, pipe ? c->side : c->stream);
-    for (size_t s = 0; s < G.segs.size(); ++s) {
-      GridSeg* gs = G.segs[s];
-      const SegDesc& d = L.segs[G.anchor[s]]->d;  // a coalesced grid signal reads its anchor's merged columns
-      GridSegDev& g = gsegs.s[s];
-      g.ecos = gs->ecos.as<double>();
-      g.esin = gs->esin.as<double>();
-      g.g = gbase + gs->rowoff * R_pad;
-      g.nf = gs->nf;
-      g.half = gs->half;
-      g.lde = gs->lde;
-      g.nm = d.nm;
-      g.col0 = d.col0;
-      g.ntab = gs->ntab;
-      g.tq = gs->tq.as<double>();
-      g.ldq = gs->ldq;
-      g.ntq = gs->ntq;
-    }
-    const bool early_free = c->coef_side && !c->coef_copy_pending;
-    const int32_t split = pipe && c->split_g < gsegs.n ? c->split_g : -1;
-    c->split_g = -1;
-    // the DFTs of a set of grid signals on one stream: each k_grid_dft_gen signal its own launch, the others in one
-    // k_grid_dft_mfma / k_grid_dft launch
-    auto dfts = [&](hipStream_t sd, const std::vector<int32_t>& sigs) -> int {
-      GridSegs rest{};
-      for (int32_t s : sigs) {
-        if (!grid_gen_fused(c, L, (size_t)s)) {
-          rest.s[rest.n++] = gsegs.s[s];
-          continue;
-        }
-        DftGenArgs d{};
-        d.g = gsegs.s[s];
-        std::vector<int32_t> order{G.anchor[s]};  // the merge order: anchor, then the others in layout order
-        for (int32_t i : G.members[s])
-          if (i != G.anchor[s]) order.push_back(i);
-        for (int32_t i : order) {
-          const SegDesc& sd2 = L.segs[i]->d;
-          d.term_kind[d.n_terms] = sd2.kind;
-          d.term_seg[d.n_terms] = i;
-          d.term_nm[d.n_terms] = sd2.nm;
-          d.term_col0[d.n_terms] = sd2.col0;
-          d.term_amp[d.n_terms] = sd2.amp;
-          ++d.n_terms;
-        }
-        d.coef = a.coef;
-        d.P = L.P;
-        d.K = a.K;
-        d.R_pad = R_pad;
-        d.n_real = a.n_real;
-        d.real0 = c->blk_real0;
-        d.k0 = c->blk_k0;
-        d.k1 = c->blk_k1;
-        HIPCHK(c, launch_grid_dft_gen(sd, d), "k_grid_dft_gen launch");
-      }
-      if (rest.n)
-        HIPCHK(c,
-               (c->grid_mfma & 1) ? launch_grid_dft_mfma(sd, rest, L.P, a.coef, a.K, R_pad)
-                                  : launch_grid_dft(sd, rest, L.P, a.coef, a.K, R_pad),
-               "k_grid_dft launch");
-      return FPTA_OK;
-    };
-    std::vector<int32_t> all_sigs(gsegs.n);
-    for (int32_t s = 0; s < gsegs.n; ++s) all_sigs[s] = s;
-    if (pipe && split >= 0) {
-      // the split signal's DFT on side2 (after its draws there), the others' on side
-      std::vector<int32_t> rest_sigs;
-      for (int32_t s = 0; s < gsegs.n; ++s)
-        if (s != split) rest_sigs.push_back(s);
-      {
-        if (c->gfree_set[gi]) HIPCHK(c, hipStreamWaitEvent(c->side2, c->ev_gfree[gi], 0), "grid buffer wait");
-        if (c->side_split == 2) {
-          if (!c->ev_s2mix) HIPCHK(c, hipEventCreateWithFlags(&c->ev_s2mix, hipEventDisableTiming), "event create");
-          HIPCHK(c, hipEventRecord(c->ev_s2mix, c->side), "event record");
-          HIPCHK(c, hipStreamWaitEvent(c->side2, c->ev_s2mix, 0), "side wait");
-        }
-        KTimer kt2(c, FPTA_K_GRID, c->side2);
-        int rc = dfts(c->side2, {split});
-        if (rc) return rc;
-      }
-      HIPCHK(c, hipEventRecord(c->ev_gready2, c->side2), "event record");
-      c->s2done_set = true;
-      int rc = dfts(c->side, rest_sigs);
-      if (rc) return rc;
-    } else if (pipe) {
-      int rc = dfts(c->side, all_sigs);
-      if (rc) return rc;
-    } else if (c->coef_side) {
-      // one DFT launch per grid signal, each after that signal's draws (and merge) only (side stream); in the
-      // order their draws complete
-      std::vector<int32_t> order(gsegs.n);
-      for (int32_t s = 0; s < gsegs.n; ++s) order[s] = s;
-      std::stable_sort(order.begin(), order.end(), [&](int32_t x, int32_t y) { return G.last[x] < G.last[y]; });
-      for (int32_t s : order) {
-        GridSegs one{};
-        one.s[0] = gsegs.s[s];
-        one.n = 1;
-        int rc = wait_coef(c, (size_t)G.last[s]);
-        if (rc) return rc;
-        HIPCHK(c,
-               (c->grid_mfma & 1) ? launch_grid_dft_mfma(c->stream, one, L.P, a.coef, a.K, R_pad)
-                                  : launch_grid_dft(c->stream, one, L.P, a.coef, a.K, R_pad),
-               "k_grid_dft launch");
-      }
-      c->coef_side = false;
-    } else {
-      int rc = dfts(c->stream, all_sigs);
-      if (rc) return rc;
-    }
-    if (pipe) {
-      HIPCHK(c, hipEventRecord(c->ev_gready, c->side), "event record");
-      c->coef_last_side = !c->coef_copy_pending;  // else the download on the ctx stream is the last reader
-    } else if (early_free) {  // the DFT was the last reader of coef: the next block may draw during the interpolation
-      if (!c->ev_coef_free) HIPCHK(c, hipEventCreateWithFlags(&c->ev_coef_free, hipEventDisableTiming), "event create");
-      HIPCHK(c, hipEventRecord(c->ev_coef_free, c->stream), "event record");
-      c->coef_free_set = true;
-    }
-  }
-  // partial checksums of a batch block (written into the context's own block, not accumulated)
-  if (c->fuse_sums && a.out == c->out.as<double>() && !a.accumulate) {
-    const int pi = c->part_next;
-    DevBuf& pb = c->part[pi];
-    const size_t pbytes = sizeof(double) * 2 * (size_t)G.n_chunks * R_pad;
-    if (pb.cap < pbytes && c->red) HIPCHK(c, hipStreamSynchronize(c->red), "partials regrow sync");
-    HIPCHK(c, pb.ensure(pbytes), "partial checksums alloc");
-    // the reduction of the block that last wrote this buffer (on the red stream) must have read it
-    if (c->pfree_set[pi]) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_pfree[pi], 0), "partials buffer wait");
-    a.part = pb.as<double>();
-    int rc = grid_part_groups(c, G, L.P, c->part_group);
-    if (rc) return rc;
-    c->part_cur = pi;
-    c->part_next = pi ^ 1;
-  }
-  if (pipe) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_gready, 0), "grid ready wait");
-  if (pipe && c->s2done_set) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_gready2, 0), "grid ready wait");
-  KTimer kt(c, FPTA_K_SYNTH);
-  GridBand band{G.chunks.as<int4>(), G.rows.as<int32_t>(), G.wd.as<double>(), gbase, G.n_chunks, G.vmax,
-                G.grid_rows, a.part ? G.pgfirst.as<int32_t>() : nullptr, a.part ? G.n_pg : G.n_chunks};
-  // the warp-specialised kernel for plain blocks; with fused partial checksums its reduce-scatter temporaries take
-  // its VGPRs to 230 and the register kernel is faster (C3: 47.9 vs 52.5 ms per job, profiles/r02k_ab_c2c3_ws.txt)
-  // k_grid_interp_ws tiles 512 realizations (4 compute waves x 128): when R_pad leaves some of the last tile's compute
-  // waves idle, the 256-realization tiles of k_grid_interp_ws2 waste less (C4, R_pad = 256: half of every ws tile;
-  // 6.8-7.4 vs 8.4 ms/step, profiles/r04a_c4_ws2.txt)
-  const bool ws2_fits = c->interp_ws == 1 && (R_pad + 255) / 256 * 256 - R_pad < (R_pad + 511) / 512 * 512 - R_pad;
-  int kind;  // the interpolation kernel (fpta_batch_grid_info_n slot 15)
-  if (false) {
-#ifdef FPTA_DIAG_KERNELS
-  } else if (c->interp_ws == 5 && !c->interp_lds && G.u_ok && !a.w_on) {
-    kind = 5;
-    band.pgfirst = nullptr;  // the diagnostic kernels write one partial row per chunk
-    band.n_pg = G.n_chunks;
-    GridUnion un{G.ugroups.as<int4>(), G.uurows.as<int32_t>(), G.ucbase.as<int32_t>(), G.udch.as<double>(),
-                 G.uwrow.as<int32_t>(), G.u_groups, G.u_sig, {G.u_w[0], G.u_w[1]}, {G.u_hw[0], G.u_hw[1]},
-                 {G.u_beta[0], G.u_beta[1]}};
-    HIPCHK(c, launch_grid_interp_u(c->stream, a, band, un, R_pad), "k_grid_interp_u launch");
-  } else if (c->interp_ws == 4 && !c->interp_lds) {
-    kind = 4;
-    band.pgfirst = nullptr;
-    band.n_pg = G.n_chunks;
-    HIPCHK(c, launch_grid_interp_st(c->stream, a, band, R_pad), "k_grid_interp_st launch");
-  } else if (c->interp_wr && G.wr_ok && !c->interp_lds && c->interp_ws > 0 && !a.w_on && !a.accumulate && !a.part &&
-             R_pad % kWrReal == 0 && !psr) {
-    kind = 10;
-    GridWindow wrp{G.wr_meta.as<int4>(), G.wr_list.as<int2>(), G.wr_slot.as<int32_t>()};
-    HIPCHK(c, launch_grid_interp_wr(c->stream, a, band, wrp, R_pad), "k_grid_interp_wr launch");
-#endif
-  } else if (fused) {
-    const int32_t nq = G.vmax / 4;
-    kind = nq <= 8 ? 8 : 9;  // launch_grid_fused: NQ = 8 or 12 band steps at a time
-    FusedArgs f{};
-    f.n_sig = (int32_t)G.segs.size();
-    for (int32_t s = 0; s < f.n_sig; ++s) {
-      const GridSeg* gs = G.segs[s];
-      const SegDesc& d = L.segs[G.anchor[s]]->d;
-      FusedSig& fs = f.s[s];
-      fs.tq = gs->tq.as<double>();
-      fs.ldq = gs->ldq;
-      fs.ntq = gs->ntq;
-      fs.nf = gs->nf;
-      fs.nm = d.nm;
-      fs.lrow0 = G.fused_lrow0[s];
-      fs.n_rc = (gs->nf / 4 + 32) / 32;
-      if (grid_gen_fused(c, L, (size_t)s)) {  // k_grid_dft_gen's terms: the anchor, then the others in layout order
-        std::vector<int32_t> order{G.anchor[s]};
-        for (int32_t i : G.members[s])
-          if (i != G.anchor[s]) order.push_back(i);
-        for (int32_t i : order) {
-          const SegDesc& sd2 = L.segs[i]->d;
-          fs.term_kind[fs.n_terms] = sd2.kind;
-          fs.term_seg[fs.n_terms] = i;
-          fs.term_nm[fs.n_terms] = sd2.nm;
-          fs.term_col0[fs.n_terms] = sd2.col0;
-          fs.term_amp[fs.n_terms] = sd2.amp;
-          ++fs.n_terms;
-        }
-      } else {  // k_grid_dft_mfma's operand: the anchor's (merged) columns of the coefficient buffer
-        fs.term_kind[0] = 1;
-        fs.term_seg[0] = G.anchor[s];
-        fs.term_nm[0] = d.nm;
-        fs.term_col0[0] = d.col0;
-        fs.n_terms = 1;
-      }
-    }
-    f.ring_off = (G.fused_lrow0.back() + G.segs.back()->nf) * kFusedPitch;
-    f.lrows = G.frows.as<int32_t>();
-    f.fq = G.fused_fq;
-    f.psr_c0 = G.psr_c0.as<int32_t>();
-    f.real0 = c->blk_real0;
-    f.k0 = c->blk_k0;
-    f.k1 = c->blk_k1;
-#ifdef FPTA_FUSED_PROF
-    HIPCHK(c, c->dbg_a.ensure(sizeof(unsigned long long) * 8 * 8 * 4096), "fused profile alloc");
-    HIPCHK(c, hipMemsetAsync(c->dbg_a.p, 0, sizeof(unsigned long long) * 8 * 8 * 4096, c->stream), "profile memset");
-    f.prof = c->dbg_a.as<unsigned long long>();
-#endif
-    HIPCHK(c, launch_grid_fused(c->stream, a, band, f, nq, G.fused_lds), "k_grid_fused launch");
-  } else if (psr) {
-    kind = G.vmax <= 16 ? 6 : 7;  // launch_grid_interp_psr: NQ = 4 or 8 band steps
-    HIPCHK(c,
-           launch_grid_interp_psr(c->stream, a, band, gsegs.s[0],
-                                  a.part ? G.psr_pg.as<int32_t>() : G.psr_c0.as<int32_t>(), L.P, R_pad),
-           "k_grid_interp_psr launch");
-  } else if ((c->interp_ws == 3 || ws2_fits) && !c->interp_lds && !a.w_on && !a.accumulate && !a.part) {
-    kind = 2;
-    HIPCHK(c, launch_grid_interp_ws(c->stream, a, band, R_pad, true), "k_grid_interp_ws2 launch");
-  } else if (c->interp_ws && !c->interp_lds && !a.w_on && !a.accumulate && (!a.part || c->interp_ws == 2)) {
-    kind = 1;
-    HIPCHK(c, launch_grid_interp_ws(c->stream, a, band, R_pad), "k_grid_interp_ws launch");
-#ifdef FPTA_DIAG_KERNELS
-  } else if (c->interp_lds && G.lds_ok && !a.w_on) {
-    kind = 3;
-    band.pgfirst = nullptr;
-    band.n_pg = G.n_chunks;
-    GridLds lds{G.groups.as<int4>(), G.urows.as<int32_t>(), G.lrows.as<int32_t>(), G.n_groups, G.lds_rows};
-    HIPCHK(c, launch_grid_interp_lds(c->stream, a, band, lds, R_pad), "k_grid_interp_lds launch");
-#endif
-  } else {
-    kind = 0;
-    HIPCHK(c, launch_grid_interp_mfma(c->stream, a, band, R_pad), "k_grid_interp_mfma launch");
-  }
-  c->last_interp = 1 + kind * 4 + (a.w_on ? 2 : 0) + (a.part ? 1 : 0);
-  if (pipe) {  // buffer gi is free once this interpolation is done; the next block's DFT writes the other one
-    HIPCHK(c, hipEventRecord(c->ev_gfree[gi], c->stream), "event record");
-    c->gfree_set[gi] = true;
-    c->gbuf = gi ^ 1;
-  }
-  if (a.part) {
-    c->part_ready = true;
-    c->part_chunks = band.n_pg;  // partial rows
-    c->part_rpad = R_pad;
-  }
-  return FPTA_OK;
-}
-
 // White noise + ECORR to fuse into the synthesis epilogue (batch path).
 struct WhiteCfg {
   int32_t on = 0;
@@ -2028,7 +761,7 @@ int dense_cholesky(fpta_ctx* c, const DenseDims& d) {
   return FPTA_OK;
 }
 
-}  // namespace
+}  // namespace capi
 
 // =============================================================================================== API
 extern "C" {
@@ -2109,6 +842,21 @@ int fpta_destroy(fpta_ctx* c) {
   return FPTA_OK;
 }
 
+// Option values measured slower than the shipped one exist for same-box A/B runs and the bitwise tests
+// against the shipped kernels: variant builds only (make variant DEFS=-DFPTA_DIAG_KERNELS); the product refuses them.
+static bool variant_value_ok(fpta_ctx* c, bool shipped, const char* what) {
+#ifdef FPTA_DIAG_KERNELS
+  (void)c;
+  (void)shipped;
+  (void)what;
+  return true;
+#else
+  if (shipped) return true;
+  fail(c, FPTA_EINVAL, std::string(what) + ": measured slower, a variant-build option (make variant DEFS=-DFPTA_DIAG_KERNELS)");
+  return false;
+#endif
+}
+
 int fpta_set_option(fpta_ctx* c, int32_t key, int64_t value) {
   if (!c) return fail(nullptr, FPTA_EINVAL, "set_option: null ctx");
   switch (key) {
@@ -2150,13 +898,17 @@ int fpta_set_option(fpta_ctx* c, int32_t key, int64_t value) {
       c->interp_lds = value ? 1 : 0;
       return FPTA_OK;
     case FPTA_OPT_DFT_GEN:
+      if (!variant_value_ok(c, value == 1, "dft_gen 0 (the draws through the coefficient buffer, +8 % on C2)"))
+        return FPTA_EINVAL;
       c->dft_gen = value ? 1 : 0;
       return FPTA_OK;
     case FPTA_OPT_GEN_MIX:
       if (value < 0 || value > 3) return fail(c, FPTA_EINVAL, "gen_mix must be 0 .. 3");
+      if (!variant_value_ok(c, value == 2, "gen_mix 0 / 1 / 3 (equal or slower than 2)")) return FPTA_EINVAL;
       c->gen_mix = (int)value;
       return FPTA_OK;
     case FPTA_OPT_ASYNC_SUMS:
+      if (!variant_value_ok(c, value == 0, "async_sums 1 (slower on C3)")) return FPTA_EINVAL;
       c->async_sums = value ? 1 : 0;
       return FPTA_OK;
     case FPTA_OPT_PART_GROUP:
@@ -2185,10 +937,12 @@ int fpta_set_option(fpta_ctx* c, int32_t key, int64_t value) {
       if (value > 3)
         return fail(c, FPTA_EINVAL, "interp_ws 4 / 5: k_grid_interp_st / _u are diagnostic kernels, not in this build");
 #endif
+      if (!variant_value_ok(c, value == 1 || value > 3, "interp_ws 0 / 2 / 3 (slower on C2 / C3)")) return FPTA_EINVAL;
       c->interp_ws = (int)value;
       return FPTA_OK;
     case FPTA_OPT_SIDE_SPLIT:
       if (value < 0 || value > 2) return fail(c, FPTA_EINVAL, "side_split must be 0 .. 2");
+      if (!variant_value_ok(c, value == 2, "side_split 0 / 1 (slower on C2 / C5)")) return FPTA_EINVAL;
       c->side_split = (int)value;
       return FPTA_OK;
     case FPTA_OPT_VALU_VARIANT:
@@ -2552,7 +1306,10 @@ int fpta_batch_set_white(fpta_ctx* c, const double* sigma, int64_t n_blocks, con
   return FPTA_OK;
 }
 
-static int batch_common(fpta_ctx* c, uint64_t seed, int64_t real0, int32_t n_real, const double* zin,
+}  // extern "C"
+namespace __attribute__((visibility("hidden"))) capi {  // library-internal: not exported
+
+int batch_common(fpta_ctx* c, uint64_t seed, int64_t real0, int32_t n_real, const double* zin,
                         int32_t zin_nm, double* out, double* coeffs_out, bool white) {
   double* const coeffs_host = coeffs_out;
   if (!c) return fail(nullptr, FPTA_EINVAL, "null ctx");
@@ -2640,6 +1397,9 @@ static int batch_common(fpta_ctx* c, uint64_t seed, int64_t real0, int32_t n_rea
   return FPTA_OK;
 }
 
+}  // namespace capi
+extern "C" {
+
 int fpta_batch_synth(fpta_ctx* c, uint64_t seed, int64_t real0, int32_t n_real, double* out, double* coeffs_out) {
   return batch_common(c, seed, real0, n_real, nullptr, 0, out, coeffs_out, true);
 }
@@ -2680,13 +1440,15 @@ int fpta_batch_device_out(fpta_ctx* c, double** dptr, int64_t* ld, int32_t* n_re
   return FPTA_OK;
 }
 
+}  // extern "C"
+namespace __attribute__((visibility("hidden"))) capi {  // library-internal: not exported
+
 // Per-realization {sum, sum of squares} of the context's last block into c->sums (device): from the interpolation's
 // partial checksums when it wrote them for this block, else one pass over the block. On the ctx stream, or (async,
 // streamed jobs with partials) on the red stream beside the next block's work; *used: the stream the sums are on.
 // With dst (device or pinned host memory), sums from the partials are written there directly (*direct = true)
 // instead of into c->sums.
-static int launch_block_checksums(fpta_ctx* c, bool async = false, hipStream_t* used = nullptr, double* dst = nullptr,
-                                  bool* direct = nullptr) {
+int launch_block_checksums(fpta_ctx* c, bool async, hipStream_t* used, double* dst, bool* direct) {
   if (direct) *direct = false;
   hipStream_t st = c->stream;
   if (async && c->part_ready) {
@@ -2728,6 +1490,9 @@ static int launch_block_checksums(fpta_ctx* c, bool async = false, hipStream_t* 
   }
   return FPTA_OK;
 }
+
+}  // namespace capi
+extern "C" {
 
 int fpta_batch_checksums(fpta_ctx* c, double* sums) {
   if (!c || !sums) return fail(c, FPTA_EINVAL, "checksums: bad arguments");
@@ -2864,429 +1629,5 @@ int fpta_debug_normals(fpta_ctx* c, int64_t n, const uint32_t* words, double* ou
   return FPTA_OK;
 }
 
-
-// ------------------------------------------------------------------------------------ multi-device
-// One process driving several devices (SURVEY.md §8(b) fpta_multi_*, §8(e)): one context per listed
-// device, the layout replicated on each, realizations sharded contiguously (device g of G owns
-// [real0 + g n / G, real0 + (g + 1) n / G)) and streamed in batches. Only per-realization checksums
-// leave the devices (async D2H into pinned host memory); the residual blocks stay resident. The work
-// of all devices is issued round-robin from this thread on their own streams, so the devices run
-// concurrently. Output is invariant to the device count and the batch size (Philox counters carry the
-// global realization index). Processes that own one GPU each use fakepta_amd.batch.simulate_sharded
-// (torch.distributed / RCCL) instead.
-struct fpta_multi {
-  std::vector<fpta_ctx*> ctx;
-  std::string err;
-  // checksum gather (fpta_multi_set_gather): FPTA_GATHER_AUTO = RCCL when the devices are distinct, else pinned host
-  // staging; FPTA_GATHER_RCCL; FPTA_GATHER_HOST. comm: one RCCL communicator per device (ncclCommInitAll, made on
-  // the first RCCL gather); shard: each device's checksums of its shard, gathered to device 0's root buffer
-  int gather = FPTA_GATHER_AUTO;
-  int last_gather = 0;
-  std::vector<ncclComm_t> comm;
-  std::vector<DevBuf*> shard;
-  DevBuf root;
-  ~fpta_multi() {
-    for (size_t g = 0; g < comm.size(); ++g)
-      if (comm[g]) (void)ncclCommDestroy(comm[g]);
-    for (size_t g = 0; g < shard.size(); ++g) {
-      if (g < ctx.size() && ctx[g]) (void)hipSetDevice(ctx[g]->device);
-      delete shard[g];
-    }
-    if (!ctx.empty() && ctx[0]) (void)hipSetDevice(ctx[0]->device);
-    root.release();
-  }
-};
-
-// One process per GPU (fakepta_amd.batch.RcclComm): an RCCL communicator on a context's device and stream.
-struct fpta_comm {
-  ncclComm_t comm = nullptr;
-  fpta_ctx* ctx = nullptr;
-  int32_t nranks = 0, rank = 0;
-  DevBuf send, recv;
-  std::string err;
-};
-
-namespace {
-int multi_fail(fpta_multi* m, int i, int rc) {
-  if (m) m->err = "device context " + std::to_string(i) + ": " + fpta_last_error(m->ctx[i]);
-  g_err = m ? m->err : g_err;
-  return rc;
-}
-
-// checksums of the context's last block -> dst [n_real][2] (pinned host, or device with d2d), asynchronously: on the
-// red stream beside the next block when the interpolation wrote partials, else on the ctx stream.
-int checksums_async(fpta_ctx* c, double* dst, bool d2d = false) {
-  hipStream_t st = nullptr;
-  bool direct = false;
-  int rc = launch_block_checksums(c, c->async_sums != 0, &st, dst, &direct);
-  if (rc) return rc;
-  if (direct) return FPTA_OK;  // the reduction wrote dst
-  HIPCHK(c,
-         hipMemcpyAsync(dst, c->sums.p, sizeof(double) * 2 * c->out_R,
-                        d2d ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, st),
-         "sums copy");
-  return FPTA_OK;
-}
-}  // namespace
-
-int fpta_multi_create(int32_t n_dev, const int32_t* devices, fpta_multi** out) {
-  if (!out || n_dev <= 0 || !devices) return fail(nullptr, FPTA_EINVAL, "multi_create: bad arguments");
-  *out = nullptr;
-  fpta_multi* m = new fpta_multi();
-  for (int32_t i = 0; i < n_dev; ++i) {
-    fpta_ctx* c = nullptr;
-    int rc = fpta_create(devices[i], &c);
-    if (rc) {
-      std::string msg = "multi_create: device " + std::to_string(devices[i]) + ": " + g_err;
-      fpta_multi_destroy(m);
-      return fail(nullptr, rc, msg);
-    }
-    m->ctx.push_back(c);
-  }
-  *out = m;
-  return FPTA_OK;
-}
-
-int fpta_multi_destroy(fpta_multi* m) {
-  if (!m) return FPTA_OK;
-  std::vector<fpta_ctx*> ctx = m->ctx;
-  delete m;  // communicators and device buffers first, then the contexts they were made on
-  for (fpta_ctx* c : ctx) fpta_destroy(c);
-  return FPTA_OK;
-}
-
-const char* fpta_multi_last_error(const fpta_multi* m) { return m ? m->err.c_str() : g_err.c_str(); }
-
-int fpta_multi_size(const fpta_multi* m) { return m ? (int)m->ctx.size() : 0; }
-
-fpta_ctx* fpta_multi_context(fpta_multi* m, int32_t i) {
-  return (m && i >= 0 && i < (int32_t)m->ctx.size()) ? m->ctx[i] : nullptr;
-}
-
-int fpta_multi_set_toas(fpta_multi* m, int32_t n_psr, const int64_t* offs, const double* toas, const double* nu) {
-  if (!m) return fail(nullptr, FPTA_EINVAL, "null multi");
-  for (size_t i = 0; i < m->ctx.size(); ++i) {
-    int rc = fpta_batch_set_toas(m->ctx[i], n_psr, offs, toas, nu);
-    if (rc) return multi_fail(m, (int)i, rc);
-  }
-  return FPTA_OK;
-}
-
-int fpta_multi_add_signal(fpta_multi* m, int32_t kind, int32_t n_modes, const double* f, const double* amp,
-                          double idx, double freqf, const double* Lmat, const uint8_t* mask) {
-  if (!m) return fail(nullptr, FPTA_EINVAL, "null multi");
-  int id = -1;
-  for (size_t i = 0; i < m->ctx.size(); ++i) {
-    int rc = fpta_batch_add_signal(m->ctx[i], kind, n_modes, f, amp, idx, freqf, Lmat, mask);
-    if (rc < 0) return multi_fail(m, (int)i, rc);
-    id = rc;
-  }
-  return id;
-}
-
-int fpta_multi_set_white(fpta_multi* m, const double* sigma, int64_t n_blocks, const int64_t* block_offs,
-                         const int64_t* block_idx, const double* ecorr_sigma) {
-  if (!m) return fail(nullptr, FPTA_EINVAL, "null multi");
-  for (size_t i = 0; i < m->ctx.size(); ++i) {
-    int rc = fpta_batch_set_white(m->ctx[i], sigma, n_blocks, block_offs, block_idx, ecorr_sigma);
-    if (rc) return multi_fail(m, (int)i, rc);
-  }
-  return FPTA_OK;
-}
-
-int fpta_multi_set_option(fpta_multi* m, int32_t key, int64_t value) {
-  if (!m) return fail(nullptr, FPTA_EINVAL, "null multi");
-  for (size_t i = 0; i < m->ctx.size(); ++i) {
-    int rc = fpta_set_option(m->ctx[i], key, value);
-    if (rc) return multi_fail(m, (int)i, rc);
-  }
-  return FPTA_OK;
-}
-
-int fpta_multi_set_gather(fpta_multi* m, int32_t mode) {
-  if (!m) return fail(nullptr, FPTA_EINVAL, "null multi");
-  if (mode < FPTA_GATHER_AUTO || mode > FPTA_GATHER_HOST) {
-    m->err = "multi_set_gather: mode must be FPTA_GATHER_AUTO, _RCCL or _HOST";
-    return fail(nullptr, FPTA_EINVAL, m->err);
-  }
-  m->gather = mode;
-  return FPTA_OK;
-}
-
-int fpta_multi_last_gather(const fpta_multi* m) { return m ? m->last_gather : 0; }
-
-namespace {
-int rccl_fail(std::string* err, ncclResult_t r, const char* what) {
-  std::string msg = std::string(what) + ": " + ncclGetErrorString(r);
-  if (err) *err = msg;
-  return fail(nullptr, FPTA_EDEVICE, msg);
-}
-
-// ncclCommInitAll over m's devices (once)
-int multi_rccl_init(fpta_multi* m) {
-  if (!m->comm.empty()) return FPTA_OK;
-  const int G = (int)m->ctx.size();
-  std::vector<int> devs(G);
-  for (int g = 0; g < G; ++g) devs[g] = m->ctx[g]->device;
-  std::vector<ncclComm_t> comm(G, nullptr);
-  ncclResult_t r = ncclCommInitAll(comm.data(), G, devs.data());
-  if (r != ncclSuccess) return rccl_fail(&m->err, r, "multi_synth: ncclCommInitAll");
-  m->comm = comm;
-  return FPTA_OK;
-}
-}  // namespace
-
-// Realizations real0 .. real0 + n_real - 1 split over m's contexts (context g: [g n / G, (g + 1) n / G)),
-// streamed in batches of <= `batch` round-robin over the devices. Per-realization checksums (from the gridded
-// interpolation's partial sums where it runs) either stay on each device and are gathered to device 0 by one
-// ncclGather over xGMI at the end (RCCL mode), or are copied asynchronously into pinned host staging (host mode);
-// one sync per device at the end either way: no host round trip between batches.
-static int stream_checksums(fpta_multi* m, uint64_t seed, int64_t real0, int64_t n_real, int32_t batch,
-                            double* checksums_out) {
-  const int64_t G = (int64_t)m->ctx.size();
-  std::vector<int64_t> beg(G + 1);
-  for (int64_t g = 0; g <= G; ++g) beg[g] = g * n_real / G;
-  int64_t n_max = 0;
-  for (int64_t g = 0; g < G; ++g) n_max = std::max(n_max, beg[g + 1] - beg[g]);
-  bool distinct = true;
-  for (int64_t g = 0; g < G; ++g)
-    for (int64_t h = 0; h < g; ++h) distinct = distinct && m->ctx[g]->device != m->ctx[h]->device;
-  const bool use_rccl = m->gather == FPTA_GATHER_RCCL || (m->gather == FPTA_GATHER_AUTO && distinct);
-  if (use_rccl && !distinct) {
-    m->err = "multi_synth: the RCCL gather needs distinct devices (one communicator rank per device)";
-    return fail(nullptr, FPTA_EINVAL, m->err);
-  }
-  if (use_rccl && n_max > ((int64_t)1 << 40) / (2 * G)) {
-    m->err = "multi_synth: job too large for one gather";
-    return fail(nullptr, FPTA_EINVAL, m->err);
-  }
-  int rc = use_rccl ? multi_rccl_init(m) : FPTA_OK;
-  if (rc) return rc;
-  m->last_gather = use_rccl ? FPTA_GATHER_RCCL : FPTA_GATHER_HOST;
-  // RCCL: each device's shard of checksums [n_max][2] on the device, the gather target [G][n_max][2] on device 0,
-  // and one pinned buffer for the root's download. Host: pinned staging for each device's shard
-  std::vector<double*> stage(G, nullptr);
-  double* root_host = nullptr;
-  if (use_rccl) {
-    while (m->shard.size() < (size_t)G) m->shard.push_back(new DevBuf());
-    for (int64_t g = 0; g < G && !rc; ++g) {
-      fpta_ctx* c = m->ctx[g];
-      hipError_t e = hipSetDevice(c->device);
-      if (e == hipSuccess) e = m->shard[g]->ensure(sizeof(double) * 2 * (size_t)n_max);
-      if (e == hipSuccess && g == 0) e = m->root.ensure(sizeof(double) * 2 * (size_t)n_max * G);
-      if (e == hipSuccess && g == 0)
-        e = hipHostMalloc((void**)&root_host, sizeof(double) * 2 * (size_t)n_max * G, hipHostMallocDefault);
-      if (e != hipSuccess) rc = multi_fail(m, (int)g, hip_fail(c, e, "multi_synth gather buffers"));
-    }
-  } else {
-    for (int64_t g = 0; g < G && !rc; ++g) {
-      const int64_t n = beg[g + 1] - beg[g];
-      if (n == 0) continue;
-      fpta_ctx* c = m->ctx[g];
-      hipError_t e = hipSetDevice(c->device);
-      // coherent: the partial-checksum reduction writes its sums here directly from the device (checksums_async)
-      if (e == hipSuccess) e = hipHostMalloc((void**)&stage[g], sizeof(double) * 2 * n, hipHostMallocCoherent);
-      if (e != hipSuccess) rc = multi_fail(m, (int)g, hip_fail(c, e, "multi_synth staging"));
-    }
-  }
-  // a checksums-only job: the gridded interpolation writes partial checksums (no second pass over each block).
-  // The path is chosen once for the job, not per batch: a tail batch below FPTA_OPT_MFMA_MIN_REAL would otherwise
-  // take the direct path and its realizations (and checksums) would depend on the batch split and device count
-  std::vector<int> fuse(G), min_real(G);
-  for (int64_t g = 0; g < G; ++g) {
-    fuse[g] = m->ctx[g]->fuse_sums;
-    m->ctx[g]->fuse_sums = 1;
-    min_real[g] = m->ctx[g]->mfma_min_real;
-    m->ctx[g]->mfma_min_real = 1;
-  }
-  // round-robin: batch k of every device, then batch k + 1 (each device's stream orders its own work)
-  for (int64_t k = 0; !rc; ++k) {
-    bool any = false;
-    for (int64_t g = 0; g < G && !rc; ++g) {
-      const int64_t first = beg[g] + k * (int64_t)batch;
-      if (first >= beg[g + 1]) continue;
-      any = true;
-      const int32_t n = (int32_t)std::min<int64_t>(batch, beg[g + 1] - first);
-      fpta_ctx* c = m->ctx[g];
-      if ((rc = batch_common(c, seed, real0 + first, n, nullptr, 0, nullptr, nullptr, true)))
-        rc = multi_fail(m, (int)g, rc);
-      else if (use_rccl) {
-        if ((rc = checksums_async(c, m->shard[g]->as<double>() + 2 * (first - beg[g]), true)))
-          rc = multi_fail(m, (int)g, rc);
-      } else if ((rc = checksums_async(c, stage[g] + 2 * (first - beg[g])))) {
-        rc = multi_fail(m, (int)g, rc);
-      }
-    }
-    if (!any) break;
-  }
-  for (int64_t g = 0; g < G && !rc; ++g) {  // the reductions and copies on each device's red stream come first
-    fpta_ctx* c = m->ctx[g];
-    (void)hipSetDevice(c->device);
-    if ((rc = join_red(c))) rc = multi_fail(m, (int)g, rc);
-  }
-  if (use_rccl && !rc) {
-    // every device's shard to device 0 in one collective (pad rows beyond a shard's count are dropped below)
-    ncclResult_t r = ncclGroupStart();
-    for (int64_t g = 0; g < G && r == ncclSuccess; ++g) {
-      (void)hipSetDevice(m->ctx[g]->device);
-      r = ncclGather(m->shard[g]->p, g == 0 ? m->root.p : nullptr, 2 * (size_t)n_max, ncclFloat64, 0, m->comm[g],
-                     m->ctx[g]->stream);
-    }
-    const ncclResult_t r2 = ncclGroupEnd();
-    if (r == ncclSuccess) r = r2;
-    if (r != ncclSuccess) {
-      rccl_fail(&m->err, r, "multi_synth: ncclGather");
-      rc = FPTA_EDEVICE;
-    } else {
-      fpta_ctx* c0 = m->ctx[0];
-      (void)hipSetDevice(c0->device);
-      hipError_t e = hipMemcpyAsync(root_host, m->root.p, sizeof(double) * 2 * (size_t)n_max * G,
-                                    hipMemcpyDeviceToHost, c0->stream);
-      if (e != hipSuccess) rc = multi_fail(m, 0, hip_fail(c0, e, "multi_synth root download"));
-    }
-  }
-  for (int64_t g = 0; g < G; ++g) {
-    if (!use_rccl && !stage[g]) continue;
-    fpta_ctx* c = m->ctx[g];
-    (void)hipSetDevice(c->device);
-    hipError_t e = hipStreamSynchronize(c->stream);
-    if (!rc && e != hipSuccess) rc = multi_fail(m, (int)g, hip_fail(c, e, "multi_synth sync"));
-    if (!use_rccl) {
-      if (!rc) std::memcpy(checksums_out + 2 * beg[g], stage[g], sizeof(double) * 2 * (beg[g + 1] - beg[g]));
-      (void)hipHostFree(stage[g]);
-    }
-  }
-  if (use_rccl) {
-    if (!rc)
-      for (int64_t g = 0; g < G; ++g)
-        std::memcpy(checksums_out + 2 * beg[g], root_host + 2 * (size_t)n_max * g,
-                    sizeof(double) * 2 * (beg[g + 1] - beg[g]));
-    if (root_host) {
-      (void)hipSetDevice(m->ctx[0]->device);
-      (void)hipHostFree(root_host);
-    }
-  }
-  for (int64_t g = 0; g < G; ++g) {
-    m->ctx[g]->fuse_sums = fuse[g];
-    m->ctx[g]->mfma_min_real = min_real[g];
-  }
-  return rc;
-}
-
-int fpta_multi_synth(fpta_multi* m, uint64_t seed, int64_t real0, int64_t n_real, int32_t batch,
-                     double* checksums_out) {
-  if (!m) return fail(nullptr, FPTA_EINVAL, "null multi");
-  if (n_real <= 0 || real0 < 0 || batch <= 0 || !checksums_out) {
-    m->err = "multi_synth: bad arguments";
-    return fail(nullptr, FPTA_EINVAL, m->err);
-  }
-  if (real0 + n_real > ((int64_t)1 << 32)) {
-    m->err = "multi_synth: realization index exceeds the 32-bit Philox counter word";
-    return fail(nullptr, FPTA_EINVAL, m->err);
-  }
-  return stream_checksums(m, seed, real0, n_real, batch, checksums_out);
-}
-
-// ----------------------------------------------------------------------------- one process per GPU: RCCL
-int fpta_comm_unique_id(void* id) {
-  if (!id) return fail(nullptr, FPTA_EINVAL, "comm_unique_id: null buffer");
-  ncclUniqueId u;
-  ncclResult_t r = ncclGetUniqueId(&u);
-  if (r != ncclSuccess) return rccl_fail(nullptr, r, "ncclGetUniqueId");
-  std::memcpy(id, u.internal, FPTA_COMM_ID_BYTES);
-  return FPTA_OK;
-}
-
-int fpta_comm_init_rank(fpta_ctx* c, int32_t nranks, int32_t rank, const void* id, fpta_comm** out) {
-  if (!c || !id || !out || nranks <= 0 || rank < 0 || rank >= nranks)
-    return fail(c, FPTA_EINVAL, "comm_init_rank: bad arguments");
-  *out = nullptr;
-  HIPCHK(c, hipSetDevice(c->device), "hipSetDevice");
-  ncclUniqueId u;
-  std::memcpy(u.internal, id, FPTA_COMM_ID_BYTES);
-  ncclComm_t comm = nullptr;
-  ncclResult_t r = ncclCommInitRank(&comm, nranks, u, rank);
-  if (r != ncclSuccess) {
-    rccl_fail(&c->err, r, "ncclCommInitRank");
-    return FPTA_EDEVICE;
-  }
-  fpta_comm* m = new fpta_comm();
-  m->comm = comm;
-  m->ctx = c;
-  m->nranks = nranks;
-  m->rank = rank;
-  *out = m;
-  return FPTA_OK;
-}
-
-int fpta_comm_destroy(fpta_comm* m) {
-  if (!m) return FPTA_OK;
-  (void)hipSetDevice(m->ctx->device);
-  if (m->comm) (void)ncclCommDestroy(m->comm);
-  delete m;
-  return FPTA_OK;
-}
-
-const char* fpta_comm_last_error(const fpta_comm* m) { return m ? m->err.c_str() : g_err.c_str(); }
-
-int fpta_comm_size(const fpta_comm* m, int32_t* nranks, int32_t* rank) {
-  if (!m) return fail(nullptr, FPTA_EINVAL, "null comm");
-  if (nranks) *nranks = m->nranks;
-  if (rank) *rank = m->rank;
-  return FPTA_OK;
-}
-
-// max over ranks of *value (host), on the context's stream after all its queued work: also the job barrier
-int fpta_comm_max(fpta_comm* m, double* value) {
-  if (!m || !value) return fail(nullptr, FPTA_EINVAL, "comm_max: bad arguments");
-  fpta_ctx* c = m->ctx;
-  HIPCHK(c, hipSetDevice(c->device), "hipSetDevice");
-  HIPCHK(c, m->send.ensure(sizeof(double)), "comm_max buffer");
-  HIPCHK(c, hipMemcpyAsync(m->send.p, value, sizeof(double), hipMemcpyHostToDevice, c->stream), "comm_max upload");
-  ncclResult_t r = ncclAllReduce(m->send.p, m->send.p, 1, ncclFloat64, ncclMax, m->comm, c->stream);
-  if (r != ncclSuccess) return rccl_fail(&m->err, r, "ncclAllReduce");
-  HIPCHK(c, hipMemcpyAsync(value, m->send.p, sizeof(double), hipMemcpyDeviceToHost, c->stream), "comm_max download");
-  HIPCHK(c, hipStreamSynchronize(c->stream), "comm_max sync");
-  return FPTA_OK;
-}
-
-// every rank sends `count` doubles (host); rank 0 receives nranks * count in rank order into recv (host; ignored
-// on the other ranks)
-int fpta_comm_gather(fpta_comm* m, const double* send, int64_t count, double* recv) {
-  if (!m || count < 0 || (count && !send) || (m->rank == 0 && count && !recv))
-    return fail(nullptr, FPTA_EINVAL, "comm_gather: bad arguments");
-  fpta_ctx* c = m->ctx;
-  HIPCHK(c, hipSetDevice(c->device), "hipSetDevice");
-  const size_t bytes = sizeof(double) * (size_t)std::max<int64_t>(count, 1);
-  HIPCHK(c, m->send.ensure(bytes), "comm_gather buffer");
-  if (m->rank == 0) HIPCHK(c, m->recv.ensure(bytes * m->nranks), "comm_gather buffer");
-  if (count)
-    HIPCHK(c, hipMemcpyAsync(m->send.p, send, sizeof(double) * count, hipMemcpyHostToDevice, c->stream),
-           "comm_gather upload");
-  ncclResult_t r = ncclGather(m->send.p, m->rank == 0 ? m->recv.p : nullptr, (size_t)count, ncclFloat64, 0, m->comm,
-                              c->stream);
-  if (r != ncclSuccess) return rccl_fail(&m->err, r, "ncclGather");
-  if (m->rank == 0 && count)
-    HIPCHK(c,
-           hipMemcpyAsync(recv, m->recv.p, sizeof(double) * count * m->nranks, hipMemcpyDeviceToHost, c->stream),
-           "comm_gather download");
-  HIPCHK(c, hipStreamSynchronize(c->stream), "comm_gather sync");
-  return FPTA_OK;
-}
-
-int fpta_batch_synth_checksums(fpta_ctx* c, uint64_t seed, int64_t real0, int64_t n_real, int32_t batch,
-                               double* sums) {
-  if (!c) return fail(nullptr, FPTA_EINVAL, "null ctx");
-  if (n_real <= 0 || real0 < 0 || batch <= 0 || !sums)
-    return fail(c, FPTA_EINVAL, "batch_synth_checksums: bad arguments");
-  if (real0 + n_real > ((int64_t)1 << 32))
-    return fail(c, FPTA_EINVAL, "batch_synth_checksums: realization index exceeds the 32-bit Philox counter word");
-  fpta_multi one;
-  one.ctx.push_back(c);
-  one.gather = FPTA_GATHER_HOST;  // one device: nothing to gather
-  const int rc = stream_checksums(&one, seed, real0, n_real, batch, sums);  // a failing step set c's last error
-  one.ctx.clear();  // the context is the caller's
-  return rc;
-}
 
 }  // extern "C"

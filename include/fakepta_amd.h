@@ -323,27 +323,31 @@ int fpta_comm_gather(fpta_comm* comm, const double* send, int64_t count, double*
                                      register-pipelined k_grid_interp_mfma; 4 k_grid_interp_st for every block
                                      (compute waves hand their sums to storer waves through LDS; the storers add
                                      white noise / ECORR, store and reduce partial checksums). Results are
-                                     identical. */
+                                     identical. Variant builds only (FPTA_BUILD_DIAG): 0, 2, 3 (measured slower)
+                                     and 4; the product library refuses them. */
 #define FPTA_OPT_SIDE_SPLIT 16    /* pipelined gridded blocks (FPTA_OPT_OVERLAP): 1 the grid signal with the
                                      largest DFT, when it has no common (ORF-mixed) member, is drawn and
                                      transformed on a second side stream, beside the other signals' draws, mixing
                                      and DFT; 2 (default) the same, its DFT started after the common signals'
                                      draws + mixing queued on the first side stream (they get the room beside the
                                      previous block's interpolation first: C2 -1.3 %, C5 -1.4 %); 0 one side
-                                     stream for all. Results are identical. */
+                                     stream for all. Results are identical. 0 and 1 (measured slower): variant
+                                     builds only (FPTA_BUILD_DIAG); the product library refuses them. */
 #define FPTA_OPT_DFT_GEN 17       /* gridded path: 1 (default) a grid signal with a per-pulsar member draws its
                                      coefficients inside its DFT kernel (k_grid_dft_gen: Philox + Box-Muller into
                                      LDS, same counters and draws as k_gen); 0 k_gen writes them to the coefficient
-                                     buffer and k_grid_dft_mfma reads them back. Same draws; sums agree to rounding. */
+                                     buffer and k_grid_dft_mfma reads them back. Same draws; sums agree to rounding.
+                                     0 (measured slower): variant builds only (FPTA_BUILD_DIAG). */
 #define FPTA_OPT_GEN_MIX 18       /* common signals of 64..256 pulsars (fp64 MFMA mixing): 2 (default) draws and ORF
                                      mixing in one kernel (k_gen_mix: normals in LDS, no zbuf round trip), one wave per
                                      16 realizations, 32 realizations per workgroup; 3 the same with 16 realizations
                                      per workgroup (a quarter of the LDS);
                                      1 waves of 32 realizations; 0 k_gen then k_mix_mfma. Same draws and products;
-                                     results identical. */
+                                     results identical. 0, 1, 3 (equal or slower): variant builds only. */
 #define FPTA_OPT_ASYNC_SUMS 19    /* streamed jobs (fpta_batch_synth_checksums, fpta_multi_synth): 1 a block's partial
                                      checksums are reduced on a stream of their own, beside the next block, into one
-                                     of two partials buffers; 0 (default) on the context stream. Identical results. */
+                                     of two partials buffers; 0 (default) on the context stream. Identical results.
+                                     1 (measured slower): variant builds only (FPTA_BUILD_DIAG). */
 #define FPTA_OPT_PART_GROUP 20    /* fused partial checksums (FPTA_OPT_FUSE_CHECKSUMS): the interpolation sums the partials
                                      of this many consecutive chunks (1 .. 16, default 16) in registers, in chunk order,
                                      and writes one {sum, sum of squares} row per group; the reduction then sums the
@@ -361,12 +365,12 @@ int fpta_comm_gather(fpta_comm* comm, const double* send, int64_t count, double*
                                      only the rows the previous chunk did not hold are loaded; measured slower); 0
                                      (default) the other kernels. Results are identical. */
 #define FPTA_OPT_INTERP_FUSED 23  /* gridded plain blocks (no white epilogue, no fused checksums) whose grids for 32
-                                     realizations fit in LDS with at most 8 DFT jobs of 32 quarter-range rows and
-                                     4 grid signals (C2: 129 KB): 1 (default) k_grid_fused (a workgroup draws one
-                                     pulsar's coefficients for 32 realizations, runs every grid signal's DFT into LDS
-                                     and interpolates the pulsar's chunks from it: no grid buffer, no DFT launch;
-                                     pipelined blocks alternate two coefficient buffers); 0 the DFT + interpolation
-                                     kernels. Results are identical. A layout k_grid_interp_psr serves keeps it. */
+                                     realizations fit in LDS beside the draw ring with at most 4 DFT jobs of 32
+                                     quarter-range rows and 2 grid signals (C2: 129 KB of grids): 1 (default)
+                                     k_grid_fused (persistent workgroups, one per CU: 4 DFT waves draw and transform
+                                     the next pulsar x 32 realizations into LDS while 4 interpolation waves read the
+                                     current one: no grid buffer, no DFT launch); 0 the DFT + interpolation kernels.
+                                     Results are identical. A layout k_grid_interp_psr serves keeps it. */
 int fpta_set_option(fpta_ctx* ctx, int32_t key, int64_t value);
 /* Current value of option `key` (same keys as fpta_set_option). */
 int fpta_get_option(fpta_ctx* ctx, int32_t key, int64_t* value);

@@ -4,6 +4,21 @@ import numpy as np
 from oracle import fakepta_oracle as O
 
 
+def variant_build(capi):
+    """The loaded library is a variant build (make variant DEFS=-DFPTA_DIAG_KERNELS): it holds the diagnostic kernels
+    and accepts the option values measured slower than the shipped ones, which the product library refuses."""
+    return bool(capi.build_flags() & capi.BUILD_DIAG)
+
+
+def assert_variant_refused(ctx, capi, key, value):
+    """The product library refuses a variant-only option value and keeps the old one."""
+    import pytest
+    old = ctx.get_option(key)
+    with pytest.raises(capi.FptaError, match="variant"):
+        ctx.set_option(key, value)
+    assert ctx.get_option(key) == old
+
+
 def oracle_segments(sim):
     """BatchSimulator.segments -> oracle Segment list (same layout and semantics)."""
     return [O.Segment(s["kind"], (2.0 * np.pi) * s["f"], s["amp"], idx=s["idx"], freqf=s["freqf"], L=s["L"],

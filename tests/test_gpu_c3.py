@@ -142,7 +142,11 @@ def test_async_partial_reductions_are_bitwise_identical(c3):
     """FPTA_OPT_ASYNC_SUMS: reducing each block's partial checksums on a stream of their own (two partials buffers,
     beside the next block) returns the same checksums as on the context stream, in-library and two-context driver."""
     from fakepta_amd import _capi
+    from tests.helpers import assert_variant_refused, variant_build
     psrs, sim, ctx = c3
+    if not variant_build(_capi):  # measured slower: a variant-build option
+        assert_variant_refused(ctx, _capi, _capi.OPT_ASYNC_SUMS, 1)
+        return
     try:
         res = {}
         for asy in (0, 1):

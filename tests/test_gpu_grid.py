@@ -16,7 +16,8 @@ import pytest
 
 from oracle import fakepta_oracle as O
 from tests.conftest import assert_parity, rel_err
-from tests.helpers import common_signal, oracle_segments, per_psr_signal, random_layout
+from tests.helpers import (assert_variant_refused, common_signal, oracle_segments, per_psr_signal, random_layout,
+                           variant_build)
 
 pytestmark = pytest.mark.gpu
 
@@ -60,11 +61,14 @@ def shipped(ctx, capi):
     return opts
 
 
-@pytest.fixture(params=[(1, 1), (1, 0), (0, 0)], ids=["dft_gen", "dft_mfma", "dft_valu"])
+@pytest.fixture(params=[(1, 1), (1, 0), (0, 1)], ids=["dft_gen", "dft_mfma", "dft_valu"])
 def gridded(ctx, capi, shipped, request):
     """Gridded path with the DFT drawing its per-pulsar coefficients itself (k_grid_dft_gen, the default), or reading
-    them from the coefficient buffer on fp64 MFMA or VALU (FPTA_OPT_DFT_GEN 0, FPTA_OPT_GRID_MFMA bit 0); the
-    interpolation is on MFMA in every case. The context's options are restored to the shipped snapshot afterwards."""
+    them from the coefficient buffer on fp64 MFMA (FPTA_OPT_DFT_GEN 0: a variant-build option) or VALU
+    (FPTA_OPT_GRID_MFMA bit 0, which draws through the buffer whatever DFT_GEN); the interpolation is on MFMA in every
+    case. The context's options are restored to the shipped snapshot afterwards."""
+    if request.param[1] == 0 and not variant_build(capi):
+        pytest.skip("FPTA_OPT_DFT_GEN 0 is a variant-build option")
     ctx.set_option(capi.OPT_SYNTH_PATH, 4)
     ctx.set_option(capi.OPT_GRID_MFMA, request.param[0])
     ctx.set_option(capi.OPT_DFT_GEN, request.param[1])
@@ -413,13 +417,13 @@ def test_pipelined_batches_are_bitwise_identical(ctx, capi, shipped, fuse, layou
         ctx.set_option(capi.OPT_SYNTH_PATH, 4)
         ctx.set_option(capi.OPT_FUSE_CHECKSUMS, fuse)
         res = {}
-        for ov, split in ((0, 1), (1, 1), (1, 0), (1, 2)):
+        runs = ((0, 2), (1, 1), (1, 0), (1, 2)) if variant_build(capi) else ((0, 2), (1, 2))  # SIDE_SPLIT 0 / 1: variant
+        for ov, split in runs:
             ctx.set_option(capi.OPT_OVERLAP, ov)
             ctx.set_option(capi.OPT_SIDE_SPLIT, split)
             res[ov, split] = ctx.batch_synth_checksums(21, 3, 5 * 256 - 17, batch=256)
-        np.testing.assert_array_equal(res[0, 1], res[1, 1])
-        np.testing.assert_array_equal(res[0, 1], res[1, 0])
-        np.testing.assert_array_equal(res[0, 1], res[1, 2])
+        for k in runs[1:]:
+            np.testing.assert_array_equal(res[0, 2], res[k])
     finally:
         ctx.set_options(shipped)
 
@@ -440,8 +444,8 @@ def test_pipelined_layout_switches_are_bitwise_identical(ctx, capi, shipped):
             out.append(ctx.batch_synth_checksums(5, 3, 3 * 256 - 5, batch=256))
         return out
     try:
-        ref = run(0, 1)
-        for ov, split in ((1, 1), (1, 0), (1, 2)):
+        ref = run(0, 2)
+        for ov, split in ((1, 1), (1, 0), (1, 2)) if variant_build(capi) else ((1, 2),):
             for a, b in zip(ref, run(ov, split)):
                 np.testing.assert_array_equal(a, b)
     finally:
@@ -456,7 +460,12 @@ def test_warp_specialised_interpolation_is_bitwise_identical(ctx, capi, shipped,
     same MFMA steps and only store) returns the register-pipelined kernel's block and checksums bit for bit, on a
     ragged multi-signal layout with unsorted TOAs, for realization counts that leave compute waves idle (R_pad not a
     multiple of 512), and with the fused partial checksums summed over groups of 1, 3 or 16 chunks
-    (FPTA_OPT_PART_GROUP: 23 pulsars' chunks leave a short last group)."""
+    (FPTA_OPT_PART_GROUP: 23 pulsars' chunks leave a short last group). FPTA_OPT_INTERP_WS 0 / 2 / 3 are variant-build
+    options (measured slower): the product library refuses them."""
+    if not variant_build(capi):
+        for ws in (0, 2, 3):
+            assert_variant_refused(ctx, capi, capi.OPT_INTERP_WS, ws)
+        return
     rng = np.random.default_rng(43)
     offs, toas, nu = random_layout(rng, 23, (31, 260))
     perm = rng.permutation(offs[1] - offs[0])
@@ -494,8 +503,8 @@ def test_partial_realization_blocks_write_every_sample(ctx, capi, shipped, ws, R
     poisoned with NaN first) and the fused partial checksums must match a full pass over the block; the register
     kernel once exited on its first tile's block (dropping later valid tiles) and let later invalid tiles write
     another chunk's partials."""
-    if ws == 4 and not _diag_build(capi):
-        pytest.skip("k_grid_interp_st is a diagnostic kernel (make variant DEFS=-DFPTA_DIAG_KERNELS)")
+    if ws != 1 and not _diag_build(capi):
+        pytest.skip("FPTA_OPT_INTERP_WS 0 / 2 / 3 / 4 are variant-build options (make variant DEFS=-DFPTA_DIAG_KERNELS)")
     rng = np.random.default_rng(47)
     offs, toas, nu = random_layout(rng, 40, (300, 900))
     ctx.batch_set_toas(offs, toas, nu)
@@ -620,7 +629,8 @@ def test_dft_gen_matches_buffered_draws(ctx, capi, shipped, layout):
     """k_grid_dft_gen (FPTA_OPT_DFT_GEN 1) draws the per-pulsar members' coefficients with k_gen's counters and sums
     a grid signal's terms in the merge order (anchor, then the others; products rounded first): its blocks equal
     the buffered path's (k_gen -> coefficient buffer -> k_coef_merge / mix epilogue -> k_grid_dft_mfma) bit for
-    bit, pipelined or not, over realization counts off every tile multiple; and they match the oracle."""
+    bit, pipelined or not, over realization counts off every tile multiple; and they match the oracle. The buffered
+    path (FPTA_OPT_DFT_GEN 0) is a variant-build option: the product library runs the oracle half only."""
     rng = np.random.default_rng(zlib_crc(layout))
     if layout in ("coalesced", "masked"):
         offs, toas, nu, segs = _shared_span_layout(ctx, rng, nu_const=False, with_masked=layout == "masked")
@@ -632,13 +642,13 @@ def test_dft_gen_matches_buffered_draws(ctx, capi, shipped, layout):
         ctx.set_option(capi.OPT_SYNTH_PATH, 4)
         for R, real0 in ((150, 5), (333, 1000), (16, 7)):
             res = {}
-            for gen in (0, 1):
+            for gen in (0, 1) if variant_build(capi) else (1,):
                 ctx.set_option(capi.OPT_DFT_GEN, gen)
                 for ov in (0, 1):
                     ctx.set_option(capi.OPT_OVERLAP, ov)
                     res[gen, ov] = ctx.batch_synth(13, real0, R)
             for k in res:
-                np.testing.assert_array_equal(res[k], res[0, 0])
+                np.testing.assert_array_equal(res[k], res[1, 0])
             want = O.batch_synth(offs, toas, nu, segs, 13, real0, R)
             assert_parity(res[1, 1], want, TOL)
     finally:
@@ -656,7 +666,10 @@ def test_gen_mix_matches_two_kernels(ctx, capi, shipped, factor):
     kernel: same counters, same products in the same k-step order as k_gen + k_mix_mfma, so blocks are bit-identical
     on the gridded (with and without k_grid_dft_gen) and exact paths, for a triangular (Cholesky) and a dense (SVD)
     ORF factor and the batch path's rank-3 factor of the singular dipole ORF (columns past the third exactly zero:
-    both kernels mix, and k_gen_mix draws, only those three), 70 and 160 pulsars (two and three 64-pulsar tiles)."""
+    both kernels mix, and k_gen_mix draws, only those three), 70 and 160 pulsars (two and three 64-pulsar tiles).
+    GEN_MIX 0 / 1 / 3 and DFT_GEN 0 are variant-build options: the product library runs the shipped kernels against
+    the oracle only."""
+    variant = variant_build(capi)
     from fakepta_amd.batch import batch_factor
     rng = np.random.default_rng({"cholesky": 71, "svd": 72}.get(factor, 73))
     for P in (70, 160):
@@ -673,18 +686,18 @@ def test_gen_mix_matches_two_kernels(ctx, capi, shipped, factor):
         ctx.batch_add_signal(1, fc, ac, L=L)
         segs = [O.Segment(0, 2 * np.pi * f, a, 0.0), O.Segment(1, 2 * np.pi * fc, ac, 0.0, L=L)]
         try:
-            for path, dft_gen in ((4, 1), (4, 0), (3, 0), (2, 0)):
+            for path, dft_gen in ((4, 1), (4, 0), (3, 0), (2, 0)) if variant else ((4, 1), (3, 1), (2, 1)):
                 ctx.set_option(capi.OPT_SYNTH_PATH, path)
                 ctx.set_option(capi.OPT_DFT_GEN, dft_gen)
                 res = {}
                 # 2: k_gen_mix with 16-realization waves (twice the waves per workgroup); 3: and 16-realization
                 # workgroups
-                for gm in (0, 1, 2, 3):
+                for gm in (0, 1, 2, 3) if variant else (2,):
                     ctx.set_option(capi.OPT_GEN_MIX, gm)
                     res[gm] = ctx.batch_synth(17, 40, 300)
-                for gm in (1, 2, 3):
-                    np.testing.assert_array_equal(res[0], res[gm])
-                assert_parity(res[1], O.batch_synth(offs, toas, nu, segs, 17, 40, 300), TOL)
+                for gm in res:
+                    np.testing.assert_array_equal(res[2], res[gm])
+                assert_parity(res[2], O.batch_synth(offs, toas, nu, segs, 17, 40, 300), TOL)
         finally:
             ctx.set_options(shipped)
 
@@ -699,6 +712,8 @@ def test_psr_interpolation_is_bitwise_identical(ctx, capi, shipped, case, fuse, 
     single short chunk in "common_short"), a per-pulsar red noise drawn into the coefficient buffer (FPTA_OPT_DFT_GEN
     0), and 40 modes (nf = 124, the largest one-block grid); partial rows of 1 and 16 chunks; every sample written
     (NaN-poisoned block); the kernel that ran is the per-pulsar one."""
+    if case == "per_psr" and not variant_build(capi):
+        pytest.skip("a per-pulsar signal drawn into the coefficient buffer: FPTA_OPT_DFT_GEN 0, a variant-build option")
     rng = np.random.default_rng(83 + len(case))
     # dense TOAs (bands of <= 32 rows: a 32-TOA chunk spans a few grid cells), ragged counts
     offs, toas, nu = random_layout(rng, 13, (700, 2100))

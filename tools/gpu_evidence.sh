@@ -1,9 +1,9 @@
 #!/bin/bash
-# Round-4 evidence at HEAD in one GPU call: rocprofv3 kernel statistics of the default bench command (C2), HBM traffic
+# Evidence at HEAD in one GPU call: rocprofv3 kernel statistics of the default bench command (C2), HBM traffic
 # (FETCH_SIZE / WRITE_SIZE passes) of the C2 interpolation, per-dispatch PMC of the C2 and C5 kernels (one stream).
-#   bash tools/gpu_r4_evidence.sh <tag>       (outputs under gpurun_out/<tag>_*)
+#   bash tools/gpu_evidence.sh <tag> [traffic kernel]       (outputs under gpurun_out/<tag>_*)
 set -o pipefail
-tag=${1:-R4e}
+tag=${1:-R5e}; kern=${2:-k_grid_fused}
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 o=gpurun_out/$tag
@@ -14,7 +14,7 @@ for p in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 120 rocprofv3 --pmc $p --output-format csv -d ${o}_traffic/pass$i -o run -- python bench.py --steps 5 --warmup 2 --cpu-sample 0 --exact-launches 0 --sub-configs 0 > ${o}_traffic_$p.log 2>&1 || { tail -20 ${o}_traffic_$p.log; exit 1; }
   i=$((i+1))
 done
-python tools/collect_traffic.py ${o}_traffic ${o}_grid_traffic.json 320 200000 1024 k_grid_interp_ws band32c || exit 1
+python tools/collect_traffic.py ${o}_traffic ${o}_grid_traffic.json 320 200000 1024 $kern band32c || exit 1
 P0="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE"
 P1="SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_F64 SQ_LDS_BANK_CONFLICT"
 P2="TCC_HIT_sum TCC_MISS_sum TCP_TCC_READ_REQ_sum TCP_PENDING_STALL_CYCLES_sum TA_TA_BUSY_sum TD_TD_BUSY_sum"

@@ -16,7 +16,7 @@ import os
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
-    ap.add_argument("--match", default="dft,interp,gen_mix,epoch,part,mix")
+    ap.add_argument("--match", default="dft,interp,fused,gen_mix,epoch,part,mix")
     args = ap.parse_args()
     keys = [k for k in args.match.split(",") if k]
     d = collections.defaultdict(lambda: collections.defaultdict(list))
