@@ -215,6 +215,8 @@ struct fpta_ctx {
   // work buffers
   DevBuf coef, zbuf, out, sums, zin, xout, hostz, scratch_out, scratch_z, scratch_zb, scratch_sigma,
       scratch_block_of, scratch_esig, dbg_a, dbg_b;
+  DevBuf fused_q;  // k_grid_fused's item queues: 8 per-XCD tickets + a done counter, zero between launches
+  bool fused_q_ready = false;
   int32_t out_R = 0;
   int64_t out_ld = 0;
   // options

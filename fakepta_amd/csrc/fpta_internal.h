@@ -228,7 +228,9 @@ struct FusedArgs {
   int64_t real0;          // the batch's first realization (Philox counter)
   uint32_t k0, k1;
   unsigned long long* prof;  // -DFPTA_FUSED_PROF builds only: per-wave cycle counters [gridDim][8 waves][8]; else null
+  uint32_t* queue;           // [kFusedQueueWords], zero at launch; the kernel's last workgroup zeroes it again
 };
+constexpr int kFusedQueueWords = 9;  // 8 per-XCD item tickets + the count of finished workgroups
 // nq_max: band steps of the widest chunk (vmax / 4; the kernel holds up to 12 steps' operands and takes a wider chunk's
 // in turns); lds_bytes: grids + ring + sync word
 hipError_t launch_grid_fused(hipStream_t st, const SynthArgs& a, const GridBand& band, const FusedArgs& f,

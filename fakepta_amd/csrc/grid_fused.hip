@@ -66,19 +66,25 @@ struct Prof {
 __device__ __forceinline__ void fused_barrier() { asm volatile("s_barrier" ::: "memory"); }  // no vmcnt(0) fence
 __device__ __forceinline__ void fused_wait_lgkm0() { __builtin_amdgcn_s_waitcnt(15 | (3 << 14) | (7 << 4)); }
 
-// A workgroup's items: those of XCD x (workgroup b runs on XCD b % 8) are a contiguous range, strided over its
-// workgroups, so the items of one pulsar run side by side on one XCD
-struct FusedItems {
-  int first, stride, count;
-  __device__ __forceinline__ explicit FusedItems(int n_items) {
+// A workgroup's items come from its XCD's queue (workgroup b runs on XCD b % 8): the items of XCD x are a contiguous
+// range (the items of one pulsar run side by side on one XCD, whose L2 then holds the pulsar's weights), handed out
+// one at a time by a ticket counter, so a workgroup that starts late (a co-running kernel held its CU) takes fewer
+// items instead of delaying the launch's end. Tickets are fetched two items ahead into an LDS ring of four; -1 = none.
+struct FusedQueue {
+  int first, end;
+  uint32_t* ticket;
+  __device__ __forceinline__ FusedQueue(int n_items, uint32_t* q) {
     const int per = (n_items + 7) >> 3;
     const int x = blockIdx.x & 7;
-    stride = gridDim.x >> 3;
-    first = x * per + (int)(blockIdx.x >> 3);
-    const int end = min(n_items, (x + 1) * per);
-    count = first < end ? (end - first + stride - 1) / stride : 0;
+    first = x * per;
+    end = min(n_items, first + per);
+    ticket = q + x;
   }
-  __device__ __forceinline__ int item(int k) const { return first + k * stride; }
+  // one lane: the next item of this XCD or -1 (a vector atomic: the lane's own address)
+  __device__ __forceinline__ int fetch() const {
+    const int t = (int)__hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return first + t < end ? first + t : -1;
+  }
 };
 
 }  // namespace
@@ -88,16 +94,39 @@ __global__ __launch_bounds__(64 * (kFusedIW + kFusedDW), 1) void k_grid_fused(Sy
                                                                              int32_t n_rb, int32_t n_items) {
   static_assert(kFusedReal == 32 && kFusedPitch == 32 && kFusedGroupModes * kFusedReal / 2 == 64 * kFusedDW,
                 "two realization tiles; one (mode, realization pair) of a 16-mode group per DFT lane");
-  extern __shared__ __attribute__((aligned(16))) double lds[];  // [grid rows][32] | ring [2][kFusedSlot] | sync word
-  const FusedItems items(n_items);
-  if (items.count == 0) return;  // the whole workgroup, before its first barrier
+  // [grid rows][32] | ring [2][kFusedMaxSig][kFusedSlot] | sync word, 3 pad | item ring [4]
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  const FusedQueue queue(n_items, f.queue);
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const int lr = lane & 15, lg = lane >> 4;
   double* __restrict__ ring = lds + f.ring_off;
   uint32_t* sync = (uint32_t*)(ring + 2 * kFusedMaxSig * kFusedSlot);
-  if (threadIdx.x == 0) *sync = 0u;
+  volatile int* qitem = (volatile int*)(sync + 4);  // item k at [k & 3]
+  if (threadIdx.x == 0) {
+    *sync = 0u;
+    qitem[0] = queue.fetch();
+    qitem[1] = qitem[0] >= 0 ? queue.fetch() : -1;
+  }
   __syncthreads();
+  // item k of this workgroup (k >= -1; valid once fetched: items k + 1 and k + 2 are fetched at the start of item k's
+  // build, before the barriers that publish them to the interpolation waves)
+  auto item_of = [&](int k) { return __builtin_amdgcn_readfirstlane(qitem[k & 3]); };
+  // the launch's last workgroup to finish zeroes the queues for the next launch (every workgroup's fetches precede
+  // its count)
+  auto finish = [&]() {
+    if (threadIdx.x == 0) {
+      __threadfence();
+      const uint32_t done = __hip_atomic_fetch_add(f.queue + 8, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+      if (done == gridDim.x - 1)
+        for (int i = 0; i < kFusedQueueWords; ++i)
+          __hip_atomic_store(f.queue + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  };
+  if (item_of(0) < 0) {  // the whole workgroup, before its first barrier
+    finish();
+    return;
+  }
 
   if (wave >= kFusedIW) {
     // ---------------------------------------------------------------- DFT waves
@@ -303,10 +332,12 @@ __global__ __launch_bounds__(64 * (kFusedIW + kFusedDW), 1) void k_grid_fused(Sy
     // loads of an iteration are issued before its steps.
     int sb = 0;  // ring slot of the item's group 0
     auto build = [&](int k) {
-      const int item = items.item(k);
+      if (dw == 0 && lane == 0) qitem[(k + 2) & 3] = item_of(k + 1) >= 0 ? queue.fetch() : -1;  // published by dsync
+      const int item = item_of(k);
       const int p = item / n_rb, r0 = (item - p * n_rb) * kFusedReal;
-      const bool nx = k + 1 < items.count;
-      const int item1 = nx ? items.item(k + 1) : item;
+      const int item1n = item_of(k + 1);
+      const bool nx = item1n >= 0;
+      const int item1 = nx ? item1n : item;
       const int p1 = item1 / n_rb, r1 = (item1 - p1 * n_rb) * kFusedReal;
 #pragma unroll
       for (int par = 0; par < 2; ++par)
@@ -377,8 +408,8 @@ __global__ __launch_bounds__(64 * (kFusedIW + kFusedDW), 1) void k_grid_fused(Sy
     };
     // item k + 1's draws and steps run while the interpolation waves read item k's grids (one build site: the
     // draws are most of the kernel's code)
-    for (int k = -1; k < items.count; ++k) {
-      const bool next = k + 1 < items.count;
+    for (int k = -1;; ++k) {
+      const bool next = item_of(k + 1) >= 0;
       if (next && !(FPTA_FUSED_CUT & 1)) build(k + 1);
       if (k >= 0) {
         fused_barrier();  // A(k): item k is interpolated
@@ -388,6 +419,7 @@ __global__ __launch_bounds__(64 * (kFusedIW + kFusedDW), 1) void k_grid_fused(Sy
       pf.lap(3);
       fused_barrier();  // B(k): item k + 1's grids are written
       pf.lap(4);
+      if (!next) break;
     }
     pf.flush(f.prof, wave);
     return;
@@ -401,6 +433,7 @@ __global__ __launch_bounds__(64 * (kFusedIW + kFusedDW), 1) void k_grid_fused(Sy
   // are read with readlane.
   struct ItemInfo {
     int p, r0, c0, n;  // pulsar, first realization, the wave's first chunk, the wave's chunks in the item
+    bool valid;        // an item (else past the workgroup's last)
     int64_t toa0;      // the pulsar's first TOA (residual column)
     int4 civ;          // lane i: band.chunks[c0 + kFusedIW i] (i < min(n, 64))
   };
@@ -409,8 +442,9 @@ __global__ __launch_bounds__(64 * (kFusedIW + kFusedDW), 1) void k_grid_fused(Sy
     it.c0 = 0;
     it.p = it.r0 = 0;
     it.toa0 = 0;
-    if (k < items.count) {
-      const int item = items.item(k);
+    const int item = item_of(k);
+    it.valid = item >= 0;
+    if (it.valid) {
       it.p = item / n_rb;
       it.r0 = (item - it.p * n_rb) * kFusedReal;
       const int cb = ld_uniform(f.psr_c0 + it.p) + wave, ce = ld_uniform(f.psr_c0 + it.p + 1);
@@ -554,7 +588,7 @@ __global__ __launch_bounds__(64 * (kFusedIW + kFusedDW), 1) void k_grid_fused(Sy
       ++k;
       it0 = it1;
       item_info(k + 1, it1);
-    } while (k < items.count && it0.n == 0);
+    } while (it0.valid && it0.n == 0);
     return nb;
   };
   fused_barrier();  // B(-1)
@@ -562,10 +596,10 @@ __global__ __launch_bounds__(64 * (kFusedIW + kFusedDW), 1) void k_grid_fused(Sy
   if (it0.n == 0) boundaries(advance_item());
   Ops o0, o1;  // operand sets in turn (chunks two at a time: no register copies; only o0 lives across iterations)
   int i = 0;   // the chunk in o0: the wave's i-th chunk of item k
-  if (k < items.count) load(it0.c0, chunk_info(it0, 0), o0);
+  if (it0.valid) load(it0.c0, chunk_info(it0, 0), o0);
   // the chunk after chunk i of item k: (same item, i + 1) or (it1's first chunk, crossing one item); an item of no
   // chunk for the wave is crossed without a chunk (advance_item)
-  while (k < items.count) {
+  while (it0.valid) {
     const bool same1 = i + 1 < it0.n;
     const bool next1 = same1 || it1.n > 0;
     chunk(it0.p, it0.r0, it0.toa0, o0, next1, same1 ? it0.c0 + kFusedIW * (i + 1) : it1.c0,
@@ -576,11 +610,11 @@ __global__ __launch_bounds__(64 * (kFusedIW + kFusedDW), 1) void k_grid_fused(Sy
       boundaries(advance_item());
       i = 0;
       if (!next1) {  // item k had no chunk for this wave: its first chunk is not in o1
-        if (k < items.count) load(it0.c0, chunk_info(it0, 0), o0);
+        if (it0.valid) load(it0.c0, chunk_info(it0, 0), o0);
         continue;
       }
     }
-    if (k >= items.count) break;
+    if (!it0.valid) break;
     const bool same2 = i + 1 < it0.n;
     const bool next2 = same2 || it1.n > 0;
     chunk(it0.p, it0.r0, it0.toa0, o1, next2, same2 ? it0.c0 + kFusedIW * (i + 1) : it1.c0,
@@ -590,10 +624,11 @@ __global__ __launch_bounds__(64 * (kFusedIW + kFusedDW), 1) void k_grid_fused(Sy
     } else {
       boundaries(advance_item());
       i = 0;
-      if (!next2 && k < items.count) load(it0.c0, chunk_info(it0, 0), o0);
+      if (!next2 && it0.valid) load(it0.c0, chunk_info(it0, 0), o0);
     }
   }
   pf.flush(f.prof, wave);
+  finish();  // thread 0 (an interpolation wave): after the last barrier, so after every fetch of the workgroup
 }
 
 hipError_t launch_grid_fused(hipStream_t st, const SynthArgs& a, const GridBand& band, const FusedArgs& f,
@@ -601,7 +636,7 @@ hipError_t launch_grid_fused(hipStream_t st, const SynthArgs& a, const GridBand&
   if (band.n_chunks <= 0 || band.vmax < 4 || band.vmax % 4 != 0 || a.R_pad % kFusedReal != 0 || a.w_on ||
       a.accumulate || a.part || !f.lrows || !f.psr_c0 || f.n_sig <= 0 || f.n_sig > kFusedMaxSig ||
       lds_bytes > (size_t)kFusedLdsMax || nq_max <= 0 || f.ring_off < 0 || f.fq < kFusedNQ || f.fq % 4 != 0 ||
-      (size_t)(f.ring_off + 2 * kFusedMaxSig * kFusedSlot) * sizeof(double) + sizeof(uint32_t) > lds_bytes)
+      !f.queue || (size_t)(f.ring_off + 2 * kFusedMaxSig * kFusedSlot) * sizeof(double) + 32 > lds_bytes)
     return hipErrorInvalidValue;
   int jobs = 0;
   for (int s = 0; s < f.n_sig; ++s) {

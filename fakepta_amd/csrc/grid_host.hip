@@ -566,7 +566,7 @@ int grid_build(fpta_ctx* c, Layout& L) {
       jobs += (gs->nf / 4 + 32) / 32;
       rows += gs->nf;
     }
-    const size_t lds = sizeof(double) * ((size_t)rows * kFusedPitch + 2 * kFusedMaxSig * kFusedSlot) + 16;
+    const size_t lds = sizeof(double) * ((size_t)rows * kFusedPitch + 2 * kFusedMaxSig * kFusedSlot) + 32;
     for (const std::vector<int32_t>& m : G.members) ok = ok && m.size() <= (size_t)kDftGenTerms;
     ok = ok && jobs <= kFusedDW && lds <= (size_t)kFusedLdsMax;
     if (ok) {
@@ -879,6 +879,12 @@ int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad, bool pipe) {
     HIPCHK(c, hipMemsetAsync(c->dbg_a.p, 0, sizeof(unsigned long long) * 8 * 8 * 4096, c->stream), "profile memset");
     f.prof = c->dbg_a.as<unsigned long long>();
 #endif
+    if (!c->fused_q_ready) {  // zeroed once: every launch leaves it zero (its last workgroup resets it)
+      HIPCHK(c, c->fused_q.ensure(sizeof(uint32_t) * kFusedQueueWords), "fused queue alloc");
+      HIPCHK(c, hipMemsetAsync(c->fused_q.p, 0, sizeof(uint32_t) * kFusedQueueWords, c->stream), "fused queue memset");
+      c->fused_q_ready = true;
+    }
+    f.queue = c->fused_q.as<uint32_t>();
     HIPCHK(c, launch_grid_fused(c->stream, a, band, f, nq, G.fused_lds), "k_grid_fused launch");
   } else if (psr) {
     kind = G.vmax <= 16 ? 6 : 7;  // launch_grid_interp_psr: NQ = 4 or 8 band steps
