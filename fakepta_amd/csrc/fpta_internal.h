@@ -229,8 +229,13 @@ struct FusedArgs {
   uint32_t k0, k1;
   unsigned long long* prof;  // -DFPTA_FUSED_PROF builds only: per-wave cycle counters [gridDim][8 waves][8]; else null
   uint32_t* queue;           // [kFusedQueueWords], zero at launch; the kernel's last workgroup zeroes it again
+  int32_t join_reserve;      // the DFT waves interpolate an item's chunks while more than this many are left
 };
 constexpr int kFusedQueueWords = 9;  // 8 per-XCD item tickets + the count of finished workgroups
+#ifndef FPTA_FUSED_JOIN_SAFETY
+#define FPTA_FUSED_JOIN_SAFETY 3.0  // variant builds may change it (make variant DEFS=-DFPTA_FUSED_JOIN_SAFETY=...)
+#endif
+constexpr double kFusedJoinSafety = FPTA_FUSED_JOIN_SAFETY;  // FusedArgs::join_reserve over the estimated need
 // nq_max: band steps of the widest chunk (vmax / 4; the kernel holds up to 12 steps' operands and takes a wider chunk's
 // in turns); lds_bytes: grids + ring + sync word
 hipError_t launch_grid_fused(hipStream_t st, const SynthArgs& a, const GridBand& band, const FusedArgs& f,

@@ -87,6 +87,15 @@ struct FusedQueue {
   }
 };
 
+// A chunk's operands for band steps 0 .. NS - 1 (further steps of a wider chunk are loaded one at a time)
+template <int NS>
+struct FusedOps {
+  int c;        // chunk (wave-uniform)
+  i32x4 ci;     // band.chunks[c] {pulsar, first TOA, count, band rows} (a vector load: every lane the same address)
+  dbl2 b[NS];   // weights of TOAs (2 lr, 2 lr + 1) at band row 4 q + lg
+  int row[NS];  // LDS grid row of band row 4 q + lg
+};
+
 }  // namespace
 
 template <int NQ, bool ODD>
@@ -94,7 +103,8 @@ __global__ __launch_bounds__(64 * (kFusedIW + kFusedDW), 1) void k_grid_fused(Sy
                                                                              int32_t n_rb, int32_t n_items) {
   static_assert(kFusedReal == 32 && kFusedPitch == 32 && kFusedGroupModes * kFusedReal / 2 == 64 * kFusedDW,
                 "two realization tiles; one (mode, realization pair) of a 16-mode group per DFT lane");
-  // [grid rows][32] | ring [2][kFusedMaxSig][kFusedSlot] | sync word, 3 pad | item ring [4]
+  // [grid rows][32] | ring [2][kFusedMaxSig][kFusedSlot] | sync word, 3 pad | item ring [4] | chunk tickets [2], 2 pad
+  // (48 bytes past the ring)
   extern __shared__ __attribute__((aligned(16))) double lds[];
   const FusedQueue queue(n_items, f.queue);
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -105,6 +115,8 @@ __global__ __launch_bounds__(64 * (kFusedIW + kFusedDW), 1) void k_grid_fused(Sy
   volatile int* qitem = (volatile int*)(sync + 4);  // item k at [k & 3]
   if (threadIdx.x == 0) {
     *sync = 0u;
+    ((volatile int*)sync)[8] = 0;  // chunk tickets of items 0 and 1
+    ((volatile int*)sync)[9] = 0;
     qitem[0] = queue.fetch();
     qitem[1] = qitem[0] >= 0 ? queue.fetch() : -1;
   }
@@ -128,6 +140,128 @@ __global__ __launch_bounds__(64 * (kFusedIW + kFusedDW), 1) void k_grid_fused(Sy
     return;
   }
 
+  // ------------------------------------------------------------------ chunks (both roles)
+  // Item k's chunks are handed out by an LDS ticket counter, ccnt[k & 1]: the interpolation waves take them, and so do
+  // the DFT waves once they have built item k + 1 (a layout of light DFTs, e.g. C4's one common signal, then gets eight
+  // interpolating waves). A wave takes tickets of its grid item k and of k + 1 only; counter k & 1 is zeroed by the DFT
+  // waves between barriers A(k - 2) and B(k - 2), after item k - 2's last ticket and before item k's first.
+  volatile int* ccnt = (volatile int*)(sync + 8);
+  struct Geo {          // item k
+    int p, r0, c0, n;   // pulsar, first realization, first chunk, chunks
+    int64_t toa0;       // the pulsar's first TOA (residual column)
+    bool valid;
+  };
+  auto geo = [&](int k) {
+    Geo g;
+    const int item = item_of(k);
+    g.valid = item >= 0;
+    const int it = g.valid ? item : 0;
+    g.p = it / n_rb;
+    g.r0 = (it - g.p * n_rb) * kFusedReal;
+    g.c0 = ld_uniform(f.psr_c0 + g.p);
+    g.n = g.valid ? ld_uniform(f.psr_c0 + g.p + 1) - g.c0 : 0;
+    g.toa0 = ld_uniform(a.offs + g.p);
+    return g;
+  };
+  auto ticket = [&](int k) {
+    int t = 0;
+    if (lane == 0)
+      t = __hip_atomic_fetch_add((int*)ccnt + (k & 1), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return __builtin_amdgcn_readfirstlane(t);
+  };
+  // Every operand of a chunk's band steps comes through vector loads (vmcnt): a scalar load waits lgkmcnt(0) (scalar
+  // loads return out of order), which also waits for the LDS grid reads. The chunk's table entry {pulsar, first TOA,
+  // count, band rows} is a vector load too (every lane the same address), issued with the operands and read at process.
+  using Ops = FusedOps<NQ>;
+  using OpsJ = FusedOps<(NQ < 8 ? NQ : 8)>;  // the DFT waves' joined chunks (fewer registers beside their own state)
+  // operands of band steps 0 .. NS - 1 of chunk cc, at constant offsets from two addresses (steps past the chunk's
+  // read the next chunk's or the tables' padding rows: never used)
+  auto load = [&](int cc, auto& o) {
+    constexpr int NS = sizeof(o.row) / sizeof(o.row[0]);
+    o.c = cc;
+    o.ci = *(const i32x4*)(band.chunks + cc);
+    const i32x4* __restrict__ rt = (const i32x4*)(f.lrows + ((int64_t)cc * 4 + lg) * f.fq);
+    const double* __restrict__ wp = band.wd + ((int64_t)cc * band.vmax + lg) * kGridTT + 2 * lr;
+#pragma unroll
+    for (int q4 = 0; q4 < NS / 4; ++q4) {
+      const i32x4 r4 = rt[q4];
+      o.row[4 * q4] = r4.x;
+      o.row[4 * q4 + 1] = r4.y;
+      o.row[4 * q4 + 2] = r4.z;
+      o.row[4 * q4 + 3] = r4.w;
+    }
+#pragma unroll
+    for (int q = 0; q < NS; ++q) o.b[q] = *(const dbl2*)(wp + 4 * kGridTT * q);
+  };
+  const int lds_lane = 2 * lr;  // this lane's realization pair in an LDS grid row
+  // chunk cur of item g: k_grid_interp_ws's MFMA steps (A = the realization pair's dbl2 of the LDS grid row, B = the
+  // TOA pair's weights) and stores
+  auto process = [&](const Geo& g, const auto& cur, auto& pf) {
+    constexpr int NS = sizeof(cur.row) / sizeof(cur.row[0]);
+    const int ty = __builtin_amdgcn_readfirstlane(cur.ci.y), tc = __builtin_amdgcn_readfirstlane(cur.ci.z);
+    const int nq = __builtin_amdgcn_readfirstlane(cur.ci.w) >> 2;
+    FPTA_DCHECK(nq > 0, "k_grid_fused band steps", nq, 1 << 20);
+    d4 acc[2][2];  // [TOA parity][realization tile]
+#pragma unroll
+    for (int e = 0; e < 2; ++e)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) acc[e][i] = d4{0.0, 0.0, 0.0, 0.0};
+    {
+      // step q's A operand is read from LDS ahead of step q - 1's MFMAs (rows past nq are valid clamped rows)
+      dbl2 an = *(const dbl2*)(lds + cur.row[0] * kFusedPitch + lds_lane);
+#pragma unroll
+      for (int q = 0; q < NS; ++q) {
+        if (q < nq) {
+          const dbl2 av = an;
+          if (q + 1 < NS) an = *(const dbl2*)(lds + cur.row[q + 1] * kFusedPitch + lds_lane);
+          const dbl2 bv = cur.b[q];
+          acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(av.x, bv.x, acc[0][0], 0, 0, 0);
+          acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(av.y, bv.x, acc[0][1], 0, 0, 0);
+          acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(av.x, bv.y, acc[1][0], 0, 0, 0);
+          acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(av.y, bv.y, acc[1][1], 0, 0, 0);
+        }
+      }
+    }
+    pf.lap(1);
+    // a chunk wider than NS steps (sparse pulsars): its further steps one at a time, each operand loaded and waited for
+    // here (off the common path, whose operands all arrive one chunk ahead)
+    for (int q = NS; q < nq; ++q) {
+      const int v = 4 * q + lg;
+      const int row = f.lrows[((int64_t)cur.c * 4 + lg) * f.fq + q];
+      const dbl2 bv = *(const dbl2*)(band.wd + ((int64_t)cur.c * band.vmax + v) * kGridTT + 2 * lr);
+      const dbl2 av = *(const dbl2*)(lds + row * kFusedPitch + lds_lane);
+      acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(av.x, bv.x, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(av.y, bv.x, acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(av.x, bv.y, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(av.y, bv.y, acc[1][1], 0, 0, 0);
+    }
+    pf.lap(4);
+    __builtin_amdgcn_sched_barrier(0);
+    // interp_store_rows' fast path from the item's first TOA: a full chunk, every realization of the item stored,
+    // 16-byte aligned rows: eight 16-byte non-temporal stores from one row base
+    const int64_t t0 = g.toa0 + ty;
+    if (tc == kGridTT && g.r0 + kFusedReal <= a.n_real && ((t0 | a.ldo) & 1) == 0 && a.ldo < ((int64_t)1 << 26)) {
+      const uint32_t vo = (uint32_t)(((int64_t)2 * lg * a.ldo + 2 * lr) * 8);
+      const char* base = (const char*)(a.out + t0 + (int64_t)g.r0 * a.ldo);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int gg = 0; gg < 4; ++gg)
+          __builtin_nontemporal_store(dbl2{acc[0][i][gg], acc[1][i][gg]},
+                                      (dbl2*)((char*)base + (int64_t)(8 * gg + i) * a.ldo * 8 + vo));
+    } else {
+      InterpTile<2> t;
+      t.c = cur.c;
+      t.p = g.p;
+      t.r0 = g.r0;
+      t.y = ty;
+      t.cnt = tc;
+      t.nq = nq;
+      interp_store_rows<2>(a, a.out, t, acc);
+    }
+    pf.lap(2);
+  };
+
   if (wave >= kFusedIW) {
     // ---------------------------------------------------------------- DFT waves
     const int dw = wave - kFusedIW;
@@ -148,8 +282,8 @@ __global__ __launch_bounds__(64 * (kFusedIW + kFusedDW), 1) void k_grid_fused(Sy
     }
     js = __builtin_amdgcn_readfirstlane(js);
     jrc = __builtin_amdgcn_readfirstlane(jrc);
-    Prof pf;  // DFT waves: 0 loads issue, 1 MFMA steps, 2 ring sync, 3 grid writes, 4 barriers, 5 iterations, 6 draws,
-              // 7 the first item's first draws
+    Prof pf;  // DFT waves: 0 loads issue, 1 MFMA steps (DFT and joined chunks), 2 ring sync / joined chunks' stores, 3 grid
+              // writes, 4 barriers / joined wide chunks, 5 iterations, 6 draws, 7 joined chunks (count)
     pf.start();
     uint32_t epoch = 0;
     // every DFT wave's ring writes and reads so far are done (an LDS counter; the interpolation waves run on)
@@ -173,7 +307,17 @@ __global__ __launch_bounds__(64 * (kFusedIW + kFusedDW), 1) void k_grid_fused(Sy
     // this wave's job, hoisted: its table rows (parity 0 cos, t = lg, rows 32 jrc + 2 lr) and k-steps per parity
     const FusedSig& jf = f.s[js < 0 ? 0 : js];
     const int64_t jts = (int64_t)jf.ntq * jf.ldq, jld4 = 4 * (int64_t)jf.ldq;
-    const double* __restrict__ jtq = jf.tq + (int64_t)lg * jf.ldq + 32 * jrc + 2 * lr;
+    // Lane-derived addresses are re-derived where used from an opaque copy of the lane index: hoisted out of the item
+    // loop they would stay live across the joined chunks (see join) and spill
+    auto lane_now = [&]() {
+      int v = lane;
+      asm volatile("" : "+v"(v));
+      return v;
+    };
+    auto jtq_now = [&]() {
+      const int ln = lane_now();
+      return jf.tq + (int64_t)(ln >> 4) * jf.ldq + 32 * jrc + 2 * (ln & 15);
+    };
     const int jnq0 = (((jf.nm + 1) >> 1) + 3) >> 2, jnq1 = ((jf.nm >> 1) + 3) >> 2;
     const int jng = js < 0 ? 0 : (jnq0 + 1) >> 1;
     // [parity: 0 odd k, 1 even k][row tile h: rows 2 i + h][realization tile t]
@@ -187,12 +331,11 @@ __global__ __launch_bounds__(64 * (kFusedIW + kFusedDW), 1) void k_grid_fused(Sy
     //  draw_store: amp * z (rounded) and the loaded values summed in the terms' order, into the ring.
     // The signal index is a constant wherever these run (loops over kFusedMaxSig unrolled): the descriptor's fields are
     // scalar loads at fixed kernel-argument offsets, not re-read by computed index in every group.
-    const int didx = dw * 64 + lane;
-    const int dmm = didx >> 4, drl = 2 * (didx & 15);
     struct DrawIn {
       dbl2 x0[kFusedTerms], x1[kFusedTerms];  // generated: x0.x amplitude pair; loaded: x0 cos pair, x1 sin pair
     };
     auto draw_load = [&](const FusedSig& fs, int g, int p, int r0, DrawIn& in) {
+      const int didx = dw * 64 + lane_now(), dmm = didx >> 4, drl = 2 * (didx & 15);
       const int m = kFusedGroupModes * g + dmm, r = r0 + drl;
 #pragma unroll
       for (int i = 0; i < kFusedTerms; ++i) {
@@ -213,6 +356,7 @@ __global__ __launch_bounds__(64 * (kFusedIW + kFusedDW), 1) void k_grid_fused(Sy
       }
     };
     auto draw_finish = [&](const FusedSig& fs, int g, int p, int r0, double* __restrict__ slot_s, const DrawIn& in) {
+      const int didx = dw * 64 + lane_now(), dmm = didx >> 4, drl = 2 * (didx & 15);
       const int m = kFusedGroupModes * g + dmm, r = r0 + drl;
       const uint64_t gr = (uint64_t)(f.real0 + r);
       double bc[2] = {0.0, 0.0}, bs[2] = {0.0, 0.0};
@@ -297,7 +441,7 @@ __global__ __launch_bounds__(64 * (kFusedIW + kFusedDW), 1) void k_grid_fused(Sy
         const int q = max(0, min(2 * g + h2, jnq0 - 1));
 #pragma unroll
         for (int par = 0; par < 2; ++par) {
-          const double* __restrict__ tc = jtq + (int64_t)(2 * par) * jts + q * jld4;
+          const double* __restrict__ tc = jtq_now() + (int64_t)(2 * par) * jts + q * jld4;
           tb.ac[h2][par] = ld_global((const dbl2*)tc);
           tb.as[h2][par] = ld_global((const dbl2*)(tc + jts));
         }
@@ -353,7 +497,7 @@ __global__ __launch_bounds__(64 * (kFusedIW + kFusedDW), 1) void k_grid_fused(Sy
           draw_load(f.s[s], 0, p, r0, in);
           draw_finish(f.s[s], 0, p, r0, slot_of(sb, s), in);
         }
-        pf.lap(7);
+        pf.lap(6);
         dsync();
         pf.lap(2);
       }
@@ -408,223 +552,122 @@ __global__ __launch_bounds__(64 * (kFusedIW + kFusedDW), 1) void k_grid_fused(Sy
     };
     // item k + 1's draws and steps run while the interpolation waves read item k's grids (one build site: the
     // draws are most of the kernel's code)
+    // Before building item k + 1 (its accumulators not yet live), chunks of item k while more than f.join_reserve of
+    // its tickets are left: the interpolation waves keep that many for the build's duration (host estimate; a layout
+    // whose DFTs take as long as its interpolation, C2, never joins). The counter is peeked first, so a ticket taken is
+    // always processed.
+    auto join = [&](int k) {
+      if (FPTA_FUSED_CUT & 6) return;
+      const Geo g = geo(k);
+      while (__builtin_amdgcn_readfirstlane(ccnt[k & 1]) < g.n - f.join_reserve) {
+        const int t = ticket(k);
+        if (t >= g.n) break;
+        OpsJ o;
+        load(g.c0 + t, o);
+        process(g, o, pf);
+        pf.count(7);
+      }
+    };
+    // (one build site and one grid write per trip: the accumulators are dead from the write to the next build, so the
+    // joined chunks have the registers)
     for (int k = -1;; ++k) {
       const bool next = item_of(k + 1) >= 0;
+      if (k >= 0) join(k);
       if (next && !(FPTA_FUSED_CUT & 1)) build(k + 1);
       if (k >= 0) {
         fused_barrier();  // A(k): item k is interpolated
         pf.lap(4);
+        if (dw == 0 && lane == 0) ccnt[k & 1] = 0;  // item k + 2's tickets (item k's are all taken)
       }
-      if (next) write_grid();
+      if (!next) {
+        fused_wait_lgkm0();
+        fused_barrier();  // B(k)
+        break;
+      }
+      write_grid();
       pf.lap(3);
       fused_barrier();  // B(k): item k + 1's grids are written
       pf.lap(4);
-      if (!next) break;
     }
     pf.flush(f.prof, wave);
     return;
   }
 
   // ------------------------------------------------------------------ interpolation waves
-  // Every operand of a chunk's band steps comes through vector loads (vmcnt): a scalar load waits lgkmcnt(0) (scalar
-  // loads return out of order), which also waits for the LDS grid reads, and a lane select of four scalar rows
-  // compiles to divergent branches. The chunk table entries {first TOA, count, band rows} of an item's chunks for this
-  // wave sit in the lanes of one VGPR quad (ItemInfo::civ, lane i = the wave's i-th chunk, loaded one item ahead) and
-  // are read with readlane.
-  struct ItemInfo {
-    int p, r0, c0, n;  // pulsar, first realization, the wave's first chunk, the wave's chunks in the item
-    bool valid;        // an item (else past the workgroup's last)
-    int64_t toa0;      // the pulsar's first TOA (residual column)
-    int4 civ;          // lane i: band.chunks[c0 + kFusedIW i] (i < min(n, 64))
-  };
-  auto item_info = [&](int k, ItemInfo& it) {  // the loads of civ are left in flight
-    it.n = 0;
-    it.c0 = 0;
-    it.p = it.r0 = 0;
-    it.toa0 = 0;
-    const int item = item_of(k);
-    it.valid = item >= 0;
-    if (it.valid) {
-      it.p = item / n_rb;
-      it.r0 = (item - it.p * n_rb) * kFusedReal;
-      const int cb = ld_uniform(f.psr_c0 + it.p) + wave, ce = ld_uniform(f.psr_c0 + it.p + 1);
-      it.toa0 = ld_uniform(a.offs + it.p);
-      it.c0 = cb;
-      it.n = cb < ce ? (ce - cb + kFusedIW - 1) / kFusedIW : 0;
-    }
-    const int cl = it.n > 0 ? it.c0 + kFusedIW * min(lane, it.n - 1) : 0;
-    const i32x4 v = *(const i32x4*)(band.chunks + cl);
-    it.civ = make_int4(v.x, v.y, v.z, v.w);
-  };
-  // {pulsar, first TOA, count, band rows} of the wave's i-th chunk of the item
-  auto chunk_info = [&](const ItemInfo& it, int i) {
-    if (i < 64)
-      return make_int4(it.p, __builtin_amdgcn_readlane(it.civ.y, i), __builtin_amdgcn_readlane(it.civ.z, i),
-                       __builtin_amdgcn_readlane(it.civ.w, i));
-    return ld_uniform4(band.chunks + it.c0 + kFusedIW * i);  // a pulsar of more than 256 chunks
-  };
-  struct Ops {
-    int4 ci;      // {pulsar, first TOA, count, band rows} (wave-uniform)
-    int c, nq;    // chunk, band steps (wave-uniform)
-    dbl2 b[NQ];   // weights of TOAs (2 lr, 2 lr + 1) at band row 4 (q0 + q) + lg
-    int row[NQ];  // LDS grid row of band row 4 (q0 + q) + lg
-  };
-  // operands of band steps 0 .. NQ - 1 of chunk cc, at constant offsets from two addresses (steps past nq read the
-  // next chunk's or the tables' padding rows: never used)
-  auto load = [&](int cc, int4 ci, Ops& o) {
-    o.ci = ci;
-    o.c = cc;
-    o.nq = ci.w >> 2;
-    FPTA_DCHECK(o.nq > 0, "k_grid_fused band steps", o.nq, 1 << 20);
-    const i32x4* __restrict__ rt = (const i32x4*)(f.lrows + ((int64_t)cc * 4 + lg) * f.fq);
-    const double* __restrict__ wp = band.wd + ((int64_t)cc * band.vmax + lg) * kGridTT + 2 * lr;
-#pragma unroll
-    for (int q4 = 0; q4 < NQ / 4; ++q4) {
-      const i32x4 r4 = rt[q4];
-      o.row[4 * q4] = r4.x;
-      o.row[4 * q4 + 1] = r4.y;
-      o.row[4 * q4 + 2] = r4.z;
-      o.row[4 * q4 + 3] = r4.w;
-    }
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) o.b[q] = *(const dbl2*)(wp + 4 * kGridTT * q);
-  };
-  const int lds_lane = 2 * lr;  // this lane's realization pair in an LDS grid row
-  Prof pf;  // interpolation waves: 0 next-chunk loads, 1 MFMA steps, 2 stores, 3 barriers, 4 wide-chunk reloads, 5 chunks
+  Prof pf;  // interpolation waves: 0 next-chunk loads, 1 MFMA steps, 2 stores, 3 barriers, 4 wide-chunk steps, 5 chunks,
+            // 6 ticket + stream
   pf.start();
-  // The chunk in cur (of the item at pulsar p, realizations r0 ..); the next one's operands (this item's, or the next
-  // item's first) are loaded into nxt first, so their latency hides behind this chunk's MFMAs and they precede this
-  // chunk's stores in the vmcnt queue.
-  // Loads are never conditional: a load on one side of a branch makes the compiler's vmcnt wait after the join count
-  // from the side without it, i.e. wait for nearly every load in flight (the next chunk's included). Without a next
-  // chunk the current one's operands are loaded again (never used).
-  auto chunk = [&](int p, int r0, int64_t toa0, Ops& cur, bool has_next, int c_next, int4 ci_next, Ops& nxt) {
-    if (FPTA_FUSED_CUT & 2) return;
-    pf.lap(6);
-    load(has_next ? c_next : cur.c, has_next ? ci_next : cur.ci, nxt);
-    pf.lap(0);
-    pf.count(5);
-    d4 acc[2][2];  // [TOA parity][realization tile]
-#pragma unroll
-    for (int e = 0; e < 2; ++e)
-#pragma unroll
-      for (int i = 0; i < 2; ++i) acc[e][i] = d4{0.0, 0.0, 0.0, 0.0};
-    {
-      // step q's A operand is read from LDS ahead of step q - 1's MFMAs (rows past nq are valid clamped rows)
-      dbl2 an = *(const dbl2*)(lds + cur.row[0] * kFusedPitch + lds_lane);
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-        if (q < cur.nq) {
-          const dbl2 av = an;
-          if (q + 1 < NQ) an = *(const dbl2*)(lds + cur.row[q + 1] * kFusedPitch + lds_lane);
-          const dbl2 bv = cur.b[q];
-          acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(av.x, bv.x, acc[0][0], 0, 0, 0);
-          acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(av.y, bv.x, acc[0][1], 0, 0, 0);
-          acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(av.x, bv.y, acc[1][0], 0, 0, 0);
-          acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(av.y, bv.y, acc[1][1], 0, 0, 0);
-        }
-      }
-    }
-    pf.lap(1);
-    // a chunk wider than NQ steps (sparse pulsars): its further steps one at a time, each operand loaded and waited for
-    // here (off the common path, whose operands all arrive one chunk ahead)
-    for (int q = NQ; q < cur.nq; ++q) {
-      const int v = 4 * q + lg;
-      const int row = f.lrows[((int64_t)cur.c * 4 + lg) * f.fq + q];
-      const dbl2 bv = *(const dbl2*)(band.wd + ((int64_t)cur.c * band.vmax + v) * kGridTT + 2 * lr);
-      const dbl2 av = *(const dbl2*)(lds + row * kFusedPitch + lds_lane);
-      acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(av.x, bv.x, acc[0][0], 0, 0, 0);
-      acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(av.y, bv.x, acc[0][1], 0, 0, 0);
-      acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(av.x, bv.y, acc[1][0], 0, 0, 0);
-      acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(av.y, bv.y, acc[1][1], 0, 0, 0);
-    }
-    pf.lap(4);
-    __builtin_amdgcn_sched_barrier(0);
-    // interp_store_rows' fast path from the item's first TOA (toa0, a scalar of the item): a full chunk, every
-    // realization of the item stored, 16-byte aligned rows: eight 16-byte non-temporal stores from one row base
-    const int64_t t0 = toa0 + cur.ci.y;
-    if (cur.ci.z == kGridTT && r0 + kFusedReal <= a.n_real && ((t0 | a.ldo) & 1) == 0 && a.ldo < ((int64_t)1 << 26)) {
-      const uint32_t vo = (uint32_t)(((int64_t)2 * lg * a.ldo + 2 * lr) * 8);
-      const char* base = (const char*)(a.out + t0 + (int64_t)r0 * a.ldo);
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int g = 0; g < 4; ++g)
-          __builtin_nontemporal_store(dbl2{acc[0][i][g], acc[1][i][g]},
-                                      (dbl2*)((char*)base + (int64_t)(8 * g + i) * a.ldo * 8 + vo));
-    } else {
-      InterpTile<2> t;
-      t.c = cur.c;
-      t.p = p;
-      t.r0 = r0;
-      t.y = cur.ci.y;
-      t.cnt = cur.ci.z;
-      t.nq = cur.nq;
-      interp_store_rows<2>(a, a.out, t, acc);
-    }
-    pf.lap(2);
-  };
-  // The wave's chunks of all its items as one stream: after chunk i of item k (it0) the next one is chunk i + 1, or the
-  // first chunk of the next item that has one for this wave (it1: item k + 1's table, loaded one item ahead); every item
-  // boundary crossed is a barrier pair A / B (item k interpolated / item k + 1's grids written), which the DFT waves
-  // pass once per item as well.
-  ItemInfo it0, it1;
-  int k = 0;
-  item_info(0, it0);
-  item_info(1, it1);
-  auto boundaries = [&](int nb) {
-    if (nb > 0) fused_wait_lgkm0();  // every grid read of the item is done
-    for (int i = 0; i < nb; ++i) {
-      fused_barrier();  // A
-      fused_barrier();  // B
-    }
-    pf.lap(3);
-  };
-  // move to the next item that has a chunk for this wave (or past the last): the barrier pairs of the items left
-  auto advance_item = [&]() {
-    int nb = 0;
-    do {
-      ++nb;
-      ++k;
-      it0 = it1;
-      item_info(k + 1, it1);
-    } while (it0.valid && it0.n == 0);
-    return nb;
-  };
   fused_barrier();  // B(-1)
   pf.lap(3);
-  if (it0.n == 0) boundaries(advance_item());
-  Ops o0, o1;  // operand sets in turn (chunks two at a time: no register copies; only o0 lives across iterations)
-  int i = 0;   // the chunk in o0: the wave's i-th chunk of item k
-  if (it0.valid) load(it0.c0, chunk_info(it0, 0), o0);
-  // the chunk after chunk i of item k: (same item, i + 1) or (it1's first chunk, crossing one item); an item of no
-  // chunk for the wave is crossed without a chunk (advance_item)
-  while (it0.valid) {
-    const bool same1 = i + 1 < it0.n;
-    const bool next1 = same1 || it1.n > 0;
-    chunk(it0.p, it0.r0, it0.toa0, o0, next1, same1 ? it0.c0 + kFusedIW * (i + 1) : it1.c0,
-          same1 ? chunk_info(it0, i + 1) : chunk_info(it1, 0), o1);
-    if (same1) {
-      ++i;
-    } else {
-      boundaries(advance_item());
-      i = 0;
-      if (!next1) {  // item k had no chunk for this wave: its first chunk is not in o1
-        if (it0.valid) load(it0.c0, chunk_info(it0, 0), o0);
-        continue;
+  int k = 0;                        // the item whose grids are in LDS (between barriers B(k - 1) and A(k))
+  Geo g0 = geo(0), g1 = geo(1);     // items k, k + 1
+  bool ex0 = false, ex1 = false;    // this wave found no ticket left in item k / k + 1
+  // the next chunk for this wave: a ticket of item k, else of k + 1 (never further: item k + 2's counter is zeroed
+  // after A(k)); -1 none. kn = its item.
+  auto next = [&](int& kn) {
+    if (!ex0) {
+      const int t = ticket(k);
+      if (t < g0.n) {
+        kn = k;
+        return g0.c0 + t;
       }
+      ex0 = true;
     }
-    if (!it0.valid) break;
-    const bool same2 = i + 1 < it0.n;
-    const bool next2 = same2 || it1.n > 0;
-    chunk(it0.p, it0.r0, it0.toa0, o1, next2, same2 ? it0.c0 + kFusedIW * (i + 1) : it1.c0,
-          same2 ? chunk_info(it0, i + 1) : chunk_info(it1, 0), o0);
-    if (same2) {
-      ++i;
-    } else {
-      boundaries(advance_item());
-      i = 0;
-      if (!next2 && it0.valid) load(it0.c0, chunk_info(it0, 0), o0);
+    if (!ex1 && g1.valid) {
+      const int t = ticket(k + 1);
+      if (t < g1.n) {
+        kn = k + 1;
+        return g1.c0 + t;
+      }
+      ex1 = true;
+    }
+    kn = -1;
+    return -1;
+  };
+  // chunk cur of item k; the next one's operands (this item's or the next item's) are loaded into nxt first, so their
+  // latency hides behind this chunk's MFMAs and they precede this chunk's stores in the vmcnt queue. Loads are never
+  // conditional (a load on one side of a branch makes the compiler's vmcnt wait after the join count from the side
+  // without it): without a next chunk the current one's operands are loaded again (never used).
+  auto step = [&](Ops& cur, Ops& nxt, int& kc) {
+    pf.lap(6);
+    int kn;
+    const int cn = next(kn);
+    load(cn >= 0 ? cn : cur.c, nxt);
+    pf.lap(0);
+    pf.count(5);
+    if (!(FPTA_FUSED_CUT & 2)) process(g0, cur, pf);
+    kc = kn;
+  };
+  Ops o0, o1;  // operand sets in turn (two chunks per loop trip: no register copies but at item crossings)
+  int kc;      // item of the chunk in o0 (-1: none)
+  {
+    const int cc = next(kc);
+    load(cc >= 0 ? cc : g0.c0, o0);
+  }
+  for (;;) {
+    while (kc == k) {
+      step(o0, o1, kc);
+      if (kc != k) {
+        o0 = o1;  // the next item's chunk (or none): once per item crossing
+        break;
+      }
+      step(o1, o0, kc);
+    }
+    // no chunk of item k left for this wave: cross A(k), B(k)
+    fused_wait_lgkm0();  // every grid read of the item is done
+    pf.lap(6);
+    fused_barrier();  // A(k)
+    fused_barrier();  // B(k)
+    pf.lap(3);
+    ++k;
+    g0 = g1;
+    g1 = geo(k + 1);
+    ex0 = ex1;
+    ex1 = false;
+    if (!g0.valid) break;
+    if (kc < 0) {
+      const int cc = next(kc);
+      load(cc >= 0 ? cc : g0.c0, o0);
     }
   }
   pf.flush(f.prof, wave);
@@ -633,10 +676,10 @@ __global__ __launch_bounds__(64 * (kFusedIW + kFusedDW), 1) void k_grid_fused(Sy
 
 hipError_t launch_grid_fused(hipStream_t st, const SynthArgs& a, const GridBand& band, const FusedArgs& f,
                              int32_t nq_max, size_t lds_bytes) {
-  if (band.n_chunks <= 0 || band.vmax < 4 || band.vmax % 4 != 0 || a.R_pad % kFusedReal != 0 || a.w_on ||
+  if (band.n_chunks <= 0 || band.vmax < 4 || f.join_reserve < 0 || band.vmax % 4 != 0 || a.R_pad % kFusedReal != 0 || a.w_on ||
       a.accumulate || a.part || !f.lrows || !f.psr_c0 || f.n_sig <= 0 || f.n_sig > kFusedMaxSig ||
       lds_bytes > (size_t)kFusedLdsMax || nq_max <= 0 || f.ring_off < 0 || f.fq < kFusedNQ || f.fq % 4 != 0 ||
-      !f.queue || (size_t)(f.ring_off + 2 * kFusedMaxSig * kFusedSlot) * sizeof(double) + 32 > lds_bytes)
+      !f.queue || (size_t)(f.ring_off + 2 * kFusedMaxSig * kFusedSlot) * sizeof(double) + 48 > lds_bytes)
     return hipErrorInvalidValue;
   int jobs = 0;
   for (int s = 0; s < f.n_sig; ++s) {

@@ -566,7 +566,7 @@ int grid_build(fpta_ctx* c, Layout& L) {
       jobs += (gs->nf / 4 + 32) / 32;
       rows += gs->nf;
     }
-    const size_t lds = sizeof(double) * ((size_t)rows * kFusedPitch + 2 * kFusedMaxSig * kFusedSlot) + 32;
+    const size_t lds = sizeof(double) * ((size_t)rows * kFusedPitch + 2 * kFusedMaxSig * kFusedSlot) + 48;
     for (const std::vector<int32_t>& m : G.members) ok = ok && m.size() <= (size_t)kDftGenTerms;
     ok = ok && jobs <= kFusedDW && lds <= (size_t)kFusedLdsMax;
     if (ok) {
@@ -866,6 +866,22 @@ int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad, bool pipe) {
         fs.term_col0[0] = d.col0;
         fs.n_terms = 1;
       }
+    }
+    // The DFT waves interpolate an item's chunks while more than join_reserve are left, then build the next item
+    // while the interpolation waves take the rest. In MFMA-equivalents (64 cycles): a ring iteration of a DFT wave is
+    // its 32 MFMAs + ~20 per generated term (a Philox call and two Box-Muller pairs per lane), a chunk 4 per band step
+    // + ~12 (operand loads, stores). The reserve is kFusedJoinSafety times the chunks the interpolation waves do in a
+    // build: C2 (~7 x 70 per build, ~48 per chunk, 63 chunks per item) never joins; C4 (~7 x 32, ~32 per chunk, 313
+    // chunks per item) joins for most of an item.
+    {
+      int it_max = 0, gen = 0;
+      for (int32_t s = 0; s < f.n_sig; ++s) {
+        const int nm = f.s[s].nm;
+        it_max = std::max(it_max, (((((nm + 1) >> 1) + 3) >> 2) + 1) >> 1);
+        for (int i = 0; i < f.s[s].n_terms; ++i) gen += f.s[s].term_kind[i] == 0;
+      }
+      const double build = it_max * (32.0 + 20.0 * gen), chunk = G.mean_v + 12.0;
+      f.join_reserve = (int32_t)std::min(1.0e6, std::ceil(kFusedJoinSafety * kFusedIW * build / chunk));
     }
     f.ring_off = (G.fused_lrow0.back() + G.segs.back()->nf) * kFusedPitch;
     f.lrows = G.frows.as<int32_t>();

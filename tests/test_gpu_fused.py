@@ -117,6 +117,38 @@ def test_fused_synthesis_is_bitwise_identical(ctx, capi, shipped, layout, dft_ge
         ctx.set_options(shipped)
 
 
+@pytest.mark.parametrize("R,real0", [(256, 0), (333, 7), (64, 32)])
+def test_fused_dft_waves_join_long_pulsars(ctx, capi, shipped, R, real0):
+    """C4's shape at small scale: one 100-mode common (ORF-mixed) signal, so the DFT waves only load their terms, and
+    pulsars of thousands of TOAs (hundreds of chunks per item): the DFT waves take chunk tickets of the item being
+    interpolated before they build the next one (FusedArgs.join_reserve), beside the interpolation waves. Ragged
+    pulsars (one short: an item whose chunks all go to the interpolation waves), the block bit-identical to the
+    two-kernel path and every sample written; and the oracle."""
+    rng = np.random.default_rng(229)
+    counts = np.array([6000, 4100, 90, 5200])
+    offs = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
+    t0, t1 = 4.4e9, 4.4e9 + 3.15e8
+    toas = np.concatenate([np.concatenate([[t0], np.sort(rng.uniform(t0, t1, k - 2)), [t1]]) for k in counts])
+    nu = np.full(offs[-1], 1400.0)
+    ctx.batch_set_toas(offs, toas, nu)
+    f, a, L, _ = common_signal(rng, offs, toas, 100)
+    ctx.batch_add_signal(1, f, a, L=L)
+    segs = [O.Segment(1, 2 * np.pi * f, a, 0.0, L=L)]
+    try:
+        ctx.set_option(capi.OPT_SYNTH_PATH, 4)
+        ref, k0 = _run(ctx, capi, 0, 31, real0, R)
+        got, k1 = _run(ctx, capi, 1, 31, real0, R)
+        assert k1.startswith("k_grid_fused"), k1
+        assert np.all(np.isfinite(got))
+        np.testing.assert_array_equal(ref, got)
+        want = O.batch_synth(offs, toas, nu, segs, 31, real0, R)
+        assert rel_err(got, want) <= GRID_TOL
+        assert_parity(got, want, TOL)
+    finally:
+        ctx.batch_clear()
+        ctx.set_options(shipped)
+
+
 def test_fused_pipelined_blocks(ctx, capi, shipped):
     """Pipelined blocks (FPTA_OPT_OVERLAP 1) on the fused kernel: the next block's common draws go into the other
     coefficient buffer on the side stream while this block's kernel reads its own. Blocks queued back to back without a

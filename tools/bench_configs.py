@@ -183,12 +183,12 @@ def c3(total):
                      "sharded job with fused checksums)")
 
 
-def c4(steps=5):
-    from fakepta_amd import _capi
+def c4_layout(ctx):
+    """C4's array on ctx (1000 psr x 10k TOAs, HD100 common signal with the batch path's Cholesky factor); returns
+    (P, n_p, N, L)."""
     from fakepta.constants import yr
     from fakepta.spectrum import powerlaw
-    ctx = new_context(_capi)
-    P, n_p, N, R = 1000, 10000, 100, 256
+    P, n_p, N = 1000, 10000, 100
     rng = np.random.default_rng(0)
     T = 10 * yr
     offs = (np.arange(P + 1) * n_p).astype(np.int64)
@@ -206,6 +206,14 @@ def c4(steps=5):
     amp = np.sqrt(powerlaw(f, -15.0, 13 / 3) * np.diff(np.append(0.0, f)))  # df as fake_pta.py:370
     ctx.batch_set_toas(offs, toas, nu)
     ctx.batch_add_signal(1, f, amp, idx=0.0, L=L)
+    return P, n_p, N, L
+
+
+def c4(steps=5):
+    from fakepta_amd import _capi
+    ctx = new_context(_capi)
+    R = 256
+    P, n_p, N, L = c4_layout(ctx)
     dt = timed(ctx, _capi, lambda s: ctx.batch_synth(7, s * R, R, to_host=False), steps, warmup=1)
     kt1 = isolated(ctx, _capi, lambda s: ctx.batch_synth(7, s * R, R, to_host=False), 3)
     flops = 2.0 * 2 * N * P * n_p * R

@@ -8,8 +8,7 @@ root=$(cd "$(dirname "$0")/.." && pwd)
 tmp=$(mktemp -d)
 git -C "$root" archive "$rev" fakepta_amd/csrc include | tar -x -C "$tmp"
 mkdir -p "$(dirname "$root/$out")"
-cd "$tmp/fakepta_amd/csrc"
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -Wall -Wno-unused-result -ffp-contract=fast \
-  -fno-gpu-rdc kernels.hip dense.hip grid.hip grid_mfma.hip capi.hip -o "$root/$out" -L/opt/rocm/lib -lrccl
+make -C "$tmp/fakepta_amd/csrc" -j8 > /dev/null  # the revision's own source list and flags
+cp "$tmp/fakepta_amd/lib/libfakepta_amd.so" "$root/$out"
 rm -rf "$tmp"
 echo "$out <- $rev"

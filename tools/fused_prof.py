@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--blocks", type=int, default=3)
     ap.add_argument("--ghz", type=float, default=2.2, help="clock for the cycle -> time conversion")
     ap.add_argument("--opt", action="append", default=[])
+    ap.add_argument("--config", default="c2", choices=["c2", "c4"])
     args = ap.parse_args()
     from bench import build_array
     from fakepta_amd import _capi
@@ -32,14 +33,22 @@ def main():
     if fn is None:
         sys.exit("fused_prof.py: the loaded library is not a -DFPTA_FUSED_PROF build")
     ctx = _capi.Context(0)
-    psrs = build_array(100, 2000, "c2")
-    sim = BatchSimulator(psrs, white=False, ctx=ctx)
+    if args.config == "c2":
+        psrs = build_array(100, 2000, "c2")
+        sim = BatchSimulator(psrs, white=False, ctx=ctx)
+        R = 1024
+        run = lambda b: sim.synth(R, seed=1234, real0=b * R, to_host=False)  # noqa: E731
+    else:  # C4's layout (tools/bench_configs.py c4): 1000 psr x 10k TOAs, HD100, R = 256
+        from tools.bench_configs import c4_layout
+        c4_layout(ctx)
+        R = 256
+        run = lambda b: ctx.batch_synth(7, b * R, R, to_host=False)  # noqa: E731
     ctx.set_option(_capi.OPT_OVERLAP, args.overlap)
     for kv in args.opt:
         k, v = kv.split("=")
         ctx.set_option(getattr(_capi, "OPT_" + k.upper()), int(v))
     for b in range(args.blocks):
-        sim.synth(1024, seed=1234, real0=b * 1024, to_host=False)
+        run(b)
     ctx.synchronize()
     print("kernel:", ctx.batch_grid_info()["interp_kernel"])
     n = 4096 * 8 * 8
