@@ -233,7 +233,7 @@ struct FusedArgs {
 };
 constexpr int kFusedQueueWords = 9;  // 8 per-XCD item tickets + the count of finished workgroups
 #ifndef FPTA_FUSED_JOIN_SAFETY
-#define FPTA_FUSED_JOIN_SAFETY 3.0  // variant builds may change it (make variant DEFS=-DFPTA_FUSED_JOIN_SAFETY=...)
+#define FPTA_FUSED_JOIN_SAFETY 1.5  // measured best of 0.5 .. 5 on C2 and C4 (profiles/round5/r5mn_*); variants may change it (make variant DEFS=-DFPTA_FUSED_JOIN_SAFETY=...)
 #endif
 constexpr double kFusedJoinSafety = FPTA_FUSED_JOIN_SAFETY;  // FusedArgs::join_reserve over the estimated need
 // nq_max: band steps of the widest chunk (vmax / 4; the kernel holds up to 12 steps' operands and takes a wider chunk's

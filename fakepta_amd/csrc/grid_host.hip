@@ -871,8 +871,9 @@ int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad, bool pipe) {
     // while the interpolation waves take the rest. In MFMA-equivalents (64 cycles): a ring iteration of a DFT wave is
     // its 32 MFMAs + ~20 per generated term (a Philox call and two Box-Muller pairs per lane), a chunk 4 per band step
     // + ~12 (operand loads, stores). The reserve is kFusedJoinSafety times the chunks the interpolation waves do in a
-    // build: C2 (~7 x 70 per build, ~48 per chunk, 63 chunks per item) never joins; C4 (~7 x 32, ~32 per chunk, 313
-    // chunks per item) joins for most of an item.
+    // build: C2 (~7 x 72 per build, ~48 per chunk: reserve 63 of its 63 chunks per item) hardly joins; C4 (~7 x 32,
+    // ~32 per chunk: reserve ~42 of 313) joins for most of an item. (The estimate is about half the measured build
+    // time on C2; the factor 1.5 was the best of 0.5 .. 5 on both, profiles/round5/r5mn_*.)
     {
       int it_max = 0, gen = 0;
       for (int32_t s = 0; s < f.n_sig; ++s) {
