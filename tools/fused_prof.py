@@ -61,7 +61,7 @@ def main():
     v = v[used]
     cyc_us = 1e-3 / args.ghz
     names = {"interp": ["loads", "mfma", "stores", "barriers", "reloads", "chunks", "stream+info"],
-             "dft": ["loads issue", "mfma", "ring sync", "grid writes", "barriers", "iterations", "draws", "first draws"]}
+             "dft": ["loads issue", "mfma", "sync/join st", "grid writes", "barr/join wide", "iterations", "draws", "joined chunks"]}
     print(f"workgroups with counters: {len(v)}")
     for role, waves in (("interp", range(0, 4)), ("dft", range(4, 8))):
         r = v[:, list(waves), :]
@@ -70,12 +70,12 @@ def main():
             col = r[:, :, i]
             if i >= r.shape[2]:
                 continue
-            if nm in ("chunks", "iterations"):
+            if nm in ("chunks", "iterations", "joined chunks"):
                 print(f"   {nm:14s} {col.mean():10.1f}   (per wave: {', '.join(f'{x:.1f}' for x in col.mean(axis=0))})")
             else:
                 print(f"   {nm:14s} {col.mean() * cyc_us:10.1f} us   (per wave: "
                       f"{', '.join(f'{x * cyc_us:.1f}' for x in col.mean(axis=0))})")
-        tot = r[:, :, :5].sum(axis=2) + r[:, :, 6] + (r[:, :, 7] if role == "dft" else 0)
+        tot = r[:, :, :5].sum(axis=2) + r[:, :, 6]
         print(f"   {'total':14s} {tot.mean() * cyc_us:10.1f} us")
     ctx.close()
 
