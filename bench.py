@@ -6,6 +6,8 @@ correlated common GWB (30 modes, log10_A = -15, gamma = 13/3); K = 320 basis col
 1024 new realizations per GPU drawn on device (Philox -> ORF mix -> synthesis), written to a
 resident [1024 x 200000] fp64 residual block in HBM. Inputs are resident before the timed region;
 nothing is copied back inside it. Weak scaling: rank g of G owns realizations (step G + g) R ...
+The step's launches: k_gen_mix (the GWB draws + HD mix) and k_grid_fused (per-pulsar draws, the grid DFTs into LDS and
+the interpolation, one persistent kernel); the roofline block names the dominant kernel as the library reports it.
 
 --config c3 (BASELINE configs[2]): the same 100-psr array with the HD GWB only (K = 60), a job of
 100,000 realizations sharded over the ranks (fakepta_amd.batch.simulate_sharded: rank g owns
@@ -79,6 +81,9 @@ def parse():
                     help="gridded path kernels on MFMA: bit 0 DFT, bit 1 interpolation (-1: library default)")
     ap.add_argument("--interp-ws", type=int, default=-1,
                     help="gridded interpolation kernel: 1 warp-specialised, 0 register-pipelined (-1: library default)")
+    ap.add_argument("--no-kernel-events", action="store_true",
+                    help="diagnostic: no per-kernel HIP events in the timed region (the roofline's launch time is then "
+                         "unmeasured; for the events' own cost)")
     ap.add_argument("--overlap", type=int, default=-1,
                     help="FPTA_OPT_OVERLAP: 1 pipelined blocks (side stream), 0 one stream (-1: library default)")
     ap.add_argument("--opt", action="append", default=[],
@@ -394,7 +399,7 @@ def main():
         for s in range(args.warmup):
             sim.synth(R, seed=args.seed, real0=(s * world + rank) * R, to_host=False)
         ctx.synchronize()
-        ctx.set_option(_capi.OPT_PROFILE, 1)
+        ctx.set_option(_capi.OPT_PROFILE, 0 if args.no_kernel_events else 1)
         ctx.reset_stats()
         comm.barrier()
         ctx.synchronize()
@@ -429,7 +434,7 @@ def main():
 
     ctx.set_option(_capi.OPT_PROFILE, 0)
     value = n_samples_total / dt
-    synth_avg_s = kernel_avg_s(ctx, _capi.K_SYNTH)
+    synth_avg_s = kernel_avg_s(ctx, _capi.K_SYNTH) or float("nan")  # nan: --no-kernel-events
     gi = ctx.batch_grid_info()
     path = gi["last_path"]
     # algorithmic bytes of one synthesis launch: 8 B per residual sample written; one launch
