@@ -98,7 +98,10 @@ struct FusedOps {
 
 }  // namespace
 
-template <int NQ, bool ODD>
+// NQ: band steps whose operands an interpolation wave holds; ODD: the first realization is odd (GEN only); GEN: some
+// grid signal draws its own coefficients (a per-pulsar member, C2). Without generated terms (C4: one mixed common
+// signal, loaded) the draws' Philox and Box-Muller code is compiled out.
+template <int NQ, bool ODD, bool GEN>
 __global__ __launch_bounds__(64 * (kFusedIW + kFusedDW), 1) void k_grid_fused(SynthArgs a, GridBand band, FusedArgs f,
                                                                              int32_t n_rb, int32_t n_items) {
   static_assert(kFusedReal == 32 && kFusedPitch == 32 && kFusedGroupModes * kFusedReal / 2 == 64 * kFusedDW,
@@ -172,6 +175,13 @@ __global__ __launch_bounds__(64 * (kFusedIW + kFusedDW), 1) void k_grid_fused(Sy
   // Every operand of a chunk's band steps comes through vector loads (vmcnt): a scalar load waits lgkmcnt(0) (scalar
   // loads return out of order), which also waits for the LDS grid reads. The chunk's table entry {pulsar, first TOA,
   // count, band rows} is a vector load too (every lane the same address), issued with the operands and read at process.
+  // lane-derived addresses from an opaque copy of the lane index, re-derived where used: hoisted out of the roles' item
+  // loops they would stay live across everything in them (the DFT waves' builds and joined chunks) and spill
+  auto lane_now = [&]() {
+    int v = lane;
+    asm volatile("" : "+v"(v));
+    return v;
+  };
   using Ops = FusedOps<NQ>;
   using OpsJ = FusedOps<(NQ < 8 ? NQ : 8)>;  // the DFT waves' joined chunks (fewer registers beside their own state)
   // operands of band steps 0 .. NS - 1 of chunk cc, at constant offsets from two addresses (steps past the chunk's
@@ -180,8 +190,9 @@ __global__ __launch_bounds__(64 * (kFusedIW + kFusedDW), 1) void k_grid_fused(Sy
     constexpr int NS = sizeof(o.row) / sizeof(o.row[0]);
     o.c = cc;
     o.ci = *(const i32x4*)(band.chunks + cc);
-    const i32x4* __restrict__ rt = (const i32x4*)(f.lrows + ((int64_t)cc * 4 + lg) * f.fq);
-    const double* __restrict__ wp = band.wd + ((int64_t)cc * band.vmax + lg) * kGridTT + 2 * lr;
+    const int ln = lane_now(), lgo = ln >> 4, lro = ln & 15;
+    const i32x4* __restrict__ rt = (const i32x4*)(f.lrows + ((int64_t)cc * 4 + lgo) * f.fq);
+    const double* __restrict__ wp = band.wd + ((int64_t)cc * band.vmax + lgo) * kGridTT + 2 * lro;
 #pragma unroll
     for (int q4 = 0; q4 < NS / 4; ++q4) {
       const i32x4 r4 = rt[q4];
@@ -193,11 +204,12 @@ __global__ __launch_bounds__(64 * (kFusedIW + kFusedDW), 1) void k_grid_fused(Sy
 #pragma unroll
     for (int q = 0; q < NS; ++q) o.b[q] = *(const dbl2*)(wp + 4 * kGridTT * q);
   };
-  const int lds_lane = 2 * lr;  // this lane's realization pair in an LDS grid row
   // chunk cur of item g: k_grid_interp_ws's MFMA steps (A = the realization pair's dbl2 of the LDS grid row, B = the
   // TOA pair's weights) and stores
   auto process = [&](const Geo& g, const auto& cur, auto& pf) {
     constexpr int NS = sizeof(cur.row) / sizeof(cur.row[0]);
+    const int ln = lane_now(), lg = ln >> 4, lr = ln & 15;
+    const int lds_lane = 2 * lr;  // this lane's realization pair in an LDS grid row
     const int ty = __builtin_amdgcn_readfirstlane(cur.ci.y), tc = __builtin_amdgcn_readfirstlane(cur.ci.z);
     const int nq = __builtin_amdgcn_readfirstlane(cur.ci.w) >> 2;
     FPTA_DCHECK(nq > 0, "k_grid_fused band steps", nq, 1 << 20);
@@ -309,11 +321,6 @@ __global__ __launch_bounds__(64 * (kFusedIW + kFusedDW), 1) void k_grid_fused(Sy
     const int64_t jts = (int64_t)jf.ntq * jf.ldq, jld4 = 4 * (int64_t)jf.ldq;
     // Lane-derived addresses are re-derived where used from an opaque copy of the lane index: hoisted out of the item
     // loop they would stay live across the joined chunks (see join) and spill
-    auto lane_now = [&]() {
-      int v = lane;
-      asm volatile("" : "+v"(v));
-      return v;
-    };
     auto jtq_now = [&]() {
       const int ln = lane_now();
       return jf.tq + (int64_t)(ln >> 4) * jf.ldq + 32 * jrc + 2 * (ln & 15);
@@ -386,7 +393,7 @@ __global__ __launch_bounds__(64 * (kFusedIW + kFusedDW), 1) void k_grid_fused(Sy
       for (int i = 0; i < kFusedTerms; ++i) {
         if (i >= fs.n_terms) continue;
         double pc[2], ps[2];
-        if (fs.term_kind[i] == 0) {
+        if (GEN && fs.term_kind[i] == 0) {
           double z[4];
           normals(fs.term_seg[i], z);
           const double amp = (m & 1) ? in.x0[i].y : in.x0[i].x;
@@ -407,7 +414,7 @@ __global__ __launch_bounds__(64 * (kFusedIW + kFusedDW), 1) void k_grid_fused(Sy
       for (int i = kFusedTerms; i < fs.n_terms; ++i) {
         const int mi = min(m, fs.term_nm[i] - 1);
         double pc[2], ps[2];
-        if (fs.term_kind[i] == 0) {
+        if (GEN && fs.term_kind[i] == 0) {
           double z[4];
           normals(fs.term_seg[i], z);
           const double amp = ld_global(fs.term_amp[i] + (int64_t)p * fs.term_nm[i] + mi);
@@ -559,31 +566,47 @@ __global__ __launch_bounds__(64 * (kFusedIW + kFusedDW), 1) void k_grid_fused(Sy
     auto join = [&](int k) {
       if (FPTA_FUSED_CUT & 6) return;
       const Geo g = geo(k);
-      while (__builtin_amdgcn_readfirstlane(ccnt[k & 1]) < g.n - f.join_reserve) {
+      auto take = [&]() {  // a ticket while more than the reserve are left, else -1
+        if (__builtin_amdgcn_readfirstlane(ccnt[k & 1]) >= g.n - f.join_reserve) return -1;
         const int t = ticket(k);
-        if (t >= g.n) break;
-        OpsJ o;
-        load(g.c0 + t, o);
-        process(g, o, pf);
+        return t < g.n ? t : -1;
+      };
+      int t = take();
+      if (t < 0) return;
+      // two operand sets in turn, the next chunk's loaded before this one's stores (as the interpolation waves)
+      OpsJ o0, o1;
+      load(g.c0 + t, o0);
+      for (;;) {
+        t = take();
+        load(t >= 0 ? g.c0 + t : o0.c, o1);
+        process(g, o0, pf);
         pf.count(7);
+        if (t < 0) return;
+        t = take();
+        load(t >= 0 ? g.c0 + t : o1.c, o0);
+        process(g, o1, pf);
+        pf.count(7);
+        if (t < 0) return;
       }
     };
-    // (one build site and one grid write per trip: the accumulators are dead from the write to the next build, so the
-    // joined chunks have the registers)
+    // (one build site and one grid write per trip, on one path: the accumulators are dead from the write to the next
+    // build, so the joined chunks have the registers)
+    auto barrier_a = [&](int k) {
+      fused_barrier();  // A(k): item k is interpolated
+      pf.lap(4);
+      if (dw == 0 && lane == 0) ccnt[k & 1] = 0;  // item k + 2's tickets (item k's are all taken)
+    };
     for (int k = -1;; ++k) {
       const bool next = item_of(k + 1) >= 0;
       if (k >= 0) join(k);
-      if (next && !(FPTA_FUSED_CUT & 1)) build(k + 1);
-      if (k >= 0) {
-        fused_barrier();  // A(k): item k is interpolated
-        pf.lap(4);
-        if (dw == 0 && lane == 0) ccnt[k & 1] = 0;  // item k + 2's tickets (item k's are all taken)
-      }
-      if (!next) {
+      if (!next) {  // the last item: no build, no grid write
+        if (k >= 0) barrier_a(k);
         fused_wait_lgkm0();
         fused_barrier();  // B(k)
         break;
       }
+      if (!(FPTA_FUSED_CUT & 1)) build(k + 1);  // build and write on one path: the accumulators die at the write
+      if (k >= 0) barrier_a(k);
       write_grid();
       pf.lap(3);
       fused_barrier();  // B(k): item k + 1's grids are written
@@ -709,11 +732,18 @@ hipError_t launch_grid_fused(hipStream_t st, const SynthArgs& a, const GridBand&
   const int64_t grid = std::min<int64_t>((items + 7) / 8 * 8, ((int64_t)n_cu + 7) / 8 * 8);
   // NQ: band steps whose operands an interpolation wave holds (a wider chunk takes them NQ at a time)
   // ODD: the first realization is odd, so no lane's realization pair is one Philox pair (the draws take two)
-  const bool odd = f.real0 & 1;
-  auto kernel = nq_max <= 8 ? (odd ? k_grid_fused<8, true> : k_grid_fused<8, false>)
-                            : (odd ? k_grid_fused<12, true> : k_grid_fused<12, false>);
-  static bool attr_set[4] = {false, false, false, false};
-  const int ki = (nq_max <= 8 ? 0 : 2) + odd;
+  // GEN: some term is drawn in the kernel
+  bool gen = false;
+  for (int s = 0; s < f.n_sig; ++s)
+    for (int i = 0; i < f.s[s].n_terms; ++i) gen = gen || f.s[s].term_kind[i] == 0;
+  const bool odd = gen && (f.real0 & 1);
+  const int ki = (nq_max <= 8 ? 0 : 3) + (gen ? 1 + odd : 0);
+  using K = void (*)(SynthArgs, GridBand, FusedArgs, int32_t, int32_t);
+  static const K kernels[6] = {k_grid_fused<8, false, false>, k_grid_fused<8, false, true>,
+                               k_grid_fused<8, true, true>,   k_grid_fused<12, false, false>,
+                               k_grid_fused<12, false, true>, k_grid_fused<12, true, true>};
+  const K kernel = kernels[ki];
+  static bool attr_set[6] = {false, false, false, false, false, false};
   if (!attr_set[ki]) {  // dynamic LDS beyond 64 KB
     hipError_t e = hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, kFusedLdsMax);
     if (e != hipSuccess) return e;
