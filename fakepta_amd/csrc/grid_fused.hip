@@ -186,11 +186,12 @@ __global__ __launch_bounds__(64 * (kFusedIW + kFusedDW), 1) void k_grid_fused(Sy
   using OpsJ = FusedOps<(NQ < 8 ? NQ : 8)>;  // the DFT waves' joined chunks (fewer registers beside their own state)
   // operands of band steps 0 .. NS - 1 of chunk cc, at constant offsets from two addresses (steps past the chunk's
   // read the next chunk's or the tables' padding rows: never used)
-  auto load = [&](int cc, auto& o) {
+  // ln: the lane index (the DFT waves pass an opaque copy, lane_now)
+  auto load = [&](int cc, auto& o, int ln) {
     constexpr int NS = sizeof(o.row) / sizeof(o.row[0]);
     o.c = cc;
     o.ci = *(const i32x4*)(band.chunks + cc);
-    const int ln = lane_now(), lgo = ln >> 4, lro = ln & 15;
+    const int lgo = ln >> 4, lro = ln & 15;
     const i32x4* __restrict__ rt = (const i32x4*)(f.lrows + ((int64_t)cc * 4 + lgo) * f.fq);
     const double* __restrict__ wp = band.wd + ((int64_t)cc * band.vmax + lgo) * kGridTT + 2 * lro;
 #pragma unroll
@@ -206,9 +207,9 @@ __global__ __launch_bounds__(64 * (kFusedIW + kFusedDW), 1) void k_grid_fused(Sy
   };
   // chunk cur of item g: k_grid_interp_ws's MFMA steps (A = the realization pair's dbl2 of the LDS grid row, B = the
   // TOA pair's weights) and stores
-  auto process = [&](const Geo& g, const auto& cur, auto& pf) {
+  auto process = [&](const Geo& g, const auto& cur, auto& pf, int ln) {
     constexpr int NS = sizeof(cur.row) / sizeof(cur.row[0]);
-    const int ln = lane_now(), lg = ln >> 4, lr = ln & 15;
+    const int lg = ln >> 4, lr = ln & 15;
     const int lds_lane = 2 * lr;  // this lane's realization pair in an LDS grid row
     const int ty = __builtin_amdgcn_readfirstlane(cur.ci.y), tc = __builtin_amdgcn_readfirstlane(cur.ci.z);
     const int nq = __builtin_amdgcn_readfirstlane(cur.ci.w) >> 2;
@@ -575,16 +576,16 @@ __global__ __launch_bounds__(64 * (kFusedIW + kFusedDW), 1) void k_grid_fused(Sy
       if (t < 0) return;
       // two operand sets in turn, the next chunk's loaded before this one's stores (as the interpolation waves)
       OpsJ o0, o1;
-      load(g.c0 + t, o0);
+      load(g.c0 + t, o0, lane_now());
       for (;;) {
         t = take();
-        load(t >= 0 ? g.c0 + t : o0.c, o1);
-        process(g, o0, pf);
+        load(t >= 0 ? g.c0 + t : o0.c, o1, lane_now());
+        process(g, o0, pf, lane_now());
         pf.count(7);
         if (t < 0) return;
         t = take();
-        load(t >= 0 ? g.c0 + t : o1.c, o0);
-        process(g, o1, pf);
+        load(t >= 0 ? g.c0 + t : o1.c, o0, lane_now());
+        process(g, o1, pf, lane_now());
         pf.count(7);
         if (t < 0) return;
       }
@@ -655,17 +656,17 @@ __global__ __launch_bounds__(64 * (kFusedIW + kFusedDW), 1) void k_grid_fused(Sy
     pf.lap(6);
     int kn;
     const int cn = next(kn);
-    load(cn >= 0 ? cn : cur.c, nxt);
+    load(cn >= 0 ? cn : cur.c, nxt, lane);
     pf.lap(0);
     pf.count(5);
-    if (!(FPTA_FUSED_CUT & 2)) process(g0, cur, pf);
+    if (!(FPTA_FUSED_CUT & 2)) process(g0, cur, pf, lane);
     kc = kn;
   };
   Ops o0, o1;  // operand sets in turn (two chunks per loop trip: no register copies but at item crossings)
   int kc;      // item of the chunk in o0 (-1: none)
   {
     const int cc = next(kc);
-    load(cc >= 0 ? cc : g0.c0, o0);
+    load(cc >= 0 ? cc : g0.c0, o0, lane);
   }
   for (;;) {
     while (kc == k) {
@@ -690,7 +691,7 @@ __global__ __launch_bounds__(64 * (kFusedIW + kFusedDW), 1) void k_grid_fused(Sy
     if (!g0.valid) break;
     if (kc < 0) {
       const int cc = next(kc);
-      load(cc >= 0 ? cc : g0.c0, o0);
+      load(cc >= 0 ? cc : g0.c0, o0, lane);
     }
   }
   pf.flush(f.prof, wave);
