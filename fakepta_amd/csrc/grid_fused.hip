@@ -744,11 +744,14 @@ hipError_t launch_grid_fused(hipStream_t st, const SynthArgs& a, const GridBand&
                                k_grid_fused<8, true, true>,   k_grid_fused<12, false, false>,
                                k_grid_fused<12, false, true>, k_grid_fused<12, true, true>};
   const K kernel = kernels[ki];
-  static bool attr_set[6] = {false, false, false, false, false, false};
-  if (!attr_set[ki]) {  // dynamic LDS beyond 64 KB
+  // dynamic LDS beyond 64 KB: set once per device and kernel (one process may drive several devices, fpta_multi_*)
+  static bool attr_set[64][6] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+  if (!attr_set[dev][ki]) {
     hipError_t e = hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, kFusedLdsMax);
     if (e != hipSuccess) return e;
-    attr_set[ki] = true;
+    attr_set[dev][ki] = true;
   }
   // unused descriptors are copies of the first: the kernel's unconditional draw loads read valid memory through them
   FusedArgs fa = f;
