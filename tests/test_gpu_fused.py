@@ -149,6 +149,49 @@ def test_fused_dft_waves_join_long_pulsars(ctx, capi, shipped, R, real0):
         ctx.set_options(shipped)
 
 
+@pytest.mark.parametrize("seed", range(12))
+def test_fused_randomized_layouts(ctx, capi, shipped, seed):
+    """Random layouts on a common span (so the fused kernel serves them): 1 to 40 pulsars of 1 to 3000 TOAs (one-TOA
+    pulsars included: items of a single short chunk), red noise of 1 to 40 modes, DM of 10 to 100, with or without a
+    common GWB, realization counts and first realizations off every tile and parity. The block equals the two-kernel
+    path's bit for bit and every sample is written (NaN-poisoned block); item queues, chunk tickets and the DFT waves'
+    join are exercised with whatever shapes come."""
+    rng = np.random.default_rng(1000 + seed)
+    P = int(rng.integers(1, 41))
+    counts = rng.integers(1, 3001, size=P)
+    counts[rng.integers(0, P)] = 1
+    offs = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
+    t0, t1 = 4.4e9, 4.4e9 + 3.15e8
+    toas = np.concatenate([np.sort(rng.uniform(t0, t1, k)) if k < 3 else
+                           np.concatenate([[t0], np.sort(rng.uniform(t0, t1, k - 2)), [t1]]) for k in counts])
+    nu = rng.choice([800.0, 1400.0, 2500.0], size=offs[-1])
+    T = t1 - t0
+    ctx.batch_set_toas(offs, toas, nu)
+    for nm, idx in ((int(rng.integers(1, 41)), 0.0), (int(rng.integers(10, 101)), 2.0)):
+        f = np.tile(np.arange(1, nm + 1) / T, (P, 1))
+        a = np.sqrt(O.powerlaw(f, rng.uniform(-14.5, -13.5, (P, 1)), 3.0) / T)
+        ctx.batch_add_signal(0, f, a, idx=idx)
+    if P >= 2 and rng.random() < 0.7:
+        nc = int(rng.integers(1, 31))
+        fc = np.arange(1, nc + 1) / T
+        v = rng.normal(size=(P, 3))
+        ctx.batch_add_signal(1, fc, np.sqrt(O.powerlaw(fc, -14.0, 13 / 3) / T),
+                             L=O.mvn_factor(O.orf_hd(v / np.linalg.norm(v, axis=1)[:, None])))
+    R, real0 = int(rng.integers(16, 701)), int(rng.integers(0, 5000))
+    try:
+        ctx.set_option(capi.OPT_SYNTH_PATH, 4)
+        ref, k0 = _run(ctx, capi, 0, 41 + seed, real0, R)
+        got, k1 = _run(ctx, capi, 1, 41 + seed, real0, R)
+        assert np.all(np.isfinite(got))
+        np.testing.assert_array_equal(ref, got)
+        print(f"layout {seed}: P {P}, {offs[-1]} TOAs, R {R}, real0 {real0}: {k1} (two-kernel {k0})")
+        if not k1.startswith("k_grid_fused"):  # a layout the fused kernel does not serve (e.g. a grid over LDS)
+            assert k1 == k0, (k0, k1)
+    finally:
+        ctx.batch_clear()
+        ctx.set_options(shipped)
+
+
 def test_fused_pipelined_blocks(ctx, capi, shipped):
     """Pipelined blocks (FPTA_OPT_OVERLAP 1) on the fused kernel: the next block's common draws go into the other
     coefficient buffer on the side stream while this block's kernel reads its own. Blocks queued back to back without a
