@@ -7,21 +7,21 @@
 // grid lives in LDS only; HBM sees the residual stores, the interpolation weights (read once per pulsar per XCD: the 32
 // items of a pulsar run side by side on one XCD) and the mixed common coefficients.
 //
-// A workgroup (one per CU) has two roles, one wave of each per SIMD:
-//  * DFT waves (kFusedDW): build item k + 1's grids while item k is interpolated. The coefficients of a grid signal are
-//    drawn in groups of 16 modes x 32 realizations (one (mode, realization pair) per lane, grid_term_coefs:
-//    k_grid_dft_gen's terms and order) into a two-slot LDS ring: while every wave's MFMAs read group g, the waves draw
-//    group g + 1 into the other slot; the DFT waves meet at an LDS counter after each group (the interpolation waves
-//    take no part). Wave d's job is the d-th 32-row chunk of the quarter ranges: k_grid_dft_gen's MFMA k-steps for both
-//    realization tiles (A = table row pairs from global memory / L2, B = the (cos, sin) pair of a realization from the
-//    ring), the accumulators kept in registers until the item boundary, then k_grid_dft_gen's butterfly writes grid rows
-//    j, H + j, H - j, nf - j into LDS.
-//  * interpolation waves (kFusedIW): the item's chunks c0 + w, c0 + w + kFusedIW, ...: per band step A = the dbl2 pair
-//    of realizations (2 lr, 2 lr + 1) of LDS row lrows[c][4 q + lg] (one ds_read_b128), B = the weight pair of TOAs
-//    (2 lr, 2 lr + 1) from global memory, four MFMAs (even / odd TOA x realization tile) as k_grid_interp_ws; the next
-//    chunk's weights are loaded before this chunk's eight 16-byte stores enter the vmcnt queue.
+// A workgroup (one per CU) has two roles, one wave of each per SIMD; items come from per-XCD ticket queues:
+//  * DFT waves (kFusedDW): build item k + 1's grids while item k is interpolated. Ring iteration g draws 16-mode group
+//    g + 1 of every grid signal (one (mode, realization pair) per lane, grid_term_coefs: k_grid_dft_gen's terms and
+//    order) into one slot of a two-slot LDS ring while the waves' MFMAs read group g from the other; the DFT waves meet
+//    at an LDS counter after each iteration (the interpolation waves take no part). Wave d's job is the d-th 32-row
+//    chunk of the quarter ranges: k_grid_dft_gen's MFMA k-steps for both realization tiles (A = table row pairs from
+//    global memory / L2, B = the (cos, sin) pair of a realization from the ring), the accumulators kept in registers
+//    until the item boundary, then k_grid_dft_gen's butterfly writes grid rows j, H + j, H - j, nf - j into LDS. Before
+//    building, they interpolate chunks of item k while enough are left (light DFTs, C4).
+//  * interpolation waves (kFusedIW): the item's chunks by LDS tickets: per band step A = the dbl2 pair of realizations
+//    (2 lr, 2 lr + 1) of LDS row lrows[c][4 q + lg] (one ds_read_b128), B = the weight pair of TOAs (2 lr, 2 lr + 1)
+//    from global memory, four MFMAs (even / odd TOA x realization tile) as k_grid_interp_ws; the next chunk's operands
+//    are loaded before this chunk's eight 16-byte stores enter the vmcnt queue.
 // Two s_barriers per item separate the roles: A (item k interpolated, item k + 1's accumulators ready), after which the
-// DFT waves overwrite the grids, and B (the new grids written).
+// DFT waves overwrite the grids, and B (the new grids written). DESIGN.md §5a.
 // Every value is made by the same operations in the same order as k_grid_dft_gen (or k_grid_dft_mfma from the merged
 // anchor columns) + k_grid_interp_ws: the block is bit-identical to theirs (tests/test_gpu_fused.py).
 #include <hip/hip_runtime.h>
