@@ -124,8 +124,8 @@ __global__ __launch_bounds__(64 * (kFusedIW + kFusedDW), 1) void k_grid_fused(Sy
     qitem[1] = qitem[0] >= 0 ? queue.fetch() : -1;
   }
   __syncthreads();
-  // item k of this workgroup (k >= -1; valid once fetched: items k + 1 and k + 2 are fetched at the start of item k's
-  // build, before the barriers that publish them to the interpolation waves)
+  // item k of this workgroup (k >= -1; -1 = none): items 0 and 1 are fetched here, item k + 2 at the start of item k's
+  // build, before the ring syncs and barriers that publish it to the other waves
   auto item_of = [&](int k) { return __builtin_amdgcn_readfirstlane(qitem[k & 3]); };
   // the launch's last workgroup to finish zeroes the queues for the next launch (every workgroup's fetches precede
   // its count)
@@ -145,9 +145,10 @@ __global__ __launch_bounds__(64 * (kFusedIW + kFusedDW), 1) void k_grid_fused(Sy
 
   // ------------------------------------------------------------------ chunks (both roles)
   // Item k's chunks are handed out by an LDS ticket counter, ccnt[k & 1]: the interpolation waves take them, and so do
-  // the DFT waves once they have built item k + 1 (a layout of light DFTs, e.g. C4's one common signal, then gets eight
-  // interpolating waves). A wave takes tickets of its grid item k and of k + 1 only; counter k & 1 is zeroed by the DFT
-  // waves between barriers A(k - 2) and B(k - 2), after item k - 2's last ticket and before item k's first.
+  // the DFT waves before they build item k + 1 while more than FusedArgs::join_reserve are left (a layout of light DFTs,
+  // e.g. C4's one common signal, then gets eight interpolating waves). A wave takes tickets of its grid item k and of
+  // k + 1 only; counter k & 1 is zeroed by the DFT waves between barriers A(k - 2) and B(k - 2), after item k - 2's last
+  // ticket and before item k's first.
   volatile int* ccnt = (volatile int*)(sync + 8);
   struct Geo {          // item k
     int p, r0, c0, n;   // pulsar, first realization, first chunk, chunks
