@@ -124,8 +124,8 @@ __global__ __launch_bounds__(64 * (kFusedIW + kFusedDW), 1) void k_grid_fused(Sy
     qitem[1] = qitem[0] >= 0 ? queue.fetch() : -1;
   }
   __syncthreads();
-  // item k of this workgroup (k >= -1; -1 = none): items 0 and 1 are fetched here, item k + 2 at the start of item k's
-  // build, before the ring syncs and barriers that publish it to the other waves
+  // item k of this workgroup (k >= -1; -1 = none): items 0 and 1 are fetched here, item k + 3 by the DFT waves' loop
+  // trip k (before item k + 1's build), ahead of the ring syncs and barriers that publish it to the other waves
   auto item_of = [&](int k) { return __builtin_amdgcn_readfirstlane(qitem[k & 3]); };
   // the launch's last workgroup to finish zeroes the queues for the next launch (every workgroup's fetches precede
   // its count)
@@ -485,7 +485,6 @@ __global__ __launch_bounds__(64 * (kFusedIW + kFusedDW), 1) void k_grid_fused(Sy
     // loads of an iteration are issued before its steps.
     int sb = 0;  // ring slot of the item's group 0
     auto build = [&](int k) {
-      if (dw == 0 && lane == 0) qitem[(k + 2) & 3] = item_of(k + 1) >= 0 ? queue.fetch() : -1;  // published by dsync
       const int item = item_of(k);
       const int p = item / n_rb, r0 = (item - p * n_rb) * kFusedReal;
       const int item1n = item_of(k + 1);
@@ -600,6 +599,9 @@ __global__ __launch_bounds__(64 * (kFusedIW + kFusedDW), 1) void k_grid_fused(Sy
     };
     for (int k = -1;; ++k) {
       const bool next = item_of(k + 1) >= 0;
+      // item k + 3 into the slot of item k - 1 (no wave reads it after barrier B(k - 1)); published to the other waves
+      // by the waits before the ring syncs and barriers that follow
+      if (dw == 0 && lane == 0) qitem[(k + 3) & 3] = item_of(k + 2) >= 0 ? queue.fetch() : -1;
       if (k >= 0) join(k);
       if (!next) {  // the last item: no build, no grid write
         if (k >= 0) barrier_a(k);
