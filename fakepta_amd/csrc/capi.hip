@@ -402,12 +402,13 @@ int run_coefficients(fpta_ctx* c, Layout& L, uint64_t seed, int64_t real0, int32
     hipStream_t si = stream_of(group_of[i]);  // side2 only for members of split_g (kind 0: no mixing below)
     if (in_fused[i] && d.kind == 0) continue;  // drawn inside its grid signal's DFT
     if (d.kind == 1 && c->gen_mix && mfma_mix && !zin && !x_out && fuse_into[i] < 0 && P <= kGenMixMaxP) {
-      KTimer kt(c, FPTA_K_MIX, st);  // draws + mixing in one kernel, into the signal's own columns
+      KTimer kt(c, FPTA_K_MIX, st, true);  // draws + mixing in one kernel, into the signal's own columns
       // 16-realization workgroups (FPTA_OPT_GEN_MIX 3: they fit in the LDS two k_grid_interp_psr workgroups leave;
       // C3 measured the same either way, profiles/round4/R5d)
       const int rb = c->gen_mix == 3 ? 16 : 32;
+      hipEvent_t e0 = kt.start_ev();
       HIPCHK(c, launch_gen_mix(st, d, (int32_t)i, P, R, R_pad, real0, k0, k1, c->coef.as<double>(), L.K,
-                               c->gen_mix == 1 ? 2 : 1, rb),
+                               c->gen_mix == 1 ? 2 : 1, rb, e0, kt.stop_ev()),
              "k_gen_mix launch");
     } else {
     {

@@ -352,17 +352,31 @@ struct KTimer {
   int which;
   hipStream_t st;
   hipEvent_t a = nullptr, b = nullptr;
-  KTimer(fpta_ctx* c_, int w, hipStream_t s = nullptr) : c(c_), which(w), st(s ? s : c_->stream) {
+  // ext: the events are handed to the launch (hipExtLaunchKernel: the kernel's own dispatch timestamps, no marker
+  // packets between the step's kernels); unused (the launch took another path) they go back to the pool untimed
+  bool ext = false, bound = false;
+  KTimer(fpta_ctx* c_, int w, hipStream_t s = nullptr, bool ext_ = false)
+      : c(c_), which(w), st(s ? s : c_->stream), ext(ext_) {
     if (c->profile) {
       a = get_event(c);
       b = get_event(c);
-      if (a) (void)hipEventRecord(a, st);
+      if (a && !ext) (void)hipEventRecord(a, st);
     }
   }
+  // the launch's start / stop events (null with profiling off)
+  hipEvent_t start_ev() {
+    bound = ext && a && b;
+    return bound ? a : nullptr;
+  }
+  hipEvent_t stop_ev() const { return bound ? b : nullptr; }
   ~KTimer() {
-    if (c->profile && a && b) {
-      (void)hipEventRecord(b, st);
+    if (!c->profile || !a || !b) return;
+    if (!ext) (void)hipEventRecord(b, st);
+    if (!ext || bound) {
       c->pending.push_back({which, a, b});
+    } else {
+      c->pool.push_back(a);
+      c->pool.push_back(b);
     }
   }
 };

@@ -237,9 +237,9 @@ constexpr int kFusedQueueWords = 9;  // 8 per-XCD item tickets + the count of fi
 #endif
 constexpr double kFusedJoinSafety = FPTA_FUSED_JOIN_SAFETY;  // FusedArgs::join_reserve over the estimated need
 // nq_max: band steps of the widest chunk (vmax / 4; the kernel holds up to 12 steps' operands and takes a wider chunk's
-// in turns); lds_bytes: grids + ring + sync word
+// in turns); lds_bytes: grids + ring + sync word; ev0 / ev1: timing events bound to the dispatch (hipExtLaunchKernel)
 hipError_t launch_grid_fused(hipStream_t st, const SynthArgs& a, const GridBand& band, const FusedArgs& f,
-                             int32_t nq_max, size_t lds_bytes);
+                             int32_t nq_max, size_t lds_bytes, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
 // Storer-wave variant: compute waves hand finished sums to storer waves through LDS; every block kind (white / ECORR
 // epilogue, partial checksums, accumulate) with R_pad a multiple of 128
 hipError_t launch_grid_interp_st(hipStream_t st, const SynthArgs& a, const GridBand& band, int32_t R_pad);
@@ -299,7 +299,8 @@ hipError_t launch_mix_mfma(hipStream_t st, const SegDesc& sd, int32_t P, int32_t
 // draw + mixing of a common signal in one kernel (kMixTiledMinP <= P <= kGenMixMaxP): writes the signal's own columns
 constexpr int kGenMixMaxP = 256;
 hipError_t launch_gen_mix(hipStream_t st, const SegDesc& sd, int32_t seg_id, int32_t P, int32_t n_real, int32_t R_pad,
-                          int64_t real0, uint32_t k0, uint32_t k1, double* coef, int32_t K, int rh = 2, int rb = 32);
+                          int64_t real0, uint32_t k0, uint32_t k1, double* coef, int32_t K, int rh = 2, int rb = 32,
+                          hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
 hipError_t launch_mix_tiled(hipStream_t st, const SegDesc& sd, int32_t P, int32_t R_pad, const double* zbuf,
                             double* coef, int32_t K, double* x_out);
 hipError_t launch_epoch_normals(hipStream_t st, int64_t n_blocks, int32_t n_real, int64_t real0, uint32_t k0,

@@ -25,6 +25,7 @@
 // Every value is made by the same operations in the same order as k_grid_dft_gen (or k_grid_dft_mfma from the merged
 // anchor columns) + k_grid_interp_ws: the block is bit-identical to theirs (tests/test_gpu_fused.py).
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <algorithm>
 
 #include "grid_device.h"
@@ -702,7 +703,7 @@ __global__ __launch_bounds__(64 * (kFusedIW + kFusedDW), 1) void k_grid_fused(Sy
 }
 
 hipError_t launch_grid_fused(hipStream_t st, const SynthArgs& a, const GridBand& band, const FusedArgs& f,
-                             int32_t nq_max, size_t lds_bytes) {
+                             int32_t nq_max, size_t lds_bytes, hipEvent_t ev0, hipEvent_t ev1) {
   if (band.n_chunks <= 0 || band.vmax < 4 || f.join_reserve < 0 || band.vmax % 4 != 0 || a.R_pad % kFusedReal != 0 || a.w_on ||
       a.accumulate || a.part || !f.lrows || !f.psr_c0 || f.n_sig <= 0 || f.n_sig > kFusedMaxSig ||
       lds_bytes > (size_t)kFusedLdsMax || nq_max <= 0 || f.ring_off < 0 || f.fq < kFusedNQ || f.fq % 4 != 0 ||
@@ -759,8 +760,8 @@ hipError_t launch_grid_fused(hipStream_t st, const SynthArgs& a, const GridBand&
   // unused descriptors are copies of the first: the kernel's unconditional draw loads read valid memory through them
   FusedArgs fa = f;
   for (int s = f.n_sig; s < kFusedMaxSig; ++s) fa.s[s] = f.s[0];
-  hipLaunchKernelGGL(kernel, dim3((unsigned)grid), dim3(64 * (kFusedIW + kFusedDW)), lds_bytes, st, a, band, fa, n_rb,
-                     (int32_t)items);
+  hipExtLaunchKernelGGL(kernel, dim3((unsigned)grid), dim3(64 * (kFusedIW + kFusedDW)), (uint32_t)lds_bytes, st, ev0, ev1,
+                        0u, a, band, fa, n_rb, (int32_t)items);
   return hipGetLastError();
 }
 

@@ -799,7 +799,14 @@ int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad, bool pipe) {
   }
   if (pipe) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_gready, 0), "grid ready wait");
   if (pipe && c->s2done_set) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_gready2, 0), "grid ready wait");
-  KTimer kt(c, FPTA_K_SYNTH);
+  // the fused launch takes the timing events itself (no marker packets around it); the diagnostic options that take
+  // another kernel for a fused layout time it with recorded events
+#ifdef FPTA_DIAG_KERNELS
+  const bool ext = fused && c->interp_ws != 4 && c->interp_ws != 5 && !c->interp_wr;
+#else
+  const bool ext = fused;
+#endif
+  KTimer kt(c, FPTA_K_SYNTH, nullptr, ext);
   GridBand band{G.chunks.as<int4>(), G.rows.as<int32_t>(), G.wd.as<double>(), gbase, G.n_chunks, G.vmax,
                 G.grid_rows, a.part ? G.pgfirst.as<int32_t>() : nullptr, a.part ? G.n_pg : G.n_chunks};
   // the warp-specialised kernel for plain blocks; with fused partial checksums its reduce-scatter temporaries take
@@ -902,7 +909,8 @@ int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad, bool pipe) {
       c->fused_q_ready = true;
     }
     f.queue = c->fused_q.as<uint32_t>();
-    HIPCHK(c, launch_grid_fused(c->stream, a, band, f, nq, G.fused_lds), "k_grid_fused launch");
+    hipEvent_t e0 = kt.start_ev();
+    HIPCHK(c, launch_grid_fused(c->stream, a, band, f, nq, G.fused_lds, e0, kt.stop_ev()), "k_grid_fused launch");
   } else if (psr) {
     kind = G.vmax <= 16 ? 6 : 7;  // launch_grid_interp_psr: NQ = 4 or 8 band steps
     HIPCHK(c,

@@ -7,6 +7,7 @@
 // Fragment maps of v_mfma_f64_16x16x4_f64 (cdna_hip_programming.md §3): A[i = l & 15][k = l >> 4],
 // B[k = l >> 4][j = l & 15], D: col = l & 15, row = (l >> 4) + 4 reg.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <algorithm>
 #include <cstdlib>
 
@@ -1499,7 +1500,8 @@ __global__ __launch_bounds__(1024) void k_gen_mix(SegDesc sd, int32_t seg_id, in
 }
 
 hipError_t launch_gen_mix(hipStream_t st, const SegDesc& sd, int32_t seg_id, int32_t P, int32_t n_real, int32_t R_pad,
-                          int64_t real0, uint32_t k0, uint32_t k1, double* coef, int32_t K, int rh, int rb) {
+                          int64_t real0, uint32_t k0, uint32_t k1, double* coef, int32_t K, int rh, int rb,
+                          hipEvent_t ev0, hipEvent_t ev1) {
   const int32_t n_pt = (P + 63) / 64;
   if (sd.kind != 1 || !sd.LT || P < 1 || P > kGenMixMaxP || R_pad % 32 != 0 || sd.lt_ld < 64 * n_pt ||
       sd.lt_rows < ((P + 7) & ~7) || sd.col0 < 0 || sd.col0 + 2 * sd.nm > K || (rh != 1 && rh != 2) ||
@@ -1509,14 +1511,14 @@ hipError_t launch_gen_mix(hipStream_t st, const SegDesc& sd, int32_t seg_id, int
   if (blocks > 0x7FFFFFFF) return hipErrorInvalidValue;
   const size_t lds = sizeof(double) * 2 * rb * (size_t)((P + 7) & ~7);
   if (rb == 16)
-    hipLaunchKernelGGL((k_gen_mix<1, 16>), dim3((unsigned)blocks), dim3(128 * n_pt), lds, st, sd, seg_id, P, n_real,
-                       R_pad, real0, k0, k1, coef, K);
+    hipExtLaunchKernelGGL((k_gen_mix<1, 16>), dim3((unsigned)blocks), dim3(128 * n_pt), (uint32_t)lds, st, ev0, ev1, 0u,
+                          sd, seg_id, P, n_real, R_pad, real0, k0, k1, coef, K);
   else if (rh == 2)
-    hipLaunchKernelGGL((k_gen_mix<2, 32>), dim3((unsigned)blocks), dim3(128 * n_pt), lds, st, sd, seg_id, P, n_real,
-                       R_pad, real0, k0, k1, coef, K);
+    hipExtLaunchKernelGGL((k_gen_mix<2, 32>), dim3((unsigned)blocks), dim3(128 * n_pt), (uint32_t)lds, st, ev0, ev1, 0u,
+                          sd, seg_id, P, n_real, R_pad, real0, k0, k1, coef, K);
   else
-    hipLaunchKernelGGL((k_gen_mix<1, 32>), dim3((unsigned)blocks), dim3(256 * n_pt), lds, st, sd, seg_id, P, n_real,
-                       R_pad, real0, k0, k1, coef, K);
+    hipExtLaunchKernelGGL((k_gen_mix<1, 32>), dim3((unsigned)blocks), dim3(256 * n_pt), (uint32_t)lds, st, ev0, ev1, 0u,
+                          sd, seg_id, P, n_real, R_pad, real0, k0, k1, coef, K);
   return hipGetLastError();
 }
 
