@@ -33,7 +33,8 @@
 namespace fpta {
 
 #ifndef FPTA_FUSED_CUT
-#define FPTA_FUSED_CUT 0  // diagnostic variant builds only (make variant DEFS=-DFPTA_FUSED_CUT=n): 1 no DFT builds, 2 no interpolation
+#define FPTA_FUSED_CUT 0  // diagnostic variant builds only (make variant DEFS=-DFPTA_FUSED_CUT=n): 1 no DFT builds, 2 no interpolation,
+                          // 8 no output stores
 #endif
 
 namespace {
@@ -255,6 +256,7 @@ __global__ __launch_bounds__(64 * (kFusedIW + kFusedDW), 1) void k_grid_fused(Sy
     // interp_store_rows' fast path from the item's first TOA: a full chunk, every realization of the item stored,
     // 16-byte aligned rows: eight 16-byte non-temporal stores from one row base
     const int64_t t0 = g.toa0 + ty;
+    if ((FPTA_FUSED_CUT & 8) && acc[0][0][0] != -1.25e300) return;  // diagnostic: no stores (the sums stay live)
     if (tc == kGridTT && g.r0 + kFusedReal <= a.n_real && ((t0 | a.ldo) & 1) == 0 && a.ldo < ((int64_t)1 << 26)) {
       const uint32_t vo = (uint32_t)(((int64_t)2 * lg * a.ldo + 2 * lr) * 8);
       const char* base = (const char*)(a.out + t0 + (int64_t)g.r0 * a.ldo);
