@@ -251,3 +251,36 @@ def test_fused_not_taken_outside_its_blocks(ctx, capi, shipped):
         ctx.batch_set_white()
         ctx.batch_clear()
         ctx.set_options(shipped)
+
+
+def test_fused_launch_timing_events(ctx, capi, shipped):
+    """With profiling on, the fused launch and k_gen_mix take their timing events as the dispatch's own start / stop
+    (hipExtLaunchKernel): one K_SYNTH and one K_MIX record per block, each a positive duration shorter than the block's
+    wall time; with profiling off, no record and the same block bit for bit."""
+    import time
+    rng = np.random.default_rng(97)
+    _c2_like(ctx, rng, P=70, n=(200, 400), unsorted=False)  # 70 pulsars: the HD mix on k_gen_mix (64 <= P <= 256)
+    try:
+        ctx.set_option(capi.OPT_SYNTH_PATH, 4)
+        ref = ctx.batch_synth(5, 0, 256)
+        assert ctx.batch_grid_info()["interp_kernel"].startswith("k_grid_fused")
+        ctx.set_option(capi.OPT_PROFILE, 1)
+        ctx.reset_stats()
+        n_blocks = 3
+        t0 = time.perf_counter()
+        for _ in range(n_blocks):
+            got = ctx.batch_synth(5, 0, 256)
+        wall_ms = (time.perf_counter() - t0) * 1e3
+        np.testing.assert_array_equal(ref, got)
+        for which in (capi.K_SYNTH, capi.K_MIX):
+            n, ms = ctx.kernel_stats(which)
+            assert n == n_blocks, (which, n)
+            assert 0.0 < ms < wall_ms, (which, ms, wall_ms)
+        ctx.set_option(capi.OPT_PROFILE, 0)
+        ctx.reset_stats()
+        np.testing.assert_array_equal(ref, ctx.batch_synth(5, 0, 256))
+        assert ctx.kernel_stats(capi.K_SYNTH)[0] == 0
+    finally:
+        ctx.set_option(capi.OPT_PROFILE, 0)
+        ctx.batch_clear()
+        ctx.set_options(shipped)
