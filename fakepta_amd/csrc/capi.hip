@@ -407,8 +407,9 @@ int run_coefficients(fpta_ctx* c, Layout& L, uint64_t seed, int64_t real0, int32
       // C3 measured the same either way, profiles/round4/R5d)
       const int rb = c->gen_mix == 3 ? 16 : 32;
       hipEvent_t e0 = kt.start_ev();
-      HIPCHK(c, launch_gen_mix(st, d, (int32_t)i, P, R, R_pad, real0, k0, k1, c->coef.as<double>(), L.K,
-                               c->gen_mix == 1 ? 2 : 1, rb, e0, kt.stop_ev()),
+      HIPCHK(c,
+             kt.checked(launch_gen_mix(st, d, (int32_t)i, P, R, R_pad, real0, k0, k1, c->coef.as<double>(), L.K,
+                                       c->gen_mix == 1 ? 2 : 1, rb, e0, kt.stop_ev())),
              "k_gen_mix launch");
     } else {
     {

@@ -369,6 +369,11 @@ struct KTimer {
     return bound ? a : nullptr;
   }
   hipEvent_t stop_ev() const { return bound ? b : nullptr; }
+  // the launch's result: a launch that failed recorded neither event, so they go back to the pool untimed
+  hipError_t checked(hipError_t e) {
+    if (e != hipSuccess) bound = false;
+    return e;
+  }
   ~KTimer() {
     if (!c->profile || !a || !b) return;
     if (!ext) (void)hipEventRecord(b, st);

@@ -910,7 +910,8 @@ int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad, bool pipe) {
     }
     f.queue = c->fused_q.as<uint32_t>();
     hipEvent_t e0 = kt.start_ev();
-    HIPCHK(c, launch_grid_fused(c->stream, a, band, f, nq, G.fused_lds, e0, kt.stop_ev()), "k_grid_fused launch");
+    HIPCHK(c, kt.checked(launch_grid_fused(c->stream, a, band, f, nq, G.fused_lds, e0, kt.stop_ev())),
+           "k_grid_fused launch");
   } else if (psr) {
     kind = G.vmax <= 16 ? 6 : 7;  // launch_grid_interp_psr: NQ = 4 or 8 band steps
     HIPCHK(c,
