@@ -120,11 +120,19 @@ def interp_kernel_name(code):
     if code <= 0:
         return None
     kind, white, part = (code - 1) >> 2, "true" if (code - 1) & 2 else "false", "true" if (code - 1) & 1 else "false"
+    if kind >= INTERP_KIND_FUSED0:  # launch_grid_fused's instance table (grid_fused.hip)
+        return FUSED_KERNELS[kind - INTERP_KIND_FUSED0] if kind - INTERP_KIND_FUSED0 < len(FUSED_KERNELS) else None
     return {0: f"k_grid_interp_mfma<{white}, {part}, 8>", 1: f"k_grid_interp_ws<{part}>",
             2: f"k_grid_interp_ws2<{part}>", 3: f"k_grid_interp_lds<{white}, {part}>",
             4: f"k_grid_interp_st<{white}, {part}>", 5: f"k_grid_interp_u<{part}>",
-            6: f"k_grid_interp_psr<{part}, 4>", 7: f"k_grid_interp_psr<{part}, 8>", 8: "k_grid_fused<8>", 9: "k_grid_fused<12>",
+            6: f"k_grid_interp_psr<{part}, 4>", 7: f"k_grid_interp_psr<{part}, 8>",
             10: "k_grid_interp_wr"}.get(kind)
+
+
+# k_grid_fused<NQ, ODD, GEN, HALF> instances in launch_grid_fused's order (capi_host.h kInterpKindFused0 + index)
+INTERP_KIND_FUSED0 = 11
+FUSED_KERNELS = tuple(f"k_grid_fused<{nq}, {odd}, {gen}, {half}>" for nq, half in ((8, "false"), (12, "false"), (8, "true"))
+                      for odd, gen in (("false", "false"), ("false", "true"), ("true", "true")))
 BUILD_DEBUG, BUILD_DIAG = 1, 2
 GATHER_AUTO, GATHER_RCCL, GATHER_HOST = 0, 1, 2
 COMM_ID_BYTES = 128

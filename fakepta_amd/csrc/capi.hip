@@ -768,7 +768,7 @@ int dense_cholesky(fpta_ctx* c, const DenseDims& d) {
 // =============================================================================================== API
 extern "C" {
 
-int fpta_version(void) { return 10000; }
+int fpta_version(void) { return FPTA_VERSION; }
 
 const char* fpta_last_error(const fpta_ctx* ctx) { return ctx ? ctx->err.c_str() : g_err.c_str(); }
 
@@ -921,7 +921,8 @@ int fpta_set_option(fpta_ctx* c, int32_t key, int64_t value) {
       c->interp_psr = value ? 1 : 0;
       return FPTA_OK;
     case FPTA_OPT_INTERP_FUSED:
-      c->interp_fused = value ? 1 : 0;
+      if (value < 0 || value > 3) return fail(c, FPTA_EINVAL, "interp_fused: 0 .. 3");
+      c->interp_fused = (int)value;
       return FPTA_OK;
     case FPTA_OPT_INTERP_WR:
 #ifndef FPTA_DIAG_KERNELS

@@ -76,6 +76,9 @@ struct GridSeg {
 };
 
 // Gridded-synthesis plan of a layout (built once per layout, reused by every batch).
+// fpta_batch_grid_info_n slot 15 (1 + 4 kind + 2 white + part): kinds 0 .. 10 the interpolation kernels
+// (_capi.interp_kernel_name), kInterpKindFused0 + i k_grid_fused instance i of launch_grid_fused's table
+constexpr int kInterpKindFused0 = 11;
 struct GridPlan {
   bool built = false;
   bool ok = false;           // usable for this layout (harmonic, <= kGridMaxSeg signals)
@@ -103,6 +106,13 @@ struct GridPlan {
   int32_t fused_fq = 0;  // band steps per (chunk, lane group) in frows
   std::vector<int32_t> fused_lrow0;
   DevBuf frows;
+  // half-chunk bands of the fused kernel (FusedHalf): hchunks {pulsar, first TOA, count, nq0 | nq1 << 16}, hrows
+  // [n_chunks][2][4][fused_hfq], hwd [2 n_chunks][fused_hvmax][16] (+ padding); fused_half_gain = the interpolation
+  // MFMAs of whole-chunk bands over those of half-chunk bands
+  bool fused_half_ok = false;
+  int32_t fused_hfq = 0, fused_hvmax = 0, fused_hnq = 0;
+  double fused_half_gain = 0.0;
+  DevBuf hchunks, hrows, hwd;
   // k_grid_interp_wr plan (GridWindow): <= 2 grid signals, each signal's band rows in a ring of kWrSlots LDS slots by
   // unwrapped row; per chunk the slot of each band row, and the rows to load: all its band rows (full) or those not in
   // the previous chunk's band (new; = full and flagged fresh when the two bands do not fit one ring window)
@@ -155,6 +165,9 @@ struct GridPlan {
     fused_ok = false;
     fused_lds = 0;
     fused_lrow0.clear();
+    fused_half_ok = false;
+    fused_hfq = fused_hvmax = fused_hnq = 0;
+    fused_half_gain = 0.0;
     members.clear();
     anchor.clear();
     last.clear();
@@ -238,7 +251,9 @@ struct fpta_ctx {
   int part_group = kPartGroup;  // fused partial checksums: consecutive chunks per partial row (FPTA_OPT_PART_GROUP)
   int interp_psr = 1;  // k_grid_interp_psr where the layout allows it (FPTA_OPT_INTERP_PSR)
   int interp_wr = 0;   // k_grid_interp_wr for plain blocks where the plan allows it (FPTA_OPT_INTERP_WR)
-  int interp_fused = 1;  // k_grid_fused for plain blocks where the plan allows it (FPTA_OPT_INTERP_FUSED)
+  int interp_fused = 1;  // k_grid_fused for plain blocks where the plan allows it (FPTA_OPT_INTERP_FUSED): 1 with
+                         // half-chunk bands where they save >= 3 % of the interpolation MFMAs, 2 whole-chunk bands, 3
+                         // half-chunk bands whenever planned
   // pipelined per-pulsar blocks read their coefficients in the interpolation (ctx stream): two coefficient buffers,
   // coef2 the other one; coef_slot = the grid-buffer index whose block owns c->coef; prev_psr: the last pipelined
   // block ran that way (its draws waited for the interpolation two blocks back, not for the whole ctx stream)

@@ -121,7 +121,7 @@ hipError_t launch_coef_merge(hipStream_t st, const CoefMerge& m, int32_t P, int3
 hipError_t launch_grid_weights(hipStream_t st, const SegDesc& sd, int64_t n_toa, const double* nu,
                                const int32_t* chunk_of, const int32_t* tt_of, const int32_t* row_of,
                                const double* d_of, int32_t w, double beta, int32_t vmax, double* wd,
-                               double* dch = nullptr, int32_t s_idx = 0, int32_t n_sig = 1);
+                               double* dch = nullptr, int32_t s_idx = 0, int32_t n_sig = 1, int32_t half = 0);
 hipError_t launch_grid_dft(hipStream_t st, GridSegs gsegs, int32_t P, const double* coef, int32_t K, int32_t R_pad);
 // the same two steps on v_mfma_f64_16x16x4_f64 (grid_mfma.hip)
 hipError_t launch_grid_dft_mfma(hipStream_t st, GridSegs gsegs, int32_t P, const double* coef, int32_t K,
@@ -218,6 +218,21 @@ struct FusedSig {
   int32_t term_col0[kDftGenTerms];
   const double* term_amp[kDftGenTerms];
 };
+// Half-chunk bands (k_grid_fused<.., HALF = true>): each 32-TOA chunk's TOAs 0..15 and 16..31 have bands of their own
+// (C2: 32 instead of 36 band rows per chunk and half, 11 % fewer interpolation MFMAs). A half's weights are [vmax_h][16
+// TOAs], laid out by pairs of band steps so that lane (TOA tt, row group j) reads steps 2 qp and 2 qp + 1 of band rows
+// 4 q + j with one 16-byte load: element (v, tt) at ((v / 8 * 4 + v % 4) * 16 + tt) * 2 + (v / 4) % 2.
+constexpr int kFusedHalfTT = 16;
+constexpr int kFusedHalfNQ = 8;  // band steps of each half whose operands an interpolation wave holds
+__host__ __device__ __forceinline__ int64_t fused_half_weight_index(int32_t v, int32_t tt) {
+  return ((int64_t)((v >> 3) * 4 + (v & 3)) * kFusedHalfTT + tt) * 2 + ((v >> 2) & 1);
+}
+struct FusedHalf {
+  const int4* chunks;    // [n_chunks] {pulsar, first TOA, count, nq0 | nq1 << 16}: band steps of each half
+  const int32_t* lrows;  // [n_chunks][2][4][fq] LDS grid row of band row 4 q + j of half h at [h][j][q]
+  const double* wd;      // [2 n_chunks][vmax][16] weights (fused_half_weight_index), + zero rows past the last
+  int32_t fq, vmax;      // band steps per (chunk, half, j) in lrows (a multiple of 4); band rows per half (mult. of 8)
+};
 struct FusedArgs {
   FusedSig s[kFusedMaxSig];
   int32_t n_sig;
@@ -230,6 +245,7 @@ struct FusedArgs {
   unsigned long long* prof;  // -DFPTA_FUSED_PROF builds only: per-wave cycle counters [gridDim][8 waves][8]; else null
   uint32_t* queue;           // [kFusedQueueWords], zero at launch; the kernel's last workgroup zeroes it again
   int32_t join_reserve;      // the DFT waves interpolate an item's chunks while more than this many are left
+  FusedHalf h;               // half-chunk bands (HALF kernels only; else zero)
 };
 constexpr int kFusedQueueWords = 9;  // 8 per-XCD item tickets + the count of finished workgroups
 #ifndef FPTA_FUSED_JOIN_SAFETY
@@ -238,8 +254,13 @@ constexpr int kFusedQueueWords = 9;  // 8 per-XCD item tickets + the count of fi
 constexpr double kFusedJoinSafety = FPTA_FUSED_JOIN_SAFETY;  // FusedArgs::join_reserve over the estimated need
 // nq_max: band steps of the widest chunk (vmax / 4; the kernel holds up to 12 steps' operands and takes a wider chunk's
 // in turns); lds_bytes: grids + ring + sync word; ev0 / ev1: timing events bound to the dispatch (hipExtLaunchKernel)
+// half: the HALF kernel on f.h (nq_max: band steps of the widest half); *kernel_out (optional): the instance launched,
+// fused_kernel_name's index
 hipError_t launch_grid_fused(hipStream_t st, const SynthArgs& a, const GridBand& band, const FusedArgs& f,
-                             int32_t nq_max, size_t lds_bytes, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
+                             int32_t nq_max, size_t lds_bytes, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr,
+                             bool half = false, int* kernel_out = nullptr);
+constexpr int kFusedKernels = 9;  // instances: {NQ 8, NQ 12} x {no draws, draws, draws from an odd realization},
+                                  // then HALF (NQ 8 per half) x the same three
 // Storer-wave variant: compute waves hand finished sums to storer waves through LDS; every block kind (white / ECORR
 // epilogue, partial checksums, accumulate) with R_pad a multiple of 128
 hipError_t launch_grid_interp_st(hipStream_t st, const SynthArgs& a, const GridBand& band, int32_t R_pad);

@@ -35,19 +35,27 @@ typedef double dbl2 __attribute__((ext_vector_type(2)));
 // signal's band offset in the chunk + the TOA's first row in that band (host plan), pitch vmax rows per chunk.
 // dch (optional, k_grid_interp_u's on-the-fly weights): {d, ch} of the TOA for signal s_idx of n_sig at
 // [(chunk * n_sig + s_idx) * kGridTT + tt].
+// half (k_grid_fused's half-chunk bands): chunk_of is a half-chunk (2 chunk + h) of <= 16 TOAs, tt < 16, and its
+// vmax x 16 weights are laid out by pairs of band steps, fused_half_weight_index: lane (tt, j) reads steps 2 qp and
+// 2 qp + 1 of its band rows 4 q + j with one 16-byte load.
 __global__ __launch_bounds__(256) void k_grid_weights(SegDesc sd, int64_t n_toa, const double* __restrict__ nu,
                                                       const int32_t* __restrict__ chunk_of,
                                                       const int32_t* __restrict__ tt_of,
                                                       const int32_t* __restrict__ row_of,
                                                       const double* __restrict__ d_of, int32_t w, double beta,
                                                       int32_t vmax, double* __restrict__ wd, dbl2* __restrict__ dch,
-                                                      int32_t s_idx, int32_t n_sig) {
+                                                      int32_t s_idx, int32_t n_sig, int32_t half) {
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (t >= n_toa) return;
   double ch = chrom_factor(sd.freqf, nu[t], sd.idx);
   if (sd.mask && !sd.mask[t]) ch = 0.0;
   const double d = d_of[t];
   const double hw = 0.5 * (double)w;
+  if (half) {
+    double* dst = wd + (int64_t)chunk_of[t] * vmax * kFusedHalfTT;
+    for (int i = 0; i < w; ++i) dst[fused_half_weight_index(row_of[t] + i, tt_of[t])] = es_weight(d, i, hw, beta, ch);
+    return;
+  }
   double* dst = wd + ((int64_t)chunk_of[t] * vmax + row_of[t]) * kGridTT + tt_of[t];
   for (int i = 0; i < w; ++i) dst[(int64_t)i * kGridTT] = es_weight(d, i, hw, beta, ch);
   if (dch) dch[((int64_t)chunk_of[t] * n_sig + s_idx) * kGridTT + tt_of[t]] = dbl2{d, ch};
@@ -126,9 +134,10 @@ __global__ __launch_bounds__(256) void k_grid_dft(GridSegs gsegs, const double* 
 hipError_t launch_grid_weights(hipStream_t st, const SegDesc& sd, int64_t n_toa, const double* nu,
                                const int32_t* chunk_of, const int32_t* tt_of, const int32_t* row_of,
                                const double* d_of, int32_t w, double beta, int32_t vmax, double* wd, double* dch,
-                               int32_t s_idx, int32_t n_sig) {
+                               int32_t s_idx, int32_t n_sig, int32_t half) {
+  if (half && (vmax % 8 != 0 || dch)) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_grid_weights, dim3((unsigned)((n_toa + 255) / 256)), dim3(256), 0, st, sd, n_toa, nu,
-                     chunk_of, tt_of, row_of, d_of, w, beta, vmax, wd, (dbl2*)dch, s_idx, n_sig);
+                     chunk_of, tt_of, row_of, d_of, w, beta, vmax, wd, (dbl2*)dch, s_idx, n_sig, half);
   return hipGetLastError();
 }
 

@@ -27,10 +27,23 @@
 #include <hip/hip_runtime.h>
 #include <hip/hip_ext.h>
 #include <algorithm>
+#include <atomic>
+#include <type_traits>
 
 #include "grid_device.h"
 
 namespace fpta {
+
+#ifndef FPTA_HALF_STORE16
+#define FPTA_HALF_STORE16 0  // HALF: 1 = lanes swap values (DPP) for 16-byte stores (measured slower than 8-byte stores)
+#endif
+#ifndef FPTA_HALF_AHEAD
+#define FPTA_HALF_AHEAD 2  // HALF: band steps (four MFMAs each, both halves) between an A operand's LDS read and its use
+#endif
+constexpr int kFusedHalfAhead = FPTA_HALF_AHEAD;
+#ifndef FPTA_HALF_PIN
+#define FPTA_HALF_PIN 0  // HALF: 1 = a scheduling barrier keeps each step's look-ahead LDS reads before its MFMAs
+#endif
 
 #ifndef FPTA_FUSED_CUT
 #define FPTA_FUSED_CUT 0  // diagnostic variant builds only (make variant DEFS=-DFPTA_FUSED_CUT=n): 1 no DFT builds, 2 no interpolation,
@@ -65,6 +78,13 @@ struct Prof {
 };
 #endif
 
+// a double from lane l ^ 1 (DPP quad_perm [1, 0, 3, 2] on both halves)
+__device__ __forceinline__ double dpp_xor1(double x) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(x), 0xB1, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(x), 0xB1, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+
 __device__ __forceinline__ void fused_barrier() { asm volatile("s_barrier" ::: "memory"); }  // no vmcnt(0) fence
 __device__ __forceinline__ void fused_wait_lgkm0() { __builtin_amdgcn_s_waitcnt(15 | (3 << 14) | (7 << 4)); }
 
@@ -97,17 +117,29 @@ struct FusedOps {
   dbl2 b[NS];   // weights of TOAs (2 lr, 2 lr + 1) at band row 4 q + lg
   int row[NS];  // LDS grid row of band row 4 q + lg
 };
+// The same with half-chunk bands (HALF): band steps 0 .. NS - 1 of each half
+template <int NS>
+struct FusedOpsH {
+  int c;
+  i32x4 ci;            // FusedHalf::chunks[c] {pulsar, first TOA, count, nq0 | nq1 << 16}
+  dbl2 b[2][NS / 2];   // [half h][step pair qp]: weights of TOA 16 h + lr at band rows 4 (2 qp) + lg, 4 (2 qp + 1) + lg
+  int row[2][NS];      // LDS grid row of band row 4 q + lg of half h
+};
 
 }  // namespace
 
-// NQ: band steps whose operands an interpolation wave holds; ODD: the first realization is odd (GEN only); GEN: some
-// grid signal draws its own coefficients (a per-pulsar member, C2). Without generated terms (C4: one mixed common
-// signal, loaded) the draws' Philox and Box-Muller code is compiled out.
-template <int NQ, bool ODD, bool GEN>
+// NQ: band steps whose operands an interpolation wave holds (HALF: per half); ODD: the first realization is odd (GEN
+// only); GEN: some grid signal draws its own coefficients (a per-pulsar member, C2). Without generated terms (C4: one
+// mixed common signal, loaded) the draws' Philox and Box-Muller code is compiled out. HALF: half-chunk bands
+// (FusedHalf): per band step of half h, A = the realization pair of the half's band row, B = the weight of TOA 16 h +
+// lr, two MFMAs (C2: 2 x 8 steps x 2 instead of 9 steps x 4 MFMAs per chunk); 8-byte stores (a lane holds TOAs lr
+// and 16 + lr of each realization).
+template <int NQ, bool ODD, bool GEN, bool HALF>
 __global__ __launch_bounds__(64 * (kFusedIW + kFusedDW), 1) void k_grid_fused(SynthArgs a, GridBand band, FusedArgs f,
                                                                              int32_t n_rb, int32_t n_items) {
   static_assert(kFusedReal == 32 && kFusedPitch == 32 && kFusedGroupModes * kFusedReal / 2 == 64 * kFusedDW,
                 "two realization tiles; one (mode, realization pair) of a 16-mode group per DFT lane");
+  static_assert(!HALF || (NQ % 4 == 0 && kGridTT == 2 * kFusedHalfTT), "half bands: whole row groups, two halves");
   // [grid rows][32] | ring [2][kFusedMaxSig][kFusedSlot] | sync word, 3 pad | item ring [4] | chunk tickets [2], 2 pad
   // (48 bytes past the ring)
   extern __shared__ __attribute__((aligned(16))) double lds[];
@@ -185,12 +217,37 @@ __global__ __launch_bounds__(64 * (kFusedIW + kFusedDW), 1) void k_grid_fused(Sy
     asm volatile("" : "+v"(v));
     return v;
   };
-  using Ops = FusedOps<NQ>;
-  using OpsJ = FusedOps<(NQ < 8 ? NQ : 8)>;  // the DFT waves' joined chunks (fewer registers beside their own state)
+  using Ops = typename std::conditional<HALF, FusedOpsH<NQ>, FusedOps<NQ>>::type;
+  // the DFT waves' joined chunks (fewer registers beside their own state)
+  using OpsJ = typename std::conditional<HALF, FusedOpsH<NQ>, FusedOps<(NQ < 8 ? NQ : 8)>>::type;
   // operands of band steps 0 .. NS - 1 of chunk cc, at constant offsets from two addresses (steps past the chunk's
   // read the next chunk's or the tables' padding rows: never used)
   // ln: the lane index (the DFT waves pass an opaque copy, lane_now)
-  auto load = [&](int cc, auto& o, int ln) {
+  auto load_half = [&](int cc, auto& o, int ln) {
+    {
+      constexpr int NS = sizeof(o.row[0]) / sizeof(o.row[0][0]);
+      o.c = cc;
+      o.ci = *(const i32x4*)(f.h.chunks + cc);
+      const int lgo = ln >> 4, lro = ln & 15;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const i32x4* __restrict__ rt = (const i32x4*)(f.h.lrows + (((int64_t)cc * 2 + h) * 4 + lgo) * f.h.fq);
+#pragma unroll
+        for (int q4 = 0; q4 < NS / 4; ++q4) {
+          const i32x4 r4 = rt[q4];
+          o.row[h][4 * q4] = r4.x;
+          o.row[h][4 * q4 + 1] = r4.y;
+          o.row[h][4 * q4 + 2] = r4.z;
+          o.row[h][4 * q4 + 3] = r4.w;
+        }
+        const double* __restrict__ wp =
+            f.h.wd + ((int64_t)cc * 2 + h) * f.h.vmax * kFusedHalfTT + (lgo * kFusedHalfTT + lro) * 2;
+#pragma unroll
+        for (int qp = 0; qp < NS / 2; ++qp) o.b[h][qp] = *(const dbl2*)(wp + qp * 8 * kFusedHalfTT);
+      }
+    }
+  };
+  auto load_full = [&](int cc, auto& o, int ln) {
     constexpr int NS = sizeof(o.row) / sizeof(o.row[0]);
     o.c = cc;
     o.ci = *(const i32x4*)(band.chunks + cc);
@@ -208,9 +265,120 @@ __global__ __launch_bounds__(64 * (kFusedIW + kFusedDW), 1) void k_grid_fused(Sy
 #pragma unroll
     for (int q = 0; q < NS; ++q) o.b[q] = *(const dbl2*)(wp + 4 * kGridTT * q);
   };
+  auto load = [&](int cc, auto& o, int ln) {
+    if constexpr (HALF)
+      load_half(cc, o, ln);
+    else
+      load_full(cc, o, ln);
+  };
   // chunk cur of item g: k_grid_interp_ws's MFMA steps (A = the realization pair's dbl2 of the LDS grid row, B = the
   // TOA pair's weights) and stores
-  auto process = [&](const Geo& g, const auto& cur, auto& pf, int ln) {
+  // HALF: the same per half h on its own band rows, TOA 16 h + lr per lane
+  auto process_half = [&](const Geo& g, const auto& cur, auto& pf, int ln) {
+    constexpr int NS = sizeof(cur.row[0]) / sizeof(cur.row[0][0]);
+    const int lg = ln >> 4, lr = ln & 15;
+    const int lds_lane = 2 * lr;
+    const int ty = __builtin_amdgcn_readfirstlane(cur.ci.y), tc = __builtin_amdgcn_readfirstlane(cur.ci.z);
+    const int nqw = __builtin_amdgcn_readfirstlane(cur.ci.w);
+    const int nq[2] = {nqw & 0xFFFF, nqw >> 16};
+    FPTA_DCHECK(nq[0] > 0, "k_grid_fused half band steps", nq[0], 1 << 20);
+    d4 acc[2][2];  // [half][realization tile]
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) acc[h][i] = d4{0.0, 0.0, 0.0, 0.0};
+    {
+      // band step q of both halves: four MFMAs back to back on four accumulators, as the whole-band kernel's steps
+      // (one half at a time left two MFMAs per basic block, with hazard nops between them). Both halves run
+      // max(nq0, nq1) steps: a half's steps past its own nq have zero weights (its weight rows up to the table's vmax
+      // are zero, its LDS rows valid repeats), so they add exactly zero. A step's A operands are read from LDS
+      // kFusedHalfAhead steps ahead (reads are unconditional).
+      constexpr int DA = kFusedHalfAhead;
+      const int nqm = min(max(nq[0], nq[1]), NS);
+      dbl2 an[2][NS];
+      auto rd = [&](int q) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) an[h][q] = *(const dbl2*)(lds + cur.row[h][q] * kFusedPitch + lds_lane);
+      };
+#pragma unroll
+      for (int q = 0; q < DA && q < NS; ++q) rd(q);
+#pragma unroll
+      for (int q = 0; q < NS; ++q) {
+        if (q < nqm) {
+          if (q + DA < NS) rd(q + DA);
+          if (FPTA_HALF_PIN) __builtin_amdgcn_sched_barrier(0);  // keep the reads ahead of this step's MFMAs
+          const double b0 = (q & 1) ? cur.b[0][q >> 1].y : cur.b[0][q >> 1].x;
+          const double b1 = (q & 1) ? cur.b[1][q >> 1].y : cur.b[1][q >> 1].x;
+          acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(an[0][q].x, b0, acc[0][0], 0, 0, 0);
+          acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(an[0][q].y, b0, acc[0][1], 0, 0, 0);
+          acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(an[1][q].x, b1, acc[1][0], 0, 0, 0);
+          acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(an[1][q].y, b1, acc[1][1], 0, 0, 0);
+        }
+      }
+    }
+    pf.lap(1);
+    // a half wider than NS steps: its further steps one at a time
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+      for (int q = NS; q < nq[h]; ++q) {
+        const int64_t hc = (int64_t)cur.c * 2 + h;
+        const int row = f.h.lrows[(hc * 4 + lg) * f.h.fq + q];
+        const double bv = f.h.wd[hc * f.h.vmax * kFusedHalfTT + fused_half_weight_index(4 * q + lg, lr)];
+        const dbl2 av = *(const dbl2*)(lds + row * kFusedPitch + lds_lane);
+        acc[h][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(av.x, bv, acc[h][0], 0, 0, 0);
+        acc[h][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(av.y, bv, acc[h][1], 0, 0, 0);
+      }
+    pf.lap(4);
+    __builtin_amdgcn_sched_barrier(0);
+    const int64_t t0 = g.toa0 + ty;
+    if ((FPTA_FUSED_CUT & 8) && acc[0][0][0] != -1.25e300) return;  // diagnostic: no stores (the sums stay live)
+    // acc[h][i][gg]: TOA 16 h + lr of realization r0 + 2 (lg + 4 gg) + i
+    if (FPTA_HALF_STORE16 && tc == kGridTT && g.r0 + kFusedReal <= a.n_real && ((t0 | a.ldo) & 1) == 0 &&
+        a.ldo < ((int64_t)1 << 26)) {
+      // a full chunk, every realization of the item, 16-byte aligned rows: lanes 2k and 2k + 1 swap TOA 16 + 2k for
+      // TOA 2k + 1 (one DPP exchange per value), so lane 2k holds TOAs 2k, 2k + 1 and lane 2k + 1 holds TOAs 16 + 2k,
+      // 17 + 2k: eight 16-byte non-temporal stores from one row base, as the whole-band kernel
+      const bool odd = lr & 1;
+      const uint32_t vo = (uint32_t)(((int64_t)2 * lg * a.ldo + (odd ? 15 + lr : lr)) * 8);
+      const char* base = (const char*)(a.out + t0 + (int64_t)g.r0 * a.ldo);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int gg = 0; gg < 4; ++gg) {
+          const double send = odd ? acc[0][i][gg] : acc[1][i][gg];
+          const double recv = dpp_xor1(send);
+          const dbl2 v = odd ? dbl2{recv, acc[1][i][gg]} : dbl2{acc[0][i][gg], recv};
+          __builtin_nontemporal_store(v, (dbl2*)((char*)base + (int64_t)(8 * gg + i) * a.ldo * 8 + vo));
+        }
+    } else if (tc == kGridTT && g.r0 + kFusedReal <= a.n_real && a.ldo < ((int64_t)1 << 26)) {
+      // a full chunk, every realization of the item: 8-byte non-temporal stores from one row base (each 16-lane row
+      // writes 128 contiguous bytes)
+      const uint32_t vo = (uint32_t)(((int64_t)2 * lg * a.ldo + lr) * 8);
+      const char* base = (const char*)(a.out + t0 + (int64_t)g.r0 * a.ldo);
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int gg = 0; gg < 4; ++gg)
+            __builtin_nontemporal_store(acc[h][i][gg],
+                                        (double*)((char*)base + ((int64_t)(8 * gg + i) * a.ldo + 16 * h) * 8 + vo));
+    } else {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        if (16 * h + lr >= tc) continue;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int gg = 0; gg < 4; ++gg) {
+            const int r = g.r0 + 2 * (lg + 4 * gg) + i;
+            if (r < a.n_real) a.out[t0 + 16 * h + lr + (int64_t)r * a.ldo] = acc[h][i][gg];
+          }
+      }
+    }
+    pf.lap(2);
+  };
+  auto process_full = [&](const Geo& g, const auto& cur, auto& pf, int ln) {
     constexpr int NS = sizeof(cur.row) / sizeof(cur.row[0]);
     const int lg = ln >> 4, lr = ln & 15;
     const int lds_lane = 2 * lr;  // this lane's realization pair in an LDS grid row
@@ -257,7 +425,8 @@ __global__ __launch_bounds__(64 * (kFusedIW + kFusedDW), 1) void k_grid_fused(Sy
     // 16-byte aligned rows: eight 16-byte non-temporal stores from one row base
     const int64_t t0 = g.toa0 + ty;
     if ((FPTA_FUSED_CUT & 8) && acc[0][0][0] != -1.25e300) return;  // diagnostic: no stores (the sums stay live)
-    if (tc == kGridTT && g.r0 + kFusedReal <= a.n_real && ((t0 | a.ldo) & 1) == 0 && a.ldo < ((int64_t)1 << 26)) {
+    if (FPTA_HALF_STORE16 && tc == kGridTT && g.r0 + kFusedReal <= a.n_real && ((t0 | a.ldo) & 1) == 0 &&
+        a.ldo < ((int64_t)1 << 26)) {
       const uint32_t vo = (uint32_t)(((int64_t)2 * lg * a.ldo + 2 * lr) * 8);
       const char* base = (const char*)(a.out + t0 + (int64_t)g.r0 * a.ldo);
 #pragma unroll
@@ -277,6 +446,12 @@ __global__ __launch_bounds__(64 * (kFusedIW + kFusedDW), 1) void k_grid_fused(Sy
       interp_store_rows<2>(a, a.out, t, acc);
     }
     pf.lap(2);
+  };
+  auto process = [&](const Geo& g, const auto& cur, auto& pf, int ln) {
+    if constexpr (HALF)
+      process_half(g, cur, pf, ln);
+    else
+      process_full(g, cur, pf, ln);
   };
 
   if (wave >= kFusedIW) {
@@ -705,11 +880,17 @@ __global__ __launch_bounds__(64 * (kFusedIW + kFusedDW), 1) void k_grid_fused(Sy
 }
 
 hipError_t launch_grid_fused(hipStream_t st, const SynthArgs& a, const GridBand& band, const FusedArgs& f,
-                             int32_t nq_max, size_t lds_bytes, hipEvent_t ev0, hipEvent_t ev1) {
+                             int32_t nq_max, size_t lds_bytes, hipEvent_t ev0, hipEvent_t ev1, bool half,
+                             int* kernel_out) {
   if (band.n_chunks <= 0 || band.vmax < 4 || f.join_reserve < 0 || band.vmax % 4 != 0 || a.R_pad % kFusedReal != 0 || a.w_on ||
       a.accumulate || a.part || !f.lrows || !f.psr_c0 || f.n_sig <= 0 || f.n_sig > kFusedMaxSig ||
       lds_bytes > (size_t)kFusedLdsMax || nq_max <= 0 || f.ring_off < 0 || f.fq < kFusedNQ || f.fq % 4 != 0 ||
       !f.queue || (size_t)(f.ring_off + 2 * kFusedMaxSig * kFusedSlot) * sizeof(double) + 48 > lds_bytes)
+    return hipErrorInvalidValue;
+  // half-chunk bands: the kernel holds kFusedHalfNQ steps of each half (a wider half takes the rest one at a time) and
+  // loads that many unconditionally (lrows entries, weight rows: the tables are padded past the last half)
+  if (half && (!f.h.chunks || !f.h.lrows || !f.h.wd || f.h.fq < kFusedHalfNQ || f.h.fq % 4 != 0 || f.h.vmax < 8 ||
+               f.h.vmax % 8 != 0))
     return hipErrorInvalidValue;
   int jobs = 0;
   for (int s = 0; s < f.n_sig; ++s) {
@@ -728,12 +909,16 @@ hipError_t launch_grid_fused(hipStream_t st, const SynthArgs& a, const GridBand&
   const int32_t n_rb = a.R_pad / kFusedReal;
   const int64_t items = (int64_t)a.P * n_rb;
   if (items > 0x7FFFFFFF || items <= 0) return hipErrorInvalidValue;
-  static int n_cu = 0;
-  if (!n_cu) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0)
-      n_cu = 256;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+  // per device (one process may drive several devices from several threads, fpta_multi_*): its CU count, and whether
+  // each instance's dynamic LDS limit is raised past 64 KB
+  static std::atomic<int> n_cus[64];
+  static std::atomic<bool> attr_set[64][kFusedKernels];
+  int n_cu = n_cus[dev].load(std::memory_order_relaxed);
+  if (n_cu <= 0) {
+    if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0) n_cu = 256;
+    n_cus[dev].store(n_cu, std::memory_order_relaxed);
   }
   // persistent: one workgroup per CU (the grids take most of the LDS)
   const int64_t grid = std::min<int64_t>((items + 7) / 8 * 8, ((int64_t)n_cu + 7) / 8 * 8);
@@ -744,27 +929,31 @@ hipError_t launch_grid_fused(hipStream_t st, const SynthArgs& a, const GridBand&
   for (int s = 0; s < f.n_sig; ++s)
     for (int i = 0; i < f.s[s].n_terms; ++i) gen = gen || f.s[s].term_kind[i] == 0;
   const bool odd = gen && (f.real0 & 1);
-  const int ki = (nq_max <= 8 ? 0 : 3) + (gen ? 1 + odd : 0);
+  const int ki = half ? 6 + (gen ? 1 + odd : 0) : (nq_max <= 8 ? 0 : 3) + (gen ? 1 + odd : 0);
   using K = void (*)(SynthArgs, GridBand, FusedArgs, int32_t, int32_t);
-  static const K kernels[6] = {k_grid_fused<8, false, false>, k_grid_fused<8, false, true>,
-                               k_grid_fused<8, true, true>,   k_grid_fused<12, false, false>,
-                               k_grid_fused<12, false, true>, k_grid_fused<12, true, true>};
+  static const K kernels[kFusedKernels] = {
+      k_grid_fused<8, false, false, false>,  k_grid_fused<8, false, true, false>,  k_grid_fused<8, true, true, false>,
+      k_grid_fused<12, false, false, false>, k_grid_fused<12, false, true, false>, k_grid_fused<12, true, true, false>,
+      k_grid_fused<kFusedHalfNQ, false, false, true>, k_grid_fused<kFusedHalfNQ, false, true, true>,
+      k_grid_fused<kFusedHalfNQ, true, true, true>};
   const K kernel = kernels[ki];
-  // dynamic LDS beyond 64 KB: set once per device and kernel (one process may drive several devices, fpta_multi_*)
-  static bool attr_set[64][6] = {};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return hipErrorInvalidDevice;
-  if (!attr_set[dev][ki]) {
+  if (!attr_set[dev][ki].load(std::memory_order_acquire)) {
     hipError_t e = hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, kFusedLdsMax);
     if (e != hipSuccess) return e;
-    attr_set[dev][ki] = true;
+    attr_set[dev][ki].store(true, std::memory_order_release);
   }
   // unused descriptors are copies of the first: the kernel's unconditional draw loads read valid memory through them
   FusedArgs fa = f;
   for (int s = f.n_sig; s < kFusedMaxSig; ++s) fa.s[s] = f.s[0];
-  hipExtLaunchKernelGGL(kernel, dim3((unsigned)grid), dim3(64 * (kFusedIW + kFusedDW)), (uint32_t)lds_bytes, st, ev0, ev1,
-                        0u, a, band, fa, n_rb, (int32_t)items);
-  return hipGetLastError();
+  (void)hipGetLastError();  // a stale error of an earlier call must not make this launch look failed
+  int32_t n_rb_arg = n_rb, items_arg = (int32_t)items;
+  void* args[] = {(void*)&a, (void*)&band, (void*)&fa, (void*)&n_rb_arg, (void*)&items_arg};
+  // the launch's own status (hipExtLaunchKernelGGL returns none, and hipGetLastError after it could report a stale
+  // error while the dispatch still holds the events)
+  const hipError_t e = hipExtLaunchKernel((const void*)kernel, dim3((unsigned)grid),
+                                          dim3(64 * (kFusedIW + kFusedDW)), args, lds_bytes, st, ev0, ev1, 0);
+  if (e == hipSuccess && kernel_out) *kernel_out = ki;
+  return e;
 }
 
 }  // namespace fpta

@@ -590,6 +590,100 @@ int grid_build(fpta_ctx* c, Layout& L) {
       G.fused_lds = lds;
     }
     G.fused_ok = ok;
+    // Half-chunk bands (FusedHalf): TOAs 0..15 and 16..31 of each chunk get bands of their own (a 32-TOA chunk's band
+    // is w + the cells its 32 TOAs span; a half's, w + the cells of 16). Per half the signals' bands back to back,
+    // padded to whole band steps; the weights by the half-band layout of k_grid_weights.
+    if (ok) {
+      std::vector<int4> hch(n_chunks);
+      std::vector<int32_t> hv((size_t)2 * n_chunks, 0);                    // band rows of each half (padded)
+      std::vector<int32_t> hrow_of(N), hchunk_of(N), htt_of(N);            // per TOA (filled per signal below)
+      std::vector<std::vector<int64_t>> hlo(n_seg, std::vector<int64_t>((size_t)2 * n_chunks, 0));
+      std::vector<std::vector<int32_t>> hvoff(n_seg, std::vector<int32_t>((size_t)2 * n_chunks, 0));
+      std::vector<std::vector<int32_t>> hn(n_seg, std::vector<int32_t>((size_t)2 * n_chunks, 0));
+      double steps_full = 0.0, steps_half = 0.0;
+      for (int32_t ci = 0; ci < n_chunks; ++ci) {
+        const int64_t a0 = L.h_offs[chunks[ci].x] + chunks[ci].y, a1 = a0 + chunks[ci].z;
+        int32_t nqh[2] = {0, 0};
+        for (int32_t h = 0; h < 2; ++h) {
+          const int64_t b0 = a0 + kFusedHalfTT * h, b1 = std::min(a1, b0 + kFusedHalfTT);
+          if (b0 >= b1) continue;
+          int32_t v = 0;
+          for (int32_t s = 0; s < n_seg; ++s) {
+            int64_t lo1 = INT64_MAX, hi1 = INT64_MIN;
+            for (int64_t u = b0; u < b1; ++u) {
+              const int64_t j = J[s][u] + band_lo[s][ci];  // unwrapped first row of the TOA
+              lo1 = std::min(lo1, j);
+              hi1 = std::max(hi1, j);
+            }
+            const size_t hc = (size_t)2 * ci + h;
+            hlo[s][hc] = lo1;
+            hvoff[s][hc] = v;
+            hn[s][hc] = (int32_t)(hi1 - lo1) + ws[s];
+            v += hn[s][hc];
+          }
+          hv[(size_t)2 * ci + h] = (v + 3) & ~3;
+          nqh[h] = hv[(size_t)2 * ci + h] / 4;
+          for (int64_t u = b0; u < b1; ++u) {
+            hchunk_of[u] = 2 * ci + h;
+            htt_of[u] = (int32_t)(u - b0);
+          }
+        }
+        hch[ci] = make_int4(chunks[ci].x, chunks[ci].y, chunks[ci].z, nqh[0] | (nqh[1] << 16));
+        steps_full += 4.0 * (chunks[ci].w / 4);
+        steps_half += 2.0 * (nqh[0] + nqh[1]);
+      }
+      int32_t hvmax = 8;
+      for (int32_t v : hv) hvmax = std::max(hvmax, (v + 7) & ~7);
+      const int32_t hfq = std::max(kFusedHalfNQ, (hvmax / 4 + 3) & ~3);
+      std::vector<int32_t> hrt((size_t)n_chunks * 2 * 4 * hfq);
+      for (int32_t ci = 0; ci < n_chunks; ++ci)
+        for (int32_t h = 0; h < 2; ++h) {
+          const size_t hc = (size_t)2 * ci + h;
+          std::vector<int32_t> band_row(std::max(hv[hc], 1), G.fused_lrow0[0]);
+          int32_t v = 0;
+          for (int32_t s = 0; s < n_seg; ++s)
+            for (int32_t i = 0; i < hn[s][hc]; ++i)
+              band_row[v++] = G.fused_lrow0[s] + (int32_t)(((hlo[s][hc] + i) % nf[s] + nf[s]) % nf[s]);
+          for (; v < (int32_t)band_row.size(); ++v) band_row[v] = band_row[0];
+          int32_t* r = hrt.data() + hc * 4 * hfq;
+          for (int32_t j = 0; j < 4; ++j)
+            for (int32_t q = 0; q < hfq; ++q)
+              r[j * hfq + q] = 4 * q + j < hv[hc] ? band_row[4 * q + j] : band_row[0];
+        }
+      if ((rc = upload(c, G.hchunks, hch.data(), sizeof(int4) * hch.size(), "fused half chunks")) ||
+          (rc = upload(c, G.hrows, hrt.data(), sizeof(int32_t) * hrt.size(), "fused half rows")))
+        return rc;
+      // + the rows the kernel's unconditional loads may read past the last half (kFusedHalfNQ steps)
+      const size_t hbytes = sizeof(double) * ((size_t)2 * n_chunks * hvmax + 4 * kFusedHalfNQ) * kFusedHalfTT;
+      HIPCHK(c, G.hwd.ensure(hbytes), "half weights alloc");
+      HIPCHK(c, hipMemsetAsync(G.hwd.p, 0, hbytes, c->stream), "half weights memset");
+      if ((rc = upload(c, d_chunk_of, hchunk_of.data(), sizeof(int32_t) * N, "half chunk_of")) ||
+          (rc = upload(c, d_tt_of, htt_of.data(), sizeof(int32_t) * N, "half tt_of")))
+        return rc;
+      for (int32_t s = 0; s < n_seg; ++s) {
+        const SegDesc& d = L.segs[G.anchor[s]]->d;
+        for (int64_t t = 0; t < N; ++t) {
+          const size_t hc = (size_t)hchunk_of[t];
+          hrow_of[t] = (int32_t)(J[s][t] + band_lo[s][hc / 2] - hlo[s][hc]) + hvoff[s][hc];
+        }
+        if ((rc = upload(c, d_row, hrow_of.data(), sizeof(int32_t) * N, "half rows")) ||
+            (rc = upload(c, d_d, D[s].data(), sizeof(double) * N, "grid offsets")))
+          return rc;
+        HIPCHK(c,
+               launch_grid_weights(c->stream, d, N, L.nu.as<double>(), d_chunk_of.as<int32_t>(), d_tt_of.as<int32_t>(),
+                                   d_row.as<int32_t>(), d_d.as<double>(), ws[s], betas[s], hvmax, G.hwd.as<double>(),
+                                   nullptr, s, n_seg, 1),
+               "k_grid_weights (half bands) launch");
+        HIPCHK(c, hipStreamSynchronize(c->stream), "half weights sync");  // d_row / d_d are reused
+      }
+      int32_t hnq = 1;
+      for (int32_t v : hv) hnq = std::max(hnq, v / 4);
+      G.fused_hfq = hfq;
+      G.fused_hvmax = hvmax;
+      G.fused_hnq = hnq;
+      G.fused_half_gain = steps_half > 0.0 ? steps_full / steps_half : 0.0;
+      G.fused_half_ok = true;
+    }
   }
   G.ok = true;
   return FPTA_OK;
@@ -838,9 +932,11 @@ int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad, bool pipe) {
     HIPCHK(c, launch_grid_interp_wr(c->stream, a, band, wrp, R_pad), "k_grid_interp_wr launch");
 #endif
   } else if (fused) {
-    const int32_t nq = G.vmax / 4;
-    kind = nq <= 8 ? 8 : 9;  // launch_grid_fused: NQ = 8 or 12 band steps at a time
+    // half-chunk bands (FPTA_OPT_INTERP_FUSED 1: where they save >= 3 % of the interpolation MFMAs; 3: always)
+    const bool half = G.fused_half_ok && (c->interp_fused == 3 || (c->interp_fused == 1 && G.fused_half_gain >= 1.03));
+    const int32_t nq = half ? G.fused_hnq : G.vmax / 4;
     FusedArgs f{};
+    if (half) f.h = FusedHalf{G.hchunks.as<int4>(), G.hrows.as<int32_t>(), G.hwd.as<double>(), G.fused_hfq, G.fused_hvmax};
     f.n_sig = (int32_t)G.segs.size();
     for (int32_t s = 0; s < f.n_sig; ++s) {
       const GridSeg* gs = G.segs[s];
@@ -903,15 +999,23 @@ int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad, bool pipe) {
     HIPCHK(c, hipMemsetAsync(c->dbg_a.p, 0, sizeof(unsigned long long) * 8 * 8 * 4096, c->stream), "profile memset");
     f.prof = c->dbg_a.as<unsigned long long>();
 #endif
-    if (!c->fused_q_ready) {  // zeroed once: every launch leaves it zero (its last workgroup resets it)
+    // The item queues are zeroed once: every launch leaves them zero (its last workgroup resets them), which holds
+    // because fused launches only go on the context stream, one after another. The debug build re-zeroes them before
+    // every launch, so a launch that did not complete cannot make the next one skip items unnoticed.
+#ifdef FPTA_DEBUG
+    c->fused_q_ready = false;
+#endif
+    if (!c->fused_q_ready) {
       HIPCHK(c, c->fused_q.ensure(sizeof(uint32_t) * kFusedQueueWords), "fused queue alloc");
       HIPCHK(c, hipMemsetAsync(c->fused_q.p, 0, sizeof(uint32_t) * kFusedQueueWords, c->stream), "fused queue memset");
       c->fused_q_ready = true;
     }
     f.queue = c->fused_q.as<uint32_t>();
     hipEvent_t e0 = kt.start_ev();
-    HIPCHK(c, kt.checked(launch_grid_fused(c->stream, a, band, f, nq, G.fused_lds, e0, kt.stop_ev())),
+    int ki = 0;
+    HIPCHK(c, kt.checked(launch_grid_fused(c->stream, a, band, f, nq, G.fused_lds, e0, kt.stop_ev(), half, &ki)),
            "k_grid_fused launch");
+    kind = kInterpKindFused0 + ki;  // fpta_batch_grid_info_n slot 15: the instance launched
   } else if (psr) {
     kind = G.vmax <= 16 ? 6 : 7;  // launch_grid_interp_psr: NQ = 4 or 8 band steps
     HIPCHK(c,

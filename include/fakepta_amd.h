@@ -39,6 +39,12 @@ extern "C" {
 typedef struct fpta_ctx fpta_ctx;
 
 /* ------------------------------------------------------------------ lifetime */
+/* 10000 * ABI major + 100 * behaviour revision (FPTA_VERSION): the major changes only if an entry point's signature
+ * or buffer size changes; the revision when a call's accepted values or reported codes change. 10100 (round 6):
+ * FPTA_OPT_INTERP_WS 0/2/3, DFT_GEN 0, GEN_MIX 0/1/3, ASYNC_SUMS 1 and SIDE_SPLIT 0/1 are refused (FPTA_EINVAL) by
+ * the product library (variant builds accept them); FPTA_OPT_INTERP_FUSED takes 0 .. 3; fpta_batch_grid_info_n slot
+ * 15 names each k_grid_fused instance (kinds 11 .. 19) instead of kinds 8 / 9. */
+#define FPTA_VERSION 10100
 int fpta_version(void);
 int fpta_create(int device, fpta_ctx** out);
 int fpta_destroy(fpta_ctx* ctx);
@@ -369,8 +375,13 @@ int fpta_comm_gather(fpta_comm* comm, const double* send, int64_t count, double*
                                      quarter-range rows and 2 grid signals (C2: 129 KB of grids): 1 (default)
                                      k_grid_fused (persistent workgroups, one per CU: 4 DFT waves draw and transform
                                      the next pulsar x 32 realizations into LDS while 4 interpolation waves read the
-                                     current one: no grid buffer, no DFT launch); 0 the DFT + interpolation kernels.
-                                     Results are identical. A layout k_grid_interp_psr serves keeps it. */
+                                     current one: no grid buffer, no DFT launch), its interpolation on half-chunk
+                                     bands (TOAs 0..15 and 16..31 of a chunk each with their own band rows) where
+                                     that saves at least 3 % of the interpolation's MFMAs (C2: 11 %); 2 k_grid_fused
+                                     on whole-chunk bands only; 3 half-chunk bands whenever the plan has them; 0 the
+                                     DFT + interpolation kernels. Whole-chunk bands are bit-identical to the DFT +
+                                     interpolation kernels; half-chunk bands group the band rows differently (sums
+                                     agree to rounding). A layout k_grid_interp_psr serves keeps it. */
 int fpta_set_option(fpta_ctx* ctx, int32_t key, int64_t value);
 /* Current value of option `key` (same keys as fpta_set_option). */
 int fpta_get_option(fpta_ctx* ctx, int32_t key, int64_t* value);

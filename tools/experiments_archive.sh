@@ -1,9 +1,11 @@
 #!/bin/bash
 # Archive of the one-off GPU experiment command lines of rounds 2-4 (formerly tools/gpu_<name>.sh, one file each).
 # Each is a function named after its old file (bodies unindented: some hold here-documents); the records they
-# produced are under profiles/ (the tags in the bodies). Kept for provenance only: new A/B runs go through
+# produced are under profiles/ (the tags in the bodies). Kept for provenance only, NOT runnable: several bodies call
+# the tools/gpu_*.sh files this archive replaced (gpu_c3_trace.sh, gpu_c3_trace3.sh, gpu_c3_batch.sh, gpu_full.sh,
+# ...), and variant libraries (build/diag/lib_*.so) of revisions long gone. New A/B runs go through
 # tools/gpu_ab_cfg.sh configurations.
-#   bash tools/experiments_archive.sh <name>   # e.g. psr3, c3_ab2 (on the GPU box, from $GRAFT_REPO_ROOT)
+#   bash tools/experiments_archive.sh <name>   # prints the archived body of exp_<name> (e.g. psr3, c3_ab2)
 
 exp_c2_trace() {
 # Kernel trace of the C2 bench (short run, no CPU legs, no sub-records) and its per-step timeline.
@@ -461,6 +463,6 @@ cat ${o}_pmc_dispatch.txt
 }
 
 fn="exp_$1"
-shift
 if ! declare -F "$fn" > /dev/null; then echo "unknown experiment: $fn" >&2; exit 2; fi
-"$fn" "$@"
+echo "# archived experiment (provenance only, not runnable: it may call removed scripts):" >&2
+declare -f "$fn"
