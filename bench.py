@@ -467,12 +467,12 @@ def main():
                     "traffic_over_algorithmic": (traffic / out_bytes) if traffic else None,
                     "traffic_source": traffic_src,
                     "implementation_bytes_per_launch": impl_bytes,
-                    "interp_fp64_TFLOPs": 2.0 * gi["fma_interp"] * R_pad / synth_avg_s / 1e12,
+                    "interp_fp64_TFLOPs": 2.0 * gi["fma_interp_run"] * R_pad / synth_avg_s / 1e12,
                     # k_grid_fused also runs the block's DFTs on the same fp64 pipe (one launch, no DFT kernel): its
                     # interpolation + DFT MFMA FLOPs against the 78.6 TF FP64 peak beside the HBM fraction
-                    "fp64_pipe": ({"flops_per_launch": 2.0 * (gi["fma_interp"] + gi["fma_dft"]) * R_pad,
-                                   "TFLOPs": 2.0 * (gi["fma_interp"] + gi["fma_dft"]) * R_pad / synth_avg_s / 1e12,
-                                   "frac": 2.0 * (gi["fma_interp"] + gi["fma_dft"]) * R_pad / synth_avg_s / 1e12
+                    "fp64_pipe": ({"flops_per_launch": 2.0 * (gi["fma_interp_run"] + gi["fma_dft"]) * R_pad,
+                                   "TFLOPs": 2.0 * (gi["fma_interp_run"] + gi["fma_dft"]) * R_pad / synth_avg_s / 1e12,
+                                   "frac": 2.0 * (gi["fma_interp_run"] + gi["fma_dft"]) * R_pad / synth_avg_s / 1e12
                                    / FP64_PEAK_TFLOPS} if fused else None),
                     "grid": {"width": gi["width"], "sigma": gi["sigma"], "err_bound": gi["err_bound"],
                              "signals": gi["signals"], "grid_signals": gi["grid_signals"],

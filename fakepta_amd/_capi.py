@@ -106,11 +106,11 @@ OPT_SYNTH_PATH, OPT_MFMA_MIN_REAL, OPT_PROFILE, OPT_ANCHOR, OPT_VALU_VARIANT, OP
 OPT_GRID_WIDTH, OPT_GRID_SIGMA, OPT_GRID_MFMA, OPT_FUSE_CHECKSUMS = 7, 8, 9, 10
 OPT_MIX_MFMA, OPT_OVERLAP, OPT_INTERP_LDS, OPT_GRID_COALESCE, OPT_INTERP_WS, OPT_SIDE_SPLIT = 11, 12, 13, 14, 15, 16
 OPT_DFT_GEN, OPT_GEN_MIX, OPT_ASYNC_SUMS, OPT_PART_GROUP, OPT_INTERP_PSR, OPT_INTERP_WR = 17, 18, 19, 20, 21, 22
-OPT_INTERP_FUSED = 23
+OPT_INTERP_FUSED, OPT_FUSED_WHITE = 23, 24
 OPTIONS = (OPT_SYNTH_PATH, OPT_MFMA_MIN_REAL, OPT_PROFILE, OPT_ANCHOR, OPT_VALU_VARIANT, OPT_FUSE_WHITE,
            OPT_GRID_WIDTH, OPT_GRID_SIGMA, OPT_GRID_MFMA, OPT_FUSE_CHECKSUMS, OPT_MIX_MFMA, OPT_OVERLAP,
            OPT_INTERP_LDS, OPT_GRID_COALESCE, OPT_INTERP_WS, OPT_SIDE_SPLIT, OPT_DFT_GEN, OPT_GEN_MIX,
-           OPT_ASYNC_SUMS, OPT_PART_GROUP, OPT_INTERP_PSR, OPT_INTERP_WR, OPT_INTERP_FUSED)
+           OPT_ASYNC_SUMS, OPT_PART_GROUP, OPT_INTERP_PSR, OPT_INTERP_WR, OPT_INTERP_FUSED, OPT_FUSED_WHITE)
 K_GEN, K_MIX, K_SYNTH, K_WHITE, K_DENSE, K_GRID = 0, 1, 2, 3, 4, 5
 
 
@@ -120,8 +120,9 @@ def interp_kernel_name(code):
     if code <= 0:
         return None
     kind, white, part = (code - 1) >> 2, "true" if (code - 1) & 2 else "false", "true" if (code - 1) & 1 else "false"
-    if kind >= INTERP_KIND_FUSED0:  # launch_grid_fused's instance table (grid_fused.hip)
-        return FUSED_KERNELS[kind - INTERP_KIND_FUSED0] if kind - INTERP_KIND_FUSED0 < len(FUSED_KERNELS) else None
+    if kind >= INTERP_KIND_FUSED0:  # launch_grid_fused's / launch_grid_fused_w's instance tables
+        i = kind - INTERP_KIND_FUSED0
+        return FUSED_KERNELS[i] if i < len(FUSED_KERNELS) else None
     return {0: f"k_grid_interp_mfma<{white}, {part}, 8>", 1: f"k_grid_interp_ws<{part}>",
             2: f"k_grid_interp_ws2<{part}>", 3: f"k_grid_interp_lds<{white}, {part}>",
             4: f"k_grid_interp_st<{white}, {part}>", 5: f"k_grid_interp_u<{part}>",
@@ -132,7 +133,8 @@ def interp_kernel_name(code):
 # k_grid_fused<NQ, ODD, GEN, HALF> instances in launch_grid_fused's order (capi_host.h kInterpKindFused0 + index)
 INTERP_KIND_FUSED0 = 11
 FUSED_KERNELS = tuple(f"k_grid_fused<{nq}, {odd}, {gen}, {half}>" for nq, half in ((8, "false"), (12, "false"), (8, "true"))
-                      for odd, gen in (("false", "false"), ("false", "true"), ("true", "true")))
+                      for odd, gen in (("false", "false"), ("false", "true"), ("true", "true"))) + \
+    ("k_grid_fused_w<16, false>", "k_grid_fused_w<16, true>")
 BUILD_DEBUG, BUILD_DIAG = 1, 2
 GATHER_AUTO, GATHER_RCCL, GATHER_HOST = 0, 1, 2
 COMM_ID_BYTES = 128
@@ -342,10 +344,12 @@ class Context:
     def batch_grid_info(self):
         """Gridded-path plan figures, the path of the last batch and why it was not the gridded path
         (fpta_batch_grid_info_n, fpta_batch_path_reason)."""
-        g = np.zeros(16, dtype=np.float64)
+        g = np.zeros(17, dtype=np.float64)
         self._check(_lib.fpta_batch_grid_info_n(self._h, _ptr(g), len(g)), "fpta_batch_grid_info_n")
         keys = ("last_path", "ok", "n_chunks", "fma_dft", "fma_interp", "fma_direct", "grid_vals", "weight_bytes",
                 "grid_mfma", "err_bound", "width", "sigma", "grid_signals", "signals", "band_rows_per_chunk")
+        # slot 16: the interpolation FMAs per realization as the last block's kernel ran them (half-chunk bands)
+        fma_run = float(g[16])
         d = dict(zip(keys, g.tolist()))
         d["last_path"] = int(d["last_path"])
         d["ok"] = bool(d["ok"])
@@ -355,6 +359,7 @@ class Context:
         d["signals"] = int(d["signals"])
         d["path_reason"] = _lib.fpta_batch_path_reason(self._h).decode()
         d["interp_kernel"] = interp_kernel_name(int(g[15]))
+        d["fma_interp_run"] = fma_run if fma_run > 0 else d["fma_interp"]
         return d
 
     def batch_synth(self, seed, real0, n_real, to_host=True, coeffs=False):

@@ -264,8 +264,18 @@ bool fused_layout(const fpta_ctx* c, const Layout& L) {
          c->interp_ws < 4 && !c->interp_wr && !psr_layout(c, L);
 }
 
+// The gridded plan of L runs white / ECORR blocks (and plain blocks k_grid_fused does not take: three grid signals)
+// on k_grid_fused_w: its 16-realization grids and draw ring fit in LDS (GridPlan::fused_w_ok).
+bool fused_w_layout(const fpta_ctx* c, const Layout& L) {
+  const GridPlan& G = L.grid;
+  return c->fused_white && c->interp_fused && G.built && G.ok && G.fused_w_ok && (c->grid_mfma & 1) && !c->interp_lds &&
+         c->interp_ws < 4 && !c->interp_wr && !psr_layout(c, L);
+}
+
 // The interpolation kernel reads the block's coefficients (pipelined blocks alternate two coefficient buffers)
-bool coef_in_interp(const fpta_ctx* c, const Layout& L) { return psr_layout(c, L) || fused_layout(c, L); }
+bool coef_in_interp(const fpta_ctx* c, const Layout& L) {
+  return psr_layout(c, L) || fused_layout(c, L) || fused_w_layout(c, L);
+}
 
 // merge: the gridded plan of L coalesces signals (GridPlan::members): after the last member of a grid signal is
 // drawn, k_coef_merge adds the other members' columns into the anchor's. coef_host (optional, with merge): the
@@ -510,6 +520,7 @@ struct WhiteCfg {
   const double* esig = nullptr;
   const double* zb = nullptr;
   int64_t nblocks = 0;
+  int64_t zb_ld = 0;  // 0: zb realization-major [R][nblocks]; > 0 epoch-major [nblocks][zb_ld] (k_grid_fused_w only)
   int64_t real0 = 0;
   uint32_t k0 = 0, k1 = 0;
 };
@@ -607,6 +618,7 @@ int run_synth(fpta_ctx* c, Layout& L, int32_t R, int32_t R_pad, double* out, int
       a.w_esig = white->esig;
       a.w_zb = white->zb;
       a.w_nblocks = white->nblocks;
+      a.w_zb_ld = white->zb_ld;
       a.real0 = white->real0;
       a.k0 = white->k0;
       a.k1 = white->k1;
@@ -924,6 +936,9 @@ int fpta_set_option(fpta_ctx* c, int32_t key, int64_t value) {
       if (value < 0 || value > 3) return fail(c, FPTA_EINVAL, "interp_fused: 0 .. 3");
       c->interp_fused = (int)value;
       return FPTA_OK;
+    case FPTA_OPT_FUSED_WHITE:
+      c->fused_white = value ? 1 : 0;
+      return FPTA_OK;
     case FPTA_OPT_INTERP_WR:
 #ifndef FPTA_DIAG_KERNELS
       if (value) return fail(c, FPTA_EINVAL, "interp_wr: k_grid_interp_wr is a diagnostic kernel, not in this build");
@@ -992,6 +1007,7 @@ int fpta_get_option(fpta_ctx* c, int32_t key, int64_t* value) {
     case FPTA_OPT_INTERP_PSR: *value = c->interp_psr; return FPTA_OK;
     case FPTA_OPT_INTERP_WR: *value = c->interp_wr; return FPTA_OK;
     case FPTA_OPT_INTERP_FUSED: *value = c->interp_fused; return FPTA_OK;
+    case FPTA_OPT_FUSED_WHITE: *value = c->fused_white; return FPTA_OK;
   }
   return fail(c, FPTA_EINVAL, "get_option: unknown key");
 }
@@ -1349,12 +1365,21 @@ int batch_common(fpta_ctx* c, uint64_t seed, int64_t real0, int32_t n_real, cons
   // ECORR epoch normals of this batch as a [R][n_epochs] block, read by every white path. (Making them from their
   // Philox counters inside the gridded epilogue instead was measured 2x slower on C5: the epilogue is VALU-bound,
   // profiles/round4/R4l_c5_storer_ecorr_inline_ab.txt.)
+  // k_grid_fused_w reads them epoch-major (an epoch's realizations contiguous: 16-byte gathers of realization pairs);
+  // the block then runs on it (grid_run checks), no other kernel reads them
   if (do_white && c->has_blocks) {
-    HIPCHK(c, c->zb_epochs.ensure(sizeof(double) * (size_t)n_real * c->n_blocks), "zb alloc");
+    const bool zb_major = path == 4 && c->fuse_white && fused_w_layout(c, L) && !c->fuse_sums;
+    const int64_t ldz = zb_major ? R_pad : 0;
+    HIPCHK(c, c->zb_epochs.ensure(sizeof(double) * (size_t)(zb_major ? R_pad : n_real) * c->n_blocks), "zb alloc");
     wc.zb = c->zb_epochs.as<double>();
+    wc.zb_ld = ldz;
     KTimer kt(c, FPTA_K_WHITE);
-    HIPCHK(c, launch_epoch_normals(c->stream, c->n_blocks, n_real, real0, k0, k1, c->zb_epochs.as<double>()),
-           "k_epoch_normals launch");
+    if (zb_major)
+      HIPCHK(c, launch_epoch_normals_t(c->stream, c->n_blocks, n_real, real0, k0, k1, c->zb_epochs.as<double>(), ldz),
+             "k_epoch_normals_t launch");
+    else
+      HIPCHK(c, launch_epoch_normals(c->stream, c->n_blocks, n_real, real0, k0, k1, c->zb_epochs.as<double>()),
+             "k_epoch_normals launch");
   }
   bool fused = false;
   if (L.segs.empty()) {
@@ -1568,6 +1593,7 @@ int fpta_batch_grid_info_n(fpta_ctx* c, double* dst, int32_t n_out) {
   out[13] = (double)c->batch.segs.size();
   out[14] = ok ? G.mean_v : 0.0;
   out[15] = c->last_interp;
+  out[16] = ok ? (c->last_fma_interp > 0.0 ? c->last_fma_interp : G.fma_interp) : 0.0;
   std::memcpy(dst, out, sizeof(double) * std::min<int32_t>(n_out, FPTA_GRID_INFO_LEN));
   return FPTA_GRID_INFO_LEN;
 }

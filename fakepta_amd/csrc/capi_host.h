@@ -103,6 +103,9 @@ struct GridPlan {
   // fused_lds the workgroup's LDS bytes
   bool fused_ok = false;
   size_t fused_lds = 0;
+  bool fused_w_ok = false;  // k_grid_fused_w's plan (16-realization grids, <= 3 grid signals); frows serves both
+  size_t fused_w_lds = 0;
+  bool frows_ok = false;
   int32_t fused_fq = 0;  // band steps per (chunk, lane group) in frows
   std::vector<int32_t> fused_lrow0;
   DevBuf frows;
@@ -112,6 +115,7 @@ struct GridPlan {
   bool fused_half_ok = false;
   int32_t fused_hfq = 0, fused_hvmax = 0, fused_hnq = 0;
   double fused_half_gain = 0.0;
+  double fma_interp_half = 0.0;  // interpolation FMAs per realization on half-chunk bands (both halves run max(nq0, nq1) steps)
   DevBuf hchunks, hrows, hwd;
   // k_grid_interp_wr plan (GridWindow): <= 2 grid signals, each signal's band rows in a ring of kWrSlots LDS slots by
   // unwrapped row; per chunk the slot of each band row, and the rows to load: all its band rows (full) or those not in
@@ -164,10 +168,14 @@ struct GridPlan {
     wr_ok = false;
     fused_ok = false;
     fused_lds = 0;
+    fused_w_ok = false;
+    fused_w_lds = 0;
+    frows_ok = false;
     fused_lrow0.clear();
     fused_half_ok = false;
     fused_hfq = fused_hvmax = fused_hnq = 0;
     fused_half_gain = 0.0;
+    fma_interp_half = 0.0;
     members.clear();
     anchor.clear();
     last.clear();
@@ -247,6 +255,8 @@ struct fpta_ctx {
   int overlap = 1;
   int interp_ws = 1;      // gridded interpolation on the warp-specialised kernel (FPTA_OPT_INTERP_WS)
   int last_interp = 0;    // interpolation kernel of the last gridded block: 1 + 4 kind + 2 white + part (0: none)
+  int fused_white = 0;  // k_grid_fused_w for white / ECORR and three-grid-signal blocks (FPTA_OPT_FUSED_WHITE)
+  double last_fma_interp = 0.0;  // its interpolation MFMA FMAs per realization as run (half-chunk bands: both halves)
   int grid_coalesce = 1;  // gridded path: signals sharing w0 and the chromatic weight share one grid (FPTA_OPT_GRID_COALESCE)
   int part_group = kPartGroup;  // fused partial checksums: consecutive chunks per partial row (FPTA_OPT_PART_GROUP)
   int interp_psr = 1;  // k_grid_interp_psr where the layout allows it (FPTA_OPT_INTERP_PSR)
@@ -409,6 +419,7 @@ int wait_coef_all(fpta_ctx* c);
 bool grid_gen_fused(const fpta_ctx* c, const Layout& L, size_t g);
 bool psr_layout(const fpta_ctx* c, const Layout& L);
 bool fused_layout(const fpta_ctx* c, const Layout& L);
+bool fused_w_layout(const fpta_ctx* c, const Layout& L);
 int batch_common(fpta_ctx* c, uint64_t seed, int64_t real0, int32_t n_real, const double* zin, int32_t zin_nm,
                  double* out, double* coeffs_out, bool white);
 int launch_block_checksums(fpta_ctx* c, bool async = false, hipStream_t* used = nullptr, double* dst = nullptr,

@@ -47,8 +47,9 @@ struct SynthArgs {
   const double* w_sigma;       // [n_toa] or null
   const int32_t* w_block_of;   // [n_toa] epoch of each TOA (-1: none) or null
   const double* w_esig;        // [n_blocks]
-  const double* w_zb;          // [n_real][n_blocks] epoch normals of this batch
+  const double* w_zb;          // [n_real][n_blocks] epoch normals of this batch (w_zb_ld > 0: [n_blocks][w_zb_ld])
   int64_t w_nblocks;
+  int64_t w_zb_ld;             // 0: realization-major epoch normals; > 0 epoch-major with this pitch (k_grid_fused_w)
   int64_t real0;               // global index of realization 0 of the batch
   uint32_t k0, k1;             // Philox key (seed)
   // geometry checked by the debug build (FPTA_DCHECK): coefficient values P*K*R_pad, and the TOA x
@@ -204,7 +205,8 @@ constexpr int kFusedSlot = kFusedGroupModes * kFusedReal * 2;  // doubles per si
 constexpr int kFusedLdsMax = 160 * 1024;
 constexpr int kFusedNQ = 12;       // band steps whose operands an interpolation wave holds (a wider chunk: the rest one
                                    // step at a time)
-constexpr int kFusedWdPad = 4 * kFusedNQ;  // band rows of zero weights past the last chunk (GridPlan::wd)
+constexpr int kFusedWdPad = 4 * 16;  // band rows of zero weights past the last chunk (GridPlan::wd): the most
+                                     // unconditional band-step loads of a fused kernel (kFusedWNQ)
 constexpr int kFusedTerms = 2;     // members of a grid signal whose inputs the DFT waves prefetch (the others: inline)
 struct FusedSig {
   const double* tq;  // quarter-range tables [4][ntq][ldq] (GridSegDev::tq)
@@ -233,8 +235,9 @@ struct FusedHalf {
   const double* wd;      // [2 n_chunks][vmax][16] weights (fused_half_weight_index), + zero rows past the last
   int32_t fq, vmax;      // band steps per (chunk, half, j) in lrows (a multiple of 4); band rows per half (mult. of 8)
 };
+constexpr int kFusedArgSig = 3;  // grid signal descriptors a FusedArgs holds (k_grid_fused takes kFusedMaxSig of them)
 struct FusedArgs {
-  FusedSig s[kFusedMaxSig];
+  FusedSig s[kFusedArgSig];
   int32_t n_sig;
   int32_t ring_off;       // LDS offset (doubles) of the draw ring (past the grids); a sync word follows it
   const int32_t* lrows;   // [n_chunks][4][fq] LDS grid row of band row 4 q + j at [j][q]
@@ -252,6 +255,10 @@ constexpr int kFusedQueueWords = 9;  // 8 per-XCD item tickets + the count of fi
 #define FPTA_FUSED_JOIN_SAFETY 1.5  // measured best of 0.5 .. 5 on C2 and C4 (profiles/round5/r5mn_*); variants may change it (make variant DEFS=-DFPTA_FUSED_JOIN_SAFETY=...)
 #endif
 constexpr double kFusedJoinSafety = FPTA_FUSED_JOIN_SAFETY;  // FusedArgs::join_reserve over the estimated need
+#ifndef FPTA_FUSED_W_JOIN_SAFETY
+#define FPTA_FUSED_W_JOIN_SAFETY 1.5  // the same for k_grid_fused_w
+#endif
+constexpr double kFusedWJoinSafety = FPTA_FUSED_W_JOIN_SAFETY;
 // nq_max: band steps of the widest chunk (vmax / 4; the kernel holds up to 12 steps' operands and takes a wider chunk's
 // in turns); lds_bytes: grids + ring + sync word; ev0 / ev1: timing events bound to the dispatch (hipExtLaunchKernel)
 // half: the HALF kernel on f.h (nq_max: band steps of the widest half); *kernel_out (optional): the instance launched,
@@ -259,6 +266,19 @@ constexpr double kFusedJoinSafety = FPTA_FUSED_JOIN_SAFETY;  // FusedArgs::join_
 hipError_t launch_grid_fused(hipStream_t st, const SynthArgs& a, const GridBand& band, const FusedArgs& f,
                              int32_t nq_max, size_t lds_bytes, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr,
                              bool half = false, int* kernel_out = nullptr);
+// White-epilogue variant (k_grid_fused_w, grid_fused_w.hip): gridded blocks with white noise / ECORR (C5: RN + three
+// common signals, DM and Sv: three grid signals of 884 rows). Items are (pulsar, kFusedWReal realizations), so every
+// grid signal's grid fits in LDS; up to kFusedWMaxSig grid signals and 2 kFusedDW DFT jobs (two per DFT wave); draw
+// groups of kFusedWGroupModes modes (one (mode, realization pair) per DFT lane); the interpolation waves add white
+// noise and ECORR (epoch normals from the block's SynthArgs::w_zb) before their stores.
+constexpr int kFusedWReal = 16, kFusedWPitch = 16, kFusedWMaxSig = 3, kFusedWGroupModes = 32;
+constexpr int kFusedWSlot = kFusedWGroupModes * kFusedWReal * 2;  // doubles per signal of a ring slot [32][16][cos, sin]
+constexpr int kFusedWJobs = 2 * kFusedDW;
+constexpr int kFusedWNQ = 16;  // band steps whose operands an interpolation wave holds
+hipError_t launch_grid_fused_w(hipStream_t st, const SynthArgs& a, const GridBand& band, const FusedArgs& f,
+                               int32_t nq_max, size_t lds_bytes, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr,
+                               int* kernel_out = nullptr);
+constexpr int kFusedWKernels = 2;  // instances: draws from an even / odd first realization
 constexpr int kFusedKernels = 9;  // instances: {NQ 8, NQ 12} x {no draws, draws, draws from an odd realization},
                                   // then HALF (NQ 8 per half) x the same three
 // Storer-wave variant: compute waves hand finished sums to storer waves through LDS; every block kind (white / ECORR
@@ -324,6 +344,10 @@ hipError_t launch_gen_mix(hipStream_t st, const SegDesc& sd, int32_t seg_id, int
                           hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
 hipError_t launch_mix_tiled(hipStream_t st, const SegDesc& sd, int32_t P, int32_t R_pad, const double* zbuf,
                             double* coef, int32_t K, double* x_out);
+// epoch-major [n_blocks][ldz] (ldz >= n_real, even): a realization's normals of one epoch are contiguous, so
+// k_grid_fused_w's gathers of an epoch's realization pairs are 16-byte loads (the same normals as launch_epoch_normals)
+hipError_t launch_epoch_normals_t(hipStream_t st, int64_t n_blocks, int32_t n_real, int64_t real0, uint32_t k0,
+                                  uint32_t k1, double* zb, int64_t ldz);
 hipError_t launch_epoch_normals(hipStream_t st, int64_t n_blocks, int32_t n_real, int64_t real0, uint32_t k0,
                                 uint32_t k1, double* zb);
 hipError_t launch_white_pairs(hipStream_t st, const double* sigma, const int32_t* block_of, const double* esig,

@@ -483,7 +483,7 @@ int grid_build(fpta_ctx* c, Layout& L) {
   if ((rc = upload(c, d_chunk_of, chunk_of.data(), sizeof(int32_t) * N, "grid chunk_of")) ||
       (rc = upload(c, d_tt_of, tt_of.data(), sizeof(int32_t) * N, "grid tt_of")))
     return rc;
-  // + kFusedWdPad band rows after the last chunk: k_grid_fused loads NQ band steps' weights of every chunk unclamped
+  // + kFusedWdPad band rows after the last chunk: k_grid_fused(_w) loads NQ band steps' weights of every chunk unclamped
   const size_t wbytes = sizeof(double) * ((size_t)n_chunks * vmax + kFusedWdPad) * kGridTT;
   HIPCHK(c, G.wd.ensure(wbytes), "grid weights alloc");
   HIPCHK(c, hipMemsetAsync(G.wd.p, 0, wbytes, c->stream), "grid weights memset");
@@ -567,12 +567,31 @@ int grid_build(fpta_ctx* c, Layout& L) {
       rows += gs->nf;
     }
     const size_t lds = sizeof(double) * ((size_t)rows * kFusedPitch + 2 * kFusedMaxSig * kFusedSlot) + 48;
-    for (const std::vector<int32_t>& m : G.members) ok = ok && m.size() <= (size_t)kDftGenTerms;
-    ok = ok && jobs <= kFusedDW && lds <= (size_t)kFusedLdsMax;
-    if (ok) {
+    bool members_ok = true;
+    for (const std::vector<int32_t>& m : G.members) members_ok = members_ok && m.size() <= (size_t)kDftGenTerms;
+    // k_grid_fused_w (white / ECORR blocks, and plain blocks of three grid signals): the grids of kFusedWReal
+    // realizations, <= kFusedWMaxSig grid signals, <= kFusedWJobs DFT jobs
+    bool ok_w = n_seg <= kFusedWMaxSig && members_ok;
+    int32_t jobs_w = 0, rows_w = 0;
+    for (int32_t s = 0; s < n_seg && ok_w; ++s) {
+      const GridSeg* gs = G.segs[s];
+      ok_w = gs->nf % 4 == 0 && gs->ldq == (gs->nf / 4 + 32) / 32 * 32;
+      jobs_w += (gs->nf / 4 + 32) / 32;
+      rows_w += gs->nf;
+    }
+    const size_t lds_w = sizeof(double) * ((size_t)rows_w * kFusedWPitch + 2 * kFusedWMaxSig * kFusedWSlot) + 48;
+    ok_w = ok_w && jobs_w <= kFusedWJobs && lds_w <= (size_t)kFusedLdsMax;
+    if (ok_w && G.fused_lrow0.size() != (size_t)n_seg) {  // the LDS row of each grid signal (as k_grid_fused's)
+      G.fused_lrow0.clear();
+      for (int32_t s = 0, r = 0; s < n_seg; r += G.segs[s]->nf, ++s) G.fused_lrow0.push_back(r);
+    }
+    G.fused_w_ok = ok_w;
+    G.fused_w_lds = lds_w;
+    ok = ok && members_ok && jobs <= kFusedDW && lds <= (size_t)kFusedLdsMax;
+    if (ok || ok_w) {
       // [n_chunks][4][fq]: band row 4 q + j of a chunk at [j][q] (a lane's rows of consecutive steps contiguous: 16-byte
       // loads), fq = the band steps rounded up to 4 and at least kFusedNQ; steps past the chunk's repeat its first row
-      const int32_t fq = std::max(kFusedNQ, (vmax / 4 + 3) & ~3);
+      const int32_t fq = std::max(std::max(kFusedNQ, kFusedWNQ), (vmax / 4 + 3) & ~3);
       std::vector<int32_t> band_row(vmax);
       std::vector<int32_t> lrt((size_t)n_chunks * 4 * fq);
       for (int32_t ci = 0; ci < n_chunks; ++ci) {
@@ -590,6 +609,7 @@ int grid_build(fpta_ctx* c, Layout& L) {
       G.fused_lds = lds;
     }
     G.fused_ok = ok;
+    G.frows_ok = ok || ok_w;
     // Half-chunk bands (FusedHalf): TOAs 0..15 and 16..31 of each chunk get bands of their own (a 32-TOA chunk's band
     // is w + the cells its 32 TOAs span; a half's, w + the cells of 16). Per half the signals' bands back to back,
     // padded to whole band steps; the weights by the half-band layout of k_grid_weights.
@@ -630,7 +650,7 @@ int grid_build(fpta_ctx* c, Layout& L) {
         }
         hch[ci] = make_int4(chunks[ci].x, chunks[ci].y, chunks[ci].z, nqh[0] | (nqh[1] << 16));
         steps_full += 4.0 * (chunks[ci].w / 4);
-        steps_half += 2.0 * (nqh[0] + nqh[1]);
+        steps_half += 4.0 * std::max(nqh[0], nqh[1]);  // the kernel runs both halves' longer step count
       }
       int32_t hvmax = 8;
       for (int32_t v : hv) hvmax = std::max(hvmax, (v + 7) & ~7);
@@ -682,6 +702,7 @@ int grid_build(fpta_ctx* c, Layout& L) {
       G.fused_hvmax = hvmax;
       G.fused_hnq = hnq;
       G.fused_half_gain = steps_half > 0.0 ? steps_full / steps_half : 0.0;
+      G.fma_interp_half = steps_half * 4.0 * kGridTT / 4.0;  // 4 rows x 32 TOAs per (both-halves) step
       G.fused_half_ok = true;
     }
   }
@@ -723,8 +744,14 @@ int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad, bool pipe) {
   // k_grid_fused: the DFTs run inside the synthesis kernel too (plain blocks: no white epilogue, no partial checksums)
   const bool fused = !psr && fused_layout(c, L) && !a.w_on && !a.accumulate &&
                      !(c->fuse_sums && a.out == c->out.as<double>()) && (!pipe || c->prev_psr);
+  // k_grid_fused_w: the same for white / ECORR blocks and for plain blocks k_grid_fused does not take (three grid
+  // signals, C5's shape)
+  const bool fused_w = !psr && !fused && fused_w_layout(c, L) && !a.accumulate &&
+                       !(c->fuse_sums && a.out == c->out.as<double>()) && (!pipe || c->prev_psr);
+  if (a.w_on && a.w_zb_ld > 0 && !fused_w)  // batch_common wrote them for k_grid_fused_w only
+    return fail(c, FPTA_ESTATE, "internal: epoch-major ECORR normals for a block k_grid_fused_w does not take");
   // grid buffers only for the kernels that read one (two of 0.41 GB each on C2)
-  if (!psr && !fused && (G.g_rpad != R_pad || (pipe && G.g2.cap < gbytes))) {
+  if (!psr && !fused && !fused_w && (G.g_rpad != R_pad || (pipe && G.g2.cap < gbytes))) {
     if (c->side) HIPCHK(c, hipStreamSynchronize(c->side), "side sync");  // no reader of a buffer being regrown
     if (c->side2) HIPCHK(c, hipStreamSynchronize(c->side2), "side sync");
     HIPCHK(c, hipStreamSynchronize(c->stream), "grid regrow sync");
@@ -740,7 +767,7 @@ int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad, bool pipe) {
     // the DFT overwrites buffer gi: the interpolation that last read it (two blocks back) must be done
     if (c->gfree_set[gi]) HIPCHK(c, hipStreamWaitEvent(c->side, c->ev_gfree[gi], 0), "grid buffer wait");
   }
-  if (psr || fused) {
+  if (psr || fused || fused_w) {
     GridSeg* gs = G.segs[0];
     GridSegDev& g = gsegs.s[0];
     g.g = nullptr;
@@ -896,9 +923,9 @@ int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad, bool pipe) {
   // the fused launch takes the timing events itself (no marker packets around it); the diagnostic options that take
   // another kernel for a fused layout time it with recorded events
 #ifdef FPTA_DIAG_KERNELS
-  const bool ext = fused && c->interp_ws != 4 && c->interp_ws != 5 && !c->interp_wr;
+  const bool ext = (fused || fused_w) && c->interp_ws != 4 && c->interp_ws != 5 && !c->interp_wr;
 #else
-  const bool ext = fused;
+  const bool ext = fused || fused_w;
 #endif
   KTimer kt(c, FPTA_K_SYNTH, nullptr, ext);
   GridBand band{G.chunks.as<int4>(), G.rows.as<int32_t>(), G.wd.as<double>(), gbase, G.n_chunks, G.vmax,
@@ -931,9 +958,10 @@ int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad, bool pipe) {
     GridWindow wrp{G.wr_meta.as<int4>(), G.wr_list.as<int2>(), G.wr_slot.as<int32_t>()};
     HIPCHK(c, launch_grid_interp_wr(c->stream, a, band, wrp, R_pad), "k_grid_interp_wr launch");
 #endif
-  } else if (fused) {
+  } else if (fused || fused_w) {
     // half-chunk bands (FPTA_OPT_INTERP_FUSED 1: where they save >= 3 % of the interpolation MFMAs; 3: always)
-    const bool half = G.fused_half_ok && (c->interp_fused == 3 || (c->interp_fused == 1 && G.fused_half_gain >= 1.03));
+    const bool half = fused && G.fused_half_ok &&
+                      (c->interp_fused == 3 || (c->interp_fused == 1 && G.fused_half_gain >= 1.03));
     const int32_t nq = half ? G.fused_hnq : G.vmax / 4;
     FusedArgs f{};
     if (half) f.h = FusedHalf{G.hchunks.as<int4>(), G.hrows.as<int32_t>(), G.hwd.as<double>(), G.fused_hfq, G.fused_hvmax};
@@ -977,17 +1005,22 @@ int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad, bool pipe) {
     // build: C2 (~7 x 72 per build, ~48 per chunk: reserve 63 of its 63 chunks per item) hardly joins; C4 (~7 x 32,
     // ~32 per chunk: reserve ~42 of 313) joins for most of an item. (The estimate is about half the measured build
     // time on C2; the factor 1.5 was the best of 0.5 .. 5 on both, profiles/round5/r5mn_*.)
+    // k_grid_fused_w (16-realization items): an iteration is up to 64 MFMAs (two jobs) + the draws, a chunk V / 2
+    // MFMAs + ~12 + the white epilogue (two Philox calls per lane: ~40 on white blocks).
     {
       int it_max = 0, gen = 0;
       for (int32_t s = 0; s < f.n_sig; ++s) {
         const int nm = f.s[s].nm;
-        it_max = std::max(it_max, (((((nm + 1) >> 1) + 3) >> 2) + 1) >> 1);
+        it_max = std::max(it_max, fused_w ? (nm + kFusedWGroupModes - 1) / kFusedWGroupModes
+                                          : (((((nm + 1) >> 1) + 3) >> 2) + 1) >> 1);
         for (int i = 0; i < f.s[s].n_terms; ++i) gen += f.s[s].term_kind[i] == 0;
       }
-      const double build = it_max * (32.0 + 20.0 * gen), chunk = G.mean_v + 12.0;
-      f.join_reserve = (int32_t)std::min(1.0e6, std::ceil(kFusedJoinSafety * kFusedIW * build / chunk));
+      const double build = it_max * ((fused_w ? 64.0 : 32.0) + 20.0 * gen);
+      const double chunk = fused_w ? G.mean_v / 2 + 12.0 + (a.w_on ? 40.0 : 0.0) : G.mean_v + 12.0;
+      f.join_reserve = (int32_t)std::min(
+          1.0e6, std::ceil((fused_w ? kFusedWJoinSafety : kFusedJoinSafety) * kFusedIW * build / chunk));
     }
-    f.ring_off = (G.fused_lrow0.back() + G.segs.back()->nf) * kFusedPitch;
+    f.ring_off = (G.fused_lrow0.back() + G.segs.back()->nf) * (fused_w ? kFusedWPitch : kFusedPitch);
     f.lrows = G.frows.as<int32_t>();
     f.fq = G.fused_fq;
     f.psr_c0 = G.psr_c0.as<int32_t>();
@@ -1013,9 +1046,16 @@ int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad, bool pipe) {
     f.queue = c->fused_q.as<uint32_t>();
     hipEvent_t e0 = kt.start_ev();
     int ki = 0;
-    HIPCHK(c, kt.checked(launch_grid_fused(c->stream, a, band, f, nq, G.fused_lds, e0, kt.stop_ev(), half, &ki)),
-           "k_grid_fused launch");
-    kind = kInterpKindFused0 + ki;  // fpta_batch_grid_info_n slot 15: the instance launched
+    if (fused_w) {
+      HIPCHK(c, kt.checked(launch_grid_fused_w(c->stream, a, band, f, nq, G.fused_w_lds, e0, kt.stop_ev(), &ki)),
+             "k_grid_fused_w launch");
+      kind = kInterpKindFused0 + kFusedKernels + ki;
+    } else {
+      HIPCHK(c, kt.checked(launch_grid_fused(c->stream, a, band, f, nq, G.fused_lds, e0, kt.stop_ev(), half, &ki)),
+             "k_grid_fused launch");
+      kind = kInterpKindFused0 + ki;  // fpta_batch_grid_info_n slot 15: the instance launched
+    }
+    c->last_fma_interp = half ? G.fma_interp_half : G.fma_interp;
   } else if (psr) {
     kind = G.vmax <= 16 ? 6 : 7;  // launch_grid_interp_psr: NQ = 4 or 8 band steps
     HIPCHK(c,
@@ -1041,6 +1081,7 @@ int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad, bool pipe) {
     HIPCHK(c, launch_grid_interp_mfma(c->stream, a, band, R_pad), "k_grid_interp_mfma launch");
   }
   c->last_interp = 1 + kind * 4 + (a.w_on ? 2 : 0) + (a.part ? 1 : 0);
+  if (kind < kInterpKindFused0) c->last_fma_interp = G.fma_interp;
   if (pipe) {  // buffer gi is free once this interpolation is done; the next block's DFT writes the other one
     HIPCHK(c, hipEventRecord(c->ev_gfree[gi], c->stream), "event record");
     c->gfree_set[gi] = true;

@@ -896,6 +896,41 @@ hipError_t launch_mix_tiled(hipStream_t st, const SegDesc& sd, int32_t P, int32_
   return hipGetLastError();
 }
 
+// k_epoch_normals_t: the same normals epoch-major, zb[b][r] (pitch ldz): one thread per (global realization pair,
+// epoch pair), realization pairs fastest, so a wave's stores are contiguous. grid (ceil(pairs / 256), epoch pairs).
+__global__ __launch_bounds__(256) void k_epoch_normals_t(int64_t n_blocks, int32_t n_real, int64_t real0, uint32_t k0,
+                                                         uint32_t k1, double* __restrict__ zb, int64_t ldz,
+                                                         int64_t npairs) {
+  const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;  // realization pair
+  const int64_t i = blockIdx.y;                               // epoch pair
+  if (j >= npairs) return;
+  const int64_t g0 = ((real0 >> 1) + j) * 2;  // even global realization of this pair
+  double z[4];
+  quad4((uint64_t)(2 * i), kEcorrStream, (uint64_t)g0, k0, k1, z);
+  const int64_t r = g0 - real0;
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    if (2 * i + e >= n_blocks) continue;
+    double* row = zb + (2 * i + e) * ldz;
+    if (r >= 0 && r + 1 < n_real && (r & 1) == 0) {
+      *(double2*)(row + r) = make_double2(z[2 * e], z[2 * e + 1]);
+    } else {
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+        if (r + h >= 0 && r + h < n_real) row[r + h] = z[2 * e + h];
+    }
+  }
+}
+
+hipError_t launch_epoch_normals_t(hipStream_t st, int64_t n_blocks, int32_t n_real, int64_t real0, uint32_t k0,
+                                  uint32_t k1, double* zb, int64_t ldz) {
+  const int64_t npairs = ((real0 + n_real + 1) >> 1) - (real0 >> 1);
+  if (ldz < n_real || (n_blocks + 1) / 2 > 0x7FFFFFFF) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_epoch_normals_t, dim3((unsigned)((npairs + 255) / 256), (unsigned)((n_blocks + 1) / 2)),
+                     dim3(256), 0, st, n_blocks, n_real, real0, k0, k1, zb, ldz, npairs);
+  return hipGetLastError();
+}
+
 hipError_t launch_epoch_normals(hipStream_t st, int64_t n_blocks, int32_t n_real, int64_t real0, uint32_t k0,
                                 uint32_t k1, double* zb) {
   const int64_t npairs = ((real0 + n_real + 1) >> 1) - (real0 >> 1);

@@ -218,11 +218,14 @@ int fpta_batch_info(fpta_ctx* ctx, int64_t* info);
  * mean band rows per chunk (all grid signals, padded to 4), out[15] the interpolation kernel of the last gridded
  * block: 0 none, else 1 + 4 kind + 2 (white / ECORR epilogue) + (fused partial checksums), kind 0
  * k_grid_interp_mfma, 1 k_grid_interp_ws, 2 k_grid_interp_ws2, 3 k_grid_interp_lds, 4 k_grid_interp_st, 5
- * k_grid_interp_u, 6 / 7 k_grid_interp_psr with 4 / 8 band steps, 8 / 9 k_grid_fused holding 8 / 12 band steps'
- * operands, 10 k_grid_interp_wr (diagnostic builds only).
+ * k_grid_interp_u, 6 / 7 k_grid_interp_psr with 4 / 8 band steps, 10 k_grid_interp_wr (diagnostic builds only),
+ * 11 .. 19 the k_grid_fused<NQ, ODD, GEN, HALF> instances (8 / 12 band steps' operands x no draws / draws / draws
+ * from an odd realization, then half-chunk bands x the same three), 20 / 21 k_grid_fused_w (white / ECORR epilogue;
+ * even / odd first realization); out[16] (FPTA_VERSION 10100) the interpolation MFMA FMAs per realization of the
+ * last gridded block as its kernel ran them (half-chunk bands: both halves' steps; else out[4]).
  * fpta_batch_grid_info_n writes the first min(n_out, FPTA_GRID_INFO_LEN) values and returns FPTA_GRID_INFO_LEN
  * (negative on error); fpta_batch_grid_info keeps the round-1 contract: out[0..8], host double[9]. */
-#define FPTA_GRID_INFO_LEN 16
+#define FPTA_GRID_INFO_LEN 17
 int fpta_batch_grid_info_n(fpta_ctx* ctx, double* out, int32_t n_out);
 int fpta_batch_grid_info(fpta_ctx* ctx, double* out);
 /* Why the last batch did not take the gridded path (signal count, non-harmonic grid, error bound, cost,
@@ -382,6 +385,13 @@ int fpta_comm_gather(fpta_comm* comm, const double* send, int64_t count, double*
                                      DFT + interpolation kernels. Whole-chunk bands are bit-identical to the DFT +
                                      interpolation kernels; half-chunk bands group the band rows differently (sums
                                      agree to rounding). A layout k_grid_interp_psr serves keeps it. */
+#define FPTA_OPT_FUSED_WHITE 24   /* (FPTA_VERSION 10100) gridded white / ECORR blocks, and plain blocks of three grid
+                                     signals, whose grids for 16 realizations fit in LDS (C5: 884 rows, 113 KB): 1
+                                     k_grid_fused_w (k_grid_fused's design with 16-realization items, up to 8 DFT
+                                     jobs, the white / ECORR epilogue in the interpolation waves, ECORR epoch normals
+                                     epoch-major); 0 (default) the DFT + interpolation kernels (measured faster on C5:
+                                     1.74 vs 2.05 ms per block). Sums agree to rounding (two summation
+                                     chains per chunk), white / ECORR terms identical. */
 int fpta_set_option(fpta_ctx* ctx, int32_t key, int64_t value);
 /* Current value of option `key` (same keys as fpta_set_option). */
 int fpta_get_option(fpta_ctx* ctx, int32_t key, int64_t* value);

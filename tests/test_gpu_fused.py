@@ -243,9 +243,10 @@ def test_fused_pipelined_blocks(ctx, capi, shipped):
 
 
 def test_fused_not_taken_outside_its_blocks(ctx, capi, shipped):
-    """Blocks the fused kernel does not serve take the two-kernel path: white / ECORR epilogue, fused partial
-    checksums (streamed jobs), more than four 32-row DFT chunks (a masked backend signal: a third grid signal), grids
-    too large for LDS (600 modes: 1,804 grid rows), and FPTA_OPT_INTERP_FUSED 0."""
+    """Blocks k_grid_fused does not serve take the two-kernel path: white / ECORR epilogue, fused partial checksums
+    (streamed jobs), three grid signals (a masked backend signal), grids too large for LDS (600 modes: 1,804 grid
+    rows), and FPTA_OPT_INTERP_FUSED 0 (k_grid_fused_w, which could take the first and third, is opt-in:
+    FPTA_OPT_FUSED_WHITE, tests/test_gpu_fused_w.py)."""
     rng = np.random.default_rng(227)
     try:
         offs, toas, nu, segs = _c2_like(ctx, rng, P=12, n=(100, 300))
@@ -270,7 +271,8 @@ def test_fused_not_taken_outside_its_blocks(ctx, capi, shipped):
             build()
             ctx.set_option(capi.OPT_SYNTH_PATH, 4)
             ctx.batch_synth(3, 0, 256, to_host=False)
-            assert not ctx.batch_grid_info()["interp_kernel"].startswith("k_grid_fused")
+            k = ctx.batch_grid_info()["interp_kernel"]
+            assert not k.startswith("k_grid_fused"), k
     finally:
         ctx.batch_set_white()
         ctx.batch_clear()

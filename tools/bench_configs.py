@@ -230,12 +230,12 @@ def c4(steps=5):
                 if kt1["mix"] else None)
 
 
-def c5(steps=10):
-    from fakepta_amd import _capi
+def c5_layout(ctx):
+    """C5's array on ctx (100 psr x 2000 TOAs on two backends: RN30 + DM100 + Sv100, HD + monopole + dipole common
+    signals, white + ECORR); returns the BatchSimulator."""
     from fakepta import correlated_noises as cn
     from fakepta import fake_pta as fp
     from fakepta_amd.batch import BatchSimulator
-    ctx = new_context(_capi)
     P = 100
     np.random.seed(7)
     pos = fib(P)
@@ -253,7 +253,13 @@ def c5(steps=10):
     cn.add_common_correlated_noise(psrs, orf="hd", name="gw", log10_A=-14.5, gamma=13 / 3)
     cn.add_common_correlated_noise(psrs, orf="monopole", name="clk", log10_A=-15.0, gamma=4.0)
     cn.add_common_correlated_noise(psrs, orf="dipole", name="eph", log10_A=-15.0, gamma=4.0)
-    sim = BatchSimulator(psrs, white=True, ecorr=True, ctx=ctx)
+    return BatchSimulator(psrs, white=True, ecorr=True, ctx=ctx)
+
+
+def c5(steps=10):
+    from fakepta_amd import _capi
+    ctx = new_context(_capi)
+    sim = c5_layout(ctx)
     R = 1024
     dt = timed(ctx, _capi, lambda s: ctx.batch_synth(9, s * R, R, to_host=False), steps)
     info = ctx.batch_info()

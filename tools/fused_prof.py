@@ -24,7 +24,7 @@ def main():
     ap.add_argument("--blocks", type=int, default=3)
     ap.add_argument("--ghz", type=float, default=2.2, help="clock for the cycle -> time conversion")
     ap.add_argument("--opt", action="append", default=[])
-    ap.add_argument("--config", default="c2", choices=["c2", "c4"])
+    ap.add_argument("--config", default="c2", choices=["c2", "c4", "c5"])
     args = ap.parse_args()
     from bench import build_array
     from fakepta_amd import _capi
@@ -38,6 +38,11 @@ def main():
         sim = BatchSimulator(psrs, white=False, ctx=ctx)
         R = 1024
         run = lambda b: sim.synth(R, seed=1234, real0=b * R, to_host=False)  # noqa: E731
+    elif args.config == "c5":  # C5's layout (tools/bench_configs.py c5): k_grid_fused_w
+        from tools.bench_configs import c5_layout
+        sim = c5_layout(ctx)
+        R = 1024
+        run = lambda b: ctx.batch_synth(9, b * R, R, to_host=False)  # noqa: E731
     else:  # C4's layout (tools/bench_configs.py c4): 1000 psr x 10k TOAs, HD100, R = 256
         from tools.bench_configs import c4_layout
         c4_layout(ctx)
