@@ -249,7 +249,12 @@ struct FusedArgs {
   uint32_t* queue;           // [kFusedQueueWords], zero at launch; the kernel's last workgroup zeroes it again
   int32_t join_reserve;      // the DFT waves interpolate an item's chunks while more than this many are left
   FusedHalf h;               // half-chunk bands (HALF kernels only; else zero)
+  int32_t cu_pct;            // host only: workgroups for this percentage of the CUs (0 = all), leaving the rest to a
+                             // co-running kernel (the next block's ORF mix)
 };
+#ifndef FPTA_FUSED_MIX_CU_PCT
+#define FPTA_FUSED_MIX_CU_PCT 100  // CUs of k_grid_fused's grid while the next block's k_mix_mfma may co-run
+#endif
 constexpr int kFusedQueueWords = 9;  // 8 per-XCD item tickets + the count of finished workgroups
 #ifndef FPTA_FUSED_JOIN_SAFETY
 #define FPTA_FUSED_JOIN_SAFETY 1.5  // measured best of 0.5 .. 5 on C2 and C4 (profiles/round5/r5mn_*); variants may change it (make variant DEFS=-DFPTA_FUSED_JOIN_SAFETY=...)

@@ -864,7 +864,8 @@ hipError_t launch_grid_fused(hipStream_t st, const SynthArgs& a, const GridBand&
     n_cus[dev].store(n_cu, std::memory_order_relaxed);
   }
   // persistent: one workgroup per CU (the grids take most of the LDS)
-  const int64_t grid = std::min<int64_t>((items + 7) / 8 * 8, ((int64_t)n_cu + 7) / 8 * 8);
+  const int64_t cus = f.cu_pct > 0 && f.cu_pct < 100 ? std::max<int64_t>(8, (int64_t)n_cu * f.cu_pct / 100) : n_cu;
+  const int64_t grid = std::min<int64_t>((items + 7) / 8 * 8, (cus + 7) / 8 * 8);
   // NQ: band steps whose operands an interpolation wave holds (a wider chunk takes them NQ at a time)
   // ODD: the first realization is odd, so no lane's realization pair is one Philox pair (the draws take two)
   // GEN: some term is drawn in the kernel

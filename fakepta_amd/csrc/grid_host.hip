@@ -935,7 +935,13 @@ int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad, bool pipe) {
   // k_grid_interp_ws tiles 512 realizations (4 compute waves x 128): when R_pad leaves some of the last tile's compute
   // waves idle, the 256-realization tiles of k_grid_interp_ws2 waste less (C4, R_pad = 256: half of every ws tile;
   // 6.8-7.4 vs 8.4 ms/step, profiles/r04a_c4_ws2.txt)
+  // (the automatic k_grid_interp_ws2 choice for such R_pad, diagnostic builds only since round 6: no shipped layout
+  // reaches it)
+#ifdef FPTA_DIAG_KERNELS
   const bool ws2_fits = c->interp_ws == 1 && (R_pad + 255) / 256 * 256 - R_pad < (R_pad + 511) / 512 * 512 - R_pad;
+#else
+  const bool ws2_fits = false;
+#endif
   int kind;  // the interpolation kernel (fpta_batch_grid_info_n slot 15)
   if (false) {
 #ifdef FPTA_DIAG_KERNELS
@@ -1021,6 +1027,13 @@ int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad, bool pipe) {
           1.0e6, std::ceil((fused_w ? kFusedWJoinSafety : kFusedJoinSafety) * kFusedIW * build / chunk));
     }
     f.ring_off = (G.fused_lrow0.back() + G.segs.back()->nf) * (fused_w ? kFusedWPitch : kFusedPitch);
+    // a pipelined block whose common signals are mixed by a separate k_mix_mfma (P > kGenMixMaxP, C4): the next
+    // block's mix is queued on the side stream while this kernel runs
+    {
+      bool sep_mix = false;
+      for (const Seg* sg : L.segs) sep_mix = sep_mix || (sg->d.kind == 1 && L.P > kGenMixMaxP);
+      f.cu_pct = pipe && sep_mix ? FPTA_FUSED_MIX_CU_PCT : 100;
+    }
     f.lrows = G.frows.as<int32_t>();
     f.fq = G.fused_fq;
     f.psr_c0 = G.psr_c0.as<int32_t>();

@@ -886,150 +886,9 @@ __global__ __launch_bounds__(512, 1) void k_grid_interp_ws(SynthArgs a, GridBand
   }
 }
 
-// ----------------------------------------------------------------------------- k_grid_interp_ws2
-// k_grid_interp_ws with half the tile per compute wave (RW = 4: 64 realizations x 32 TOAs, 8 MFMAs per band step)
-// and two workgroups per CU (16 waves, <= 128 VGPRs). The two workgroups' barriers are independent, so while the
-// compute waves of one store a finished tile the other's compute waves keep the matrix pipe busy: the MFMA stream
-// and the store stream overlap across workgroups instead of serialising inside one wave. Slot = [compute wave][band
-// row j][64 realizations] + [j][32 TOAs] weights (9 KB); a producer fills its compute wave's 4 rows with two direct-
-// to-LDS loads (two rows per instruction, 32 lanes each) and one weight row.
-constexpr int kWs2Slots = kWsLead + 1;
-constexpr int kWs2SlotGrid = 4 * 4 * 64;
-constexpr int kWs2Slot = kWs2SlotGrid + 4 * kGridTT;
-constexpr int kWs2LoadsPerStep = 3;
-
-__device__ __forceinline__ void ws2_wait_steps(int n) {
-  if (n <= 0) ws_wait_vm<0>();
-  else if (n == 1) ws_wait_vm<kWs2LoadsPerStep>();
-  else if (n == 2) ws_wait_vm<2 * kWs2LoadsPerStep>();
-  else if (n == 3) ws_wait_vm<3 * kWs2LoadsPerStep>();
-  else if (n == 4) ws_wait_vm<4 * kWs2LoadsPerStep>();
-  else if (n == 5) ws_wait_vm<5 * kWs2LoadsPerStep>();
-  else ws_wait_vm<6 * kWs2LoadsPerStep>();
-}
-
-template <bool PART>
-__global__ __launch_bounds__(512, 2) void k_grid_interp_ws2(SynthArgs a, GridBand band, int32_t n_tiles, int32_t R_pad,
-                                                            double* __restrict__ out) {
-  constexpr int RW = 4, NP = RW / 2;
-  static_assert(kGridTT == 32, "two 16-TOA B-tiles per chunk");
-  __shared__ __attribute__((aligned(16))) double ring[kWs2Slots * kWs2Slot];
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  const int lr = lane & 15, lg = lane >> 4;
-  const int per = (n_tiles + 7) >> 3;
-  const int x = blockIdx.x & 7;
-  const int stride = gridDim.x >> 3;
-  const int end = min(n_tiles, (x + 1) * per);
-  const int first = x * per + (int)(blockIdx.x >> 3);
-  const int n_rb = (R_pad + 255) / 256;
-  const bool producer = wave >= 4;
-  const int w = wave & 3;
-  if (first >= end) return;
-
-  if (producer) {
-    int tile = first, q = 0, nq = 0, c = 0, r0 = 0;
-    auto setup = [&]() {
-      c = __builtin_amdgcn_readfirstlane(tile / n_rb);
-      const int rb = __builtin_amdgcn_readfirstlane(tile - c * n_rb);
-      r0 = rb * 256 + w * 64;
-      if (r0 >= R_pad) r0 = 0;  // a compute wave past R_pad: valid rows, its sums are never stored
-      nq = __builtin_amdgcn_readfirstlane(ld_uniform4(band.chunks + c).w) >> 2;
-    };
-    int issued = 0;
-    bool valid = true;
-    setup();
-    auto issue = [&]() {
-      double* slot = ring + (issued % kWs2Slots) * kWs2Slot;
-      const int4 r4 = ld_uniform4(band.rows + (int64_t)c * band.vmax + 4 * q);  // the step's 4 rows
-      const int hl = lane >> 5, l32 = lane & 31;
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {  // rows 2h (lanes 0..31) and 2h + 1 (lanes 32..63)
-        const int ra = __builtin_amdgcn_readfirstlane(h == 0 ? r4.x : r4.z);
-        const int rb2 = __builtin_amdgcn_readfirstlane(h == 0 ? r4.y : r4.w);
-        const int row = hl ? rb2 : ra;
-        FPTA_DCHECK(row >= 0 && row < band.grid_rows, "k_grid_interp_ws2 grid row", row, band.grid_rows);
-        __builtin_amdgcn_global_load_lds((const void*)(band.g + (int64_t)row * R_pad + r0 + 2 * l32),
-                                         (__attribute__((address_space(3))) void*)(slot + (w * 4 + 2 * h) * 64), 16,
-                                         0, 0);
-      }
-      __builtin_amdgcn_global_load_lds(
-          (const void*)((const uint32_t*)(band.wd + ((int64_t)c * band.vmax + 4 * q + w) * kGridTT) + lane),
-          (__attribute__((address_space(3))) void*)(slot + kWs2SlotGrid + w * kGridTT), 4, 0, 0);
-      ++issued;
-      if (++q == nq) {
-        q = 0;
-        tile += stride;
-        valid = tile < end;
-        if (valid) setup();
-      }
-    };
-    for (int i = 0; i < kWsLead && valid; ++i) issue();
-    ws2_wait_steps(issued - 1);
-    ws_barrier();
-    for (int S = 0;; ++S) {
-      if (valid) issue();
-      ws2_wait_steps(issued - (S + 2));
-      if (S + 1 >= issued && !valid) {
-        ws_barrier();
-        break;
-      }
-      ws_barrier();
-    }
-    return;
-  }
-
-  d4 acc[2][RW];
-#pragma unroll
-  for (int e = 0; e < 2; ++e)
-#pragma unroll
-    for (int i = 0; i < RW; ++i) acc[e][i] = d4{0.0, 0.0, 0.0, 0.0};
-  auto read = [&](int S, dbl2(&av)[NP], dbl2& bv) {
-    const double* slot = ring + (S % kWs2Slots) * kWs2Slot;
-#pragma unroll
-    for (int m = 0; m < NP; ++m) av[m] = *(const dbl2*)(slot + (w * 4 + lg) * 64 + 32 * m + 2 * lr);
-    bv = *(const dbl2*)(slot + kWs2SlotGrid + lg * kGridTT + 2 * lr);
-  };
-  auto mfma = [&](const dbl2(&av)[NP], const dbl2& bv) {
-#pragma unroll
-    for (int m = 0; m < NP; ++m) {
-      acc[0][2 * m] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m].x, bv.x, acc[0][2 * m], 0, 0, 0);
-      acc[0][2 * m + 1] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m].y, bv.x, acc[0][2 * m + 1], 0, 0, 0);
-      acc[1][2 * m] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m].x, bv.y, acc[1][2 * m], 0, 0, 0);
-      acc[1][2 * m + 1] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m].y, bv.y, acc[1][2 * m + 1], 0, 0, 0);
-    }
-  };
-  dbl2 a0[NP], a1[NP], b0, b1;
-  ws_barrier();
-  read(0, a0, b0);
-  ws_wait_lgkm0();
-  int S = 0;
-  for (int tile = first; tile < end; tile += stride) {
-    InterpTile<RW> t;
-    t.c = __builtin_amdgcn_readfirstlane(tile / n_rb);
-    const int rb = __builtin_amdgcn_readfirstlane(tile - t.c * n_rb);
-    t.r0 = rb * 256 + w * 64;
-    const int4 ci = ld_uniform4(band.chunks + t.c);
-    t.p = __builtin_amdgcn_readfirstlane(ci.x);
-    t.y = __builtin_amdgcn_readfirstlane(ci.y);
-    t.cnt = __builtin_amdgcn_readfirstlane(ci.z);
-    t.nq = __builtin_amdgcn_readfirstlane(ci.w) >> 2;
-    for (int q = 0; q < t.nq; ++q, ++S) {
-      ws_barrier();
-      read(S + 1, a1, b1);
-      mfma(a0, b0);
-      ws_wait_lgkm0();
-#pragma unroll
-      for (int m = 0; m < NP; ++m) a0[m] = a1[m];
-      b0 = b1;
-    }
-    if (t.r0 < R_pad) interp_store<PART, RW>(a, out, t, acc);
-#pragma unroll
-    for (int e = 0; e < 2; ++e)
-#pragma unroll
-      for (int i = 0; i < RW; ++i) acc[e][i] = d4{0.0, 0.0, 0.0, 0.0};
-  }
-}
+#ifdef FPTA_DIAG_KERNELS
+#include "diag/interp_ws2.inc"
+#endif
 
 hipError_t launch_grid_interp_ws(hipStream_t st, const SynthArgs& a, const GridBand& band, int32_t R_pad, bool ws2) {
   if (band.n_chunks <= 0 || band.vmax < 4 || band.vmax % 4 != 0 || band.vmax > kGridVMax || R_pad % 128 != 0 ||
@@ -1048,13 +907,17 @@ hipError_t launch_grid_interp_ws(hipStream_t st, const SynthArgs& a, const GridB
   }
   // persistent: one workgroup per CU (the 4-slot ring takes 4 x 17 KB = 68 KB of the 160 KB LDS)
   const int64_t grid = std::min<int64_t>((tiles + 7) / 8 * 8, ((int64_t)n_cu + 7) / 8 * 8);
-  if (ws2) {  // 256-realization tiles, two workgroups per CU
+  if (ws2) {  // 256-realization tiles, two workgroups per CU (diagnostic builds only)
+#ifndef FPTA_DIAG_KERNELS
+    return hipErrorInvalidValue;
+#else
     if (a.part) return hipErrorInvalidValue;
     const int64_t tiles2 = (int64_t)band.n_chunks * ((R_pad + 255) / 256);
     if (tiles2 > 0x7FFFFFFF) return hipErrorInvalidValue;
     const int64_t grid2 = std::min<int64_t>((tiles2 + 7) / 8 * 8, (2 * (int64_t)n_cu + 7) / 8 * 8);
     hipLaunchKernelGGL(k_grid_interp_ws2<false>, dim3((unsigned)grid2), dim3(512), 0, st, a, band, (int32_t)tiles2,
                        R_pad, a.out);
+#endif
   } else if (a.part)
     hipLaunchKernelGGL(k_grid_interp_ws<true>, dim3((unsigned)grid), dim3(512), 0, st, a, band, (int32_t)tiles, R_pad,
                        a.out);

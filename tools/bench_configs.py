@@ -92,12 +92,21 @@ def c1():
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
-def _interp_entry(gi, n_toa, R, ms):
+def _interp_entry(gi, n_toa, R, ms, K=None, traffic_R=None):
     """The interpolation kernel of a config's last block (the dominant kernel) and its HBM fraction: 8 B per residual
-    sample written over its isolated (one-stream) launch time."""
+    sample written over its isolated (one-stream) launch time; with the newest matching PMC record
+    under profiles/ (tools/gpu_evidence6.sh: FETCH_SIZE doubled + WRITE_SIZE of the same kernel and shape), its HBM
+    bytes per launch over the algorithmic bytes."""
     gbs = 8.0 * n_toa * R / (ms / 1e3) / 1e9 if ms else None
-    return dict(kernel=gi["interp_kernel"], avg_launch_ms=ms, algorithmic_bytes=8.0 * n_toa * R, achieved_GBps=gbs,
-                frac=gbs / HBM_PEAK_GBS if gbs else None)
+    entry = dict(kernel=gi["interp_kernel"], avg_launch_ms=ms, algorithmic_bytes=8.0 * n_toa * R, achieved_GBps=gbs,
+                 frac=gbs / HBM_PEAK_GBS if gbs else None)
+    if K is not None and gi["interp_kernel"]:
+        import bench
+        RR = traffic_R or R
+        traffic, src = bench.pmc_traffic(gi["interp_kernel"], {"K": K, "n_toa": n_toa}, RR, None)
+        entry.update(traffic_bytes=traffic, traffic_source=src,
+                     traffic_over_algorithmic=traffic / (8.0 * n_toa * RR) if traffic else None)
+    return entry
 
 
 def c3_job(total=100000, batch=7168, jobs=2):
@@ -126,7 +135,7 @@ def c3_job(total=100000, batch=7168, jobs=2):
     gi = ctx.batch_grid_info()
     ctx.close()
     n_batches = -(-total // batch)
-    entry = _interp_entry(gi, info["n_toa"], total / n_batches, ms / max(n, 1))
+    entry = _interp_entry(gi, info["n_toa"], total / n_batches, ms / max(n, 1), K=info["K"], traffic_R=batch)
     entry["note"] = "average over the job's batches (the short last one included), pipelined (HIP events)"
     return dict(job_ms=dt * 1e3, samples_per_s=info["n_toa"] * total / dt, realizations=total, batch=batch,
                 checksum=float(np.sum(sums[:, 1])), interp=entry)
@@ -221,7 +230,7 @@ def c4(steps=5):
     ctx.close()
     return dict(config="c4", K=2 * N, n_toa=P * n_p, realizations=R, ms_per_step=dt / steps * 1e3,
                 samples_per_s=P * n_p * R * steps / dt, isolated_kernels_ms_per_step=kt1,
-                interp=_interp_entry(gi, P * n_p, R, kt1["synth"]),
+                interp=_interp_entry(gi, P * n_p, R, kt1["synth"], K=2 * N),
                 path=gi["last_path"],
                 synth_direct_equiv_tflops=flops / ((kt1["synth"] + kt1["grid"]) / 1e3) / 1e12,
                 mix_factor="cholesky" if np.all(np.triu(L, 1) == 0) else "svd",
@@ -268,7 +277,7 @@ def c5(steps=10):
     ctx.close()
     return dict(config="c5", K=info["K"], n_toa=info["n_toa"], realizations=R, ms_per_step=dt / steps * 1e3,
                 samples_per_s=info["n_toa"] * R * steps / dt, isolated_kernels_ms_per_step=kt,
-                interp=_interp_entry(gi, info["n_toa"], R, kt["synth"]),
+                interp=_interp_entry(gi, info["n_toa"], R, kt["synth"], K=info["K"]),
                 step_ms_per_gb_written=dt / steps * 1e3 / (8.0 * info["n_toa"] * R / 1e9),
                 synth_direct_equiv_tflops=2.0 * info["K"] * info["n_toa"] * R / ((kt["synth"] + kt["grid"]) / 1e3) / 1e12,
                 path=gi["last_path"], n_ecorr_blocks=len(sim.blocks))
