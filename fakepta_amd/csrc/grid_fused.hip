@@ -34,6 +34,9 @@
 
 namespace fpta {
 
+#ifndef FPTA_FUSED_DFT_PRIO
+#define FPTA_FUSED_DFT_PRIO 3  // issue priority of the DFT waves (round 5: 3 beat 1 and 0 on C2)
+#endif
 #ifndef FPTA_HALF_STORE16
 #define FPTA_HALF_STORE16 0  // HALF: 1 = lanes swap values (DPP) for 16-byte stores (measured slower than 8-byte stores)
 #endif
@@ -402,7 +405,7 @@ __global__ __launch_bounds__(64 * (kFusedIW + kFusedDW), 1) void k_grid_fused(Sy
     const int dw = wave - kFusedIW;
     // the DFT waves are the item's critical path (the interpolation waves wait at barrier A): first claim on the SIMD's
     // issue slots, the interpolation waves fill the gaps (C2 kernel -3%)
-    __builtin_amdgcn_s_setprio(3);
+    __builtin_amdgcn_s_setprio(FPTA_FUSED_DFT_PRIO);
     int js = -1, jrc = 0;  // this wave's job: grid signal js, quarter-range rows 32 jrc .. 32 jrc + 31
     {
       int j = dw;
