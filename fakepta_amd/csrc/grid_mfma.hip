@@ -918,10 +918,16 @@ hipError_t launch_grid_interp_ws(hipStream_t st, const SynthArgs& a, const GridB
     hipLaunchKernelGGL(k_grid_interp_ws2<false>, dim3((unsigned)grid2), dim3(512), 0, st, a, band, (int32_t)tiles2,
                        R_pad, a.out);
 #endif
-  } else if (a.part)
+  } else if (a.part) {
+    // fused partial checksums on this kernel: FPTA_OPT_INTERP_WS 2, variant builds only (slower than the register
+    // kernel on C3); the instance is not in the product library
+#ifdef FPTA_DIAG_KERNELS
     hipLaunchKernelGGL(k_grid_interp_ws<true>, dim3((unsigned)grid), dim3(512), 0, st, a, band, (int32_t)tiles, R_pad,
                        a.out);
-  else
+#else
+    return hipErrorInvalidValue;
+#endif
+  } else
     hipLaunchKernelGGL(k_grid_interp_ws<false>, dim3((unsigned)grid), dim3(512), 0, st, a, band, (int32_t)tiles, R_pad,
                        a.out);
   return hipGetLastError();

@@ -127,7 +127,10 @@ __device__ __forceinline__ void normals4(u32x4 v, double (&z)[4]) {
   bm_sincos2pi_u32(v.y, s, c);
   z[0] = r0 * c;
   z[1] = r0 * s;
-  __builtin_amdgcn_sched_barrier(0);  // the two pairs one after the other: half the live temporaries
+#ifndef FPTA_NORMALS4_SPLIT
+#define FPTA_NORMALS4_SPLIT 1  // variant builds: 0 lets the scheduler interleave the two Box-Muller pairs
+#endif
+  if (FPTA_NORMALS4_SPLIT) __builtin_amdgcn_sched_barrier(0);  // the two pairs one after the other: half the live temporaries
   const double r1 = bm_sqrt(-2.0 * bm_log_u32(v.z));
   bm_sincos2pi_u32(v.w, s, c);
   z[2] = r1 * c;
