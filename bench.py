@@ -84,6 +84,10 @@ def parse():
     ap.add_argument("--no-kernel-events", action="store_true",
                     help="diagnostic: no per-kernel HIP events in the timed region (the roofline's launch time is then "
                          "unmeasured; for the events' own cost)")
+    ap.add_argument("--event-every", type=int, default=4,
+                    help="c2: per-kernel HIP events on every N-th timed step (steps 0, N, 2N, ...): the roofline's "
+                         "average launch time from those launches (events put ~10 us of command-processor work "
+                         "between two launches, profiles/round6/r6_kernel_events_cost.txt); 1 = every step")
     ap.add_argument("--overlap", type=int, default=-1,
                     help="FPTA_OPT_OVERLAP: 1 pipelined blocks (side stream), 0 one stream (-1: library default)")
     ap.add_argument("--opt", action="append", default=[],
@@ -404,7 +408,10 @@ def main():
         comm.barrier()
         ctx.synchronize()
         t0 = time.perf_counter()
+        every = max(1, args.event_every)
         for s in range(args.steps):
+            if not args.no_kernel_events and every > 1:
+                ctx.set_option(_capi.OPT_PROFILE, 1 if s % every == 0 else 0)
             sim.synth(R, seed=args.seed, real0=((args.warmup + s) * world + rank) * R, to_host=False)
         ctx.synchronize()
         comm.barrier()
@@ -435,6 +442,7 @@ def main():
     ctx.set_option(_capi.OPT_PROFILE, 0)
     value = n_samples_total / dt
     synth_avg_s = kernel_avg_s(ctx, _capi.K_SYNTH) or float("nan")  # nan: --no-kernel-events
+    synth_n = ctx.kernel_stats(_capi.K_SYNTH)[0]  # launches timed by events (--event-every)
     gi = ctx.batch_grid_info()
     path = gi["last_path"]
     # algorithmic bytes of one synthesis launch: 8 B per residual sample written; one launch
@@ -464,6 +472,7 @@ def main():
         roofline = {"bound": "hbm", "pipe": pipe, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": kernel,
                     "algorithmic_bytes_per_launch": out_bytes, "avg_launch_ms": synth_avg_s * 1e3,
+                    "event_launches": synth_n,
                     "traffic_over_algorithmic": (traffic / out_bytes) if traffic else None,
                     "traffic_source": traffic_src,
                     "implementation_bytes_per_launch": impl_bytes,

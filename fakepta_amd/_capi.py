@@ -106,11 +106,12 @@ OPT_SYNTH_PATH, OPT_MFMA_MIN_REAL, OPT_PROFILE, OPT_ANCHOR, OPT_VALU_VARIANT, OP
 OPT_GRID_WIDTH, OPT_GRID_SIGMA, OPT_GRID_MFMA, OPT_FUSE_CHECKSUMS = 7, 8, 9, 10
 OPT_MIX_MFMA, OPT_OVERLAP, OPT_INTERP_LDS, OPT_GRID_COALESCE, OPT_INTERP_WS, OPT_SIDE_SPLIT = 11, 12, 13, 14, 15, 16
 OPT_DFT_GEN, OPT_GEN_MIX, OPT_ASYNC_SUMS, OPT_PART_GROUP, OPT_INTERP_PSR, OPT_INTERP_WR = 17, 18, 19, 20, 21, 22
-OPT_INTERP_FUSED, OPT_FUSED_WHITE = 23, 24
+OPT_INTERP_FUSED, OPT_FUSED_WHITE, OPT_FUSED_NEXT_MIX = 23, 24, 25
 OPTIONS = (OPT_SYNTH_PATH, OPT_MFMA_MIN_REAL, OPT_PROFILE, OPT_ANCHOR, OPT_VALU_VARIANT, OPT_FUSE_WHITE,
            OPT_GRID_WIDTH, OPT_GRID_SIGMA, OPT_GRID_MFMA, OPT_FUSE_CHECKSUMS, OPT_MIX_MFMA, OPT_OVERLAP,
            OPT_INTERP_LDS, OPT_GRID_COALESCE, OPT_INTERP_WS, OPT_SIDE_SPLIT, OPT_DFT_GEN, OPT_GEN_MIX,
-           OPT_ASYNC_SUMS, OPT_PART_GROUP, OPT_INTERP_PSR, OPT_INTERP_WR, OPT_INTERP_FUSED, OPT_FUSED_WHITE)
+           OPT_ASYNC_SUMS, OPT_PART_GROUP, OPT_INTERP_PSR, OPT_INTERP_WR, OPT_INTERP_FUSED, OPT_FUSED_WHITE,
+           OPT_FUSED_NEXT_MIX)
 K_GEN, K_MIX, K_SYNTH, K_WHITE, K_DENSE, K_GRID = 0, 1, 2, 3, 4, 5
 
 
@@ -344,7 +345,7 @@ class Context:
     def batch_grid_info(self):
         """Gridded-path plan figures, the path of the last batch and why it was not the gridded path
         (fpta_batch_grid_info_n, fpta_batch_path_reason)."""
-        g = np.zeros(17, dtype=np.float64)
+        g = np.zeros(19, dtype=np.float64)
         self._check(_lib.fpta_batch_grid_info_n(self._h, _ptr(g), len(g)), "fpta_batch_grid_info_n")
         keys = ("last_path", "ok", "n_chunks", "fma_dft", "fma_interp", "fma_direct", "grid_vals", "weight_bytes",
                 "grid_mfma", "err_bound", "width", "sigma", "grid_signals", "signals", "band_rows_per_chunk")
@@ -360,6 +361,10 @@ class Context:
         d["path_reason"] = _lib.fpta_batch_path_reason(self._h).decode()
         d["interp_kernel"] = interp_kernel_name(int(g[15]))
         d["fma_interp_run"] = fma_run if fma_run > 0 else d["fma_interp"]
+        # slots 17, 18: the last block's kernel made the next block's common-signal mix / the last block took its mix
+        # from the previous block's kernel (FPTA_OPT_FUSED_NEXT_MIX)
+        d["next_mix_made"] = bool(g[17])
+        d["next_mix_used"] = bool(g[18])
         return d
 
     def batch_synth(self, seed, real0, n_real, to_host=True, coeffs=False):

@@ -211,6 +211,7 @@ int layout_finalize(fpta_ctx* c, Layout& L) {
   }
   HIPCHK(c, hipStreamSynchronize(c->stream), "segdesc sync");
   L.dirty = false;
+  ++L.version;
   return FPTA_OK;
 }
 
@@ -277,6 +278,28 @@ bool coef_in_interp(const fpta_ctx* c, const Layout& L) {
   return psr_layout(c, L) || fused_layout(c, L) || fused_w_layout(c, L);
 }
 
+// FPTA_OPT_FUSED_NEXT_MIX: the common signal whose k_gen_mix a pipelined block of L (R_pad realizations) can take from
+// the previous block's k_grid_fused (FusedMix), or -1: the layout's only common signal, of kMixTiledMinP ..
+// kFusedMixMaxP pulsars, mixed by k_gen_mix (run_coefficients' branch) into its own columns; every per-pulsar signal
+// drawn inside its grid signal's DFT, so the block launches nothing else before its kernel.
+int32_t next_mix_seg(const fpta_ctx* c, const Layout& L, int32_t R_pad) {
+  if (!c->fused_next_mix || !c->overlap || !c->gen_mix || !c->mix_mfma || L.P < kMixTiledMinP || L.P > kFusedMixMaxP ||
+      L.P > kGenMixMaxP || R_pad % 128 != 0 || !L.grid.built || !L.grid.ok || !fused_layout(c, L))
+    return -1;
+  int32_t seg = -1;
+  for (size_t g = 0; g < L.grid.members.size(); ++g)
+    for (int32_t i : L.grid.members[g]) {
+      const SegDesc& d = L.segs[i]->d;
+      if (d.kind == 1) {
+        if (seg >= 0 || !d.LT || !grid_gen_fused(c, L, g)) return -1;
+        seg = i;
+      } else if (!grid_gen_fused(c, L, g)) {
+        return -1;
+      }
+    }
+  return seg;
+}
+
 // merge: the gridded plan of L coalesces signals (GridPlan::members): after the last member of a grid signal is
 // drawn, k_coef_merge adds the other members' columns into the anchor's. coef_host (optional, with merge): the
 // per-signal coefficients [P][K][R] are downloaded before any merge and *coef_done is set.
@@ -287,6 +310,20 @@ int run_coefficients(fpta_ctx* c, Layout& L, uint64_t seed, int64_t real0, int32
   const int32_t P = L.P;
   int rc0 = wait_coef_all(c);  // a previous block's draws are fully ordered before this one's
   if (rc0) return rc0;
+  // FPTA_OPT_FUSED_NEXT_MIX: the previous block's k_grid_fused made this block's mix of common signal nm_seg if this
+  // is the block it was made for (the key, pipelined, the buffer this block swaps in, k_gen_mix's branch below);
+  // otherwise that kernel may still be writing the buffer: the ctx stream is waited for before anything here
+  const fpta_ctx::NextMix nmx = c->next_mix;
+  c->next_mix.valid = false;
+  c->next_mix_used = false;
+  int32_t nm_seg = -1;
+  if (nmx.valid) {
+    if (nmx.layout == &L && nmx.version == L.version && nmx.seed == seed && nmx.real0 == real0 && nmx.n_real == R &&
+        nmx.R_pad == R_pad && pipe && side && merge && !zin && !x_out && !coef_host && nmx.seg == next_mix_seg(c, L, R_pad))
+      nm_seg = nmx.seg;
+    else
+      HIPCHK(c, hipStreamSynchronize(c->stream), "next mix sync");
+  }
   hipStream_t st = c->stream;
   const bool use_side = side && (L.segs.size() > 1 || pipe);
   const bool last_side = c->coef_last_side;
@@ -298,6 +335,10 @@ int run_coefficients(fpta_ctx* c, Layout& L, uint64_t seed, int64_t real0, int32
   if (psr && c->coef_slot != c->gbuf) {
     c->coef.swap(c->coef2);
     c->coef_slot = c->gbuf;
+  }
+  if (nm_seg >= 0 && !(psr && c->coef.p == nmx.buf)) {
+    HIPCHK(c, hipStreamSynchronize(c->stream), "next mix sync");
+    nm_seg = -1;
   }
   const size_t coef_bytes = sizeof(double) * (size_t)P * std::max(L.K, 1) * R_pad;
   if (c->side && c->coef.cap < coef_bytes) HIPCHK(c, hipStreamSynchronize(c->side), "side sync");  // before a regrow
@@ -392,6 +433,7 @@ int run_coefficients(fpta_ctx* c, Layout& L, uint64_t seed, int64_t real0, int32
     HIPCHK(c, hipStreamWaitEvent(c->side2, c->ev_s2begin, 0), "side wait");
   }
   auto stream_of = [&](int32_t g) { return g >= 0 && g == c->split_g ? c->side2 : st; };
+  int n_launch = 0;  // kernels (and copies) this call queues
   auto merge_group = [&](size_t g) -> int {
     CoefMerge m{};
     m.dst = L.segs[G.anchor[g]]->d.col0;
@@ -402,16 +444,30 @@ int run_coefficients(fpta_ctx* c, Layout& L, uint64_t seed, int64_t real0, int32
         m.ncol[m.n++] = 2 * L.segs[i]->d.nm;
       }
     if (m.n == 0) return FPTA_OK;  // every member was added inside its mix
+    ++n_launch;
     hipStream_t sg = stream_of((int32_t)g);
     KTimer kt(c, FPTA_K_GEN, sg);
     HIPCHK(c, launch_coef_merge(sg, m, P, L.K, R_pad, c->coef.as<double>()), "k_coef_merge launch");
     return FPTA_OK;
   };
+  auto gen_mix_branch = [&](size_t i) {
+    const SegDesc& d = L.segs[i]->d;
+    return d.kind == 1 && c->gen_mix && mfma_mix && !zin && !x_out && fuse_into[i] < 0 && P <= kGenMixMaxP;
+  };
+  if (nm_seg >= 0 && !gen_mix_branch((size_t)nm_seg)) {
+    HIPCHK(c, hipStreamSynchronize(c->stream), "next mix sync");
+    nm_seg = -1;
+  }
   for (size_t i = 0; i < L.segs.size(); ++i) {
     const SegDesc& d = L.segs[i]->d;
     hipStream_t si = stream_of(group_of[i]);  // side2 only for members of split_g (kind 0: no mixing below)
     if (in_fused[i] && d.kind == 0) continue;  // drawn inside its grid signal's DFT
-    if (d.kind == 1 && c->gen_mix && mfma_mix && !zin && !x_out && fuse_into[i] < 0 && P <= kGenMixMaxP) {
+    if ((int32_t)i == nm_seg) {
+      c->next_mix_used = true;  // made by the previous block's kernel into this buffer (ordered on the ctx stream)
+      continue;
+    }
+    ++n_launch;
+    if (gen_mix_branch(i)) {
       KTimer kt(c, FPTA_K_MIX, st, true);  // draws + mixing in one kernel, into the signal's own columns
       // 16-realization workgroups (FPTA_OPT_GEN_MIX 3: they fit in the LDS two k_grid_interp_psr workgroups leave;
       // C3 measured the same either way, profiles/round4/R5d)
@@ -467,6 +523,7 @@ int run_coefficients(fpta_ctx* c, Layout& L, uint64_t seed, int64_t real0, int32
   }
   c->coef_side = st != c->stream && !pipe;  // pipelined: the DFT follows on the same stream, no per-signal events
   c->prev_psr = psr;
+  c->coef_queued = n_launch > 0 || defer;
   return FPTA_OK;
 }
 
@@ -939,6 +996,9 @@ int fpta_set_option(fpta_ctx* c, int32_t key, int64_t value) {
     case FPTA_OPT_FUSED_WHITE:
       c->fused_white = value ? 1 : 0;
       return FPTA_OK;
+    case FPTA_OPT_FUSED_NEXT_MIX:
+      c->fused_next_mix = value ? 1 : 0;
+      return FPTA_OK;
     case FPTA_OPT_INTERP_WR:
 #ifndef FPTA_DIAG_KERNELS
       if (value) return fail(c, FPTA_EINVAL, "interp_wr: k_grid_interp_wr is a diagnostic kernel, not in this build");
@@ -1008,6 +1068,7 @@ int fpta_get_option(fpta_ctx* c, int32_t key, int64_t* value) {
     case FPTA_OPT_INTERP_WR: *value = c->interp_wr; return FPTA_OK;
     case FPTA_OPT_INTERP_FUSED: *value = c->interp_fused; return FPTA_OK;
     case FPTA_OPT_FUSED_WHITE: *value = c->fused_white; return FPTA_OK;
+    case FPTA_OPT_FUSED_NEXT_MIX: *value = c->fused_next_mix; return FPTA_OK;
   }
   return fail(c, FPTA_EINVAL, "get_option: unknown key");
 }
@@ -1346,6 +1407,7 @@ int batch_common(fpta_ctx* c, uint64_t seed, int64_t real0, int32_t n_real, cons
   c->out_R = n_real;
   c->out_ld = L.n_toa;
   c->part_ready = false;  // set by the gridded interpolation when it writes this block's partial checksums
+  c->next_mix_made = false;  // set by a k_grid_fused launch that also mixes the next block's common signal
   const bool do_white = white && (c->has_sigma || c->has_blocks);
   const uint32_t k0 = (uint32_t)(seed & 0xFFFFFFFFull), k1 = (uint32_t)(seed >> 32);
   WhiteCfg wc{};
@@ -1594,6 +1656,8 @@ int fpta_batch_grid_info_n(fpta_ctx* c, double* dst, int32_t n_out) {
   out[14] = ok ? G.mean_v : 0.0;
   out[15] = c->last_interp;
   out[16] = ok ? (c->last_fma_interp > 0.0 ? c->last_fma_interp : G.fma_interp) : 0.0;
+  out[17] = c->next_mix_made ? 1.0 : 0.0;
+  out[18] = c->next_mix_used ? 1.0 : 0.0;
   std::memcpy(dst, out, sizeof(double) * std::min<int32_t>(n_out, FPTA_GRID_INFO_LEN));
   return FPTA_GRID_INFO_LEN;
 }

@@ -200,6 +200,7 @@ struct Layout {
   DevBuf segdesc;
   int32_t K = 0;
   bool dirty = true;
+  uint64_t version = 0;  // bumped by every layout_finalize that rebuilds (signals, TOAs changed)
   // recurrence seeds [n_seg][n_toa] (double4), valid when every segment is harmonic
   DevBuf seeds;
   bool all_harmonic = false;
@@ -270,6 +271,20 @@ struct fpta_ctx {
   DevBuf coef2;
   int coef_slot = 0;
   bool prev_psr = false;
+  // FPTA_OPT_FUSED_NEXT_MIX: the last k_grid_fused launch also made the mix of common signal `seg` for the block
+  // (layout, version, seed, real0, n_real, R_pad) into buffer `buf` (c->coef2 then, c->coef once that block swaps).
+  // run_coefficients takes it when the next block has exactly that key, else waits for the ctx stream first.
+  int fused_next_mix = 1;
+  struct NextMix {
+    bool valid = false;
+    const Layout* layout = nullptr;
+    uint64_t version = 0, seed = 0;
+    int64_t real0 = 0;
+    int32_t n_real = 0, R_pad = 0, seg = -1;
+    const void* buf = nullptr;
+  } next_mix;
+  bool next_mix_made = false, next_mix_used = false;  // fpta_batch_grid_info_n slots 17, 18 of the last block
+  bool coef_queued = true;  // the last run_coefficients queued work (a pipelined block that queued none: no grid-ready wait)
   int async_sums = 0;    // streamed jobs: partial-checksum reductions on their own stream (FPTA_OPT_ASYNC_SUMS; measured
                          // no faster on C3, profiles/r03h_ab_c3_async_sums.txt: the reductions then compete with the interpolation)
   int gen_mix = 2;       // common signals of 64..256 pulsars: draws and ORF mixing in one kernel (k_gen_mix,
@@ -420,6 +435,7 @@ bool grid_gen_fused(const fpta_ctx* c, const Layout& L, size_t g);
 bool psr_layout(const fpta_ctx* c, const Layout& L);
 bool fused_layout(const fpta_ctx* c, const Layout& L);
 bool fused_w_layout(const fpta_ctx* c, const Layout& L);
+int32_t next_mix_seg(const fpta_ctx* c, const Layout& L, int32_t R_pad);
 int batch_common(fpta_ctx* c, uint64_t seed, int64_t real0, int32_t n_real, const double* zin, int32_t zin_nm,
                  double* out, double* coeffs_out, bool white);
 int launch_block_checksums(fpta_ctx* c, bool async = false, hipStream_t* used = nullptr, double* dst = nullptr,

@@ -235,6 +235,24 @@ struct FusedHalf {
   const double* wd;      // [2 n_chunks][vmax][16] weights (fused_half_weight_index), + zero rows past the last
   int32_t fq, vmax;      // band steps per (chunk, half, j) in lrows (a multiple of 4); band rows per half (mult. of 8)
 };
+// The next block's common-signal draws + ORF mix (k_gen_mix's work for one signal) as spare-time tickets of
+// k_grid_fused: a pipelined block whose successor is predictable (the same key, the next realizations) lets its
+// kernel's waves with nothing left to interpolate or build make that block's mixed coefficients, so the successor
+// launches no k_gen_mix. A ticket is one (mode, 16 realizations, 64 pulsars) tile: the pulsars' coefficients of both
+// columns, the draws in registers (one Philox call per lane and k-step), the mix on fp64 MFMA per 16-pulsar tile.
+// Bit-identical to k_gen_mix (the same normals, the same products per k-step in the same order: k-steps past a
+// triangular factor's diagonal add exact zeros there). DESIGN.md §5a.
+constexpr int kFusedMixMaxP = 256;   // pulsars of a signal whose mix k_grid_fused makes (k_gen_mix's limit)
+constexpr int kFusedMixGroup = 112;  // pulsars per ticket (seven 16-pulsar MFMA tiles, both columns: 112 VGPRs of sums)
+struct FusedMix {
+  const double* LT;     // SegDesc::LT of the signal (zero-padded L^T)
+  const double* amp;    // [nm] mode amplitudes
+  double* coef;         // the successor's coefficient buffer [P][K][R_pad]
+  int64_t real0;        // the successor's first realization
+  uint32_t k0, k1;      // its Philox key
+  int32_t lt_ld, lt_rows, P, K, col0, R_pad, n_real, n_q, lower, seg, nm;
+  int32_t n_tiles;      // nm x R_pad / 16 x ceil(P / 64) tickets; 0: no successor mix in this launch
+};
 constexpr int kFusedArgSig = 3;  // grid signal descriptors a FusedArgs holds (k_grid_fused takes kFusedMaxSig of them)
 struct FusedArgs {
   FusedSig s[kFusedArgSig];
@@ -251,11 +269,13 @@ struct FusedArgs {
   FusedHalf h;               // half-chunk bands (HALF kernels only; else zero)
   int32_t cu_pct;            // host only: workgroups for this percentage of the CUs (0 = all), leaving the rest to a
                              // co-running kernel (the next block's ORF mix)
+  FusedMix mix;              // the successor block's common-signal mix (k_grid_fused only; n_tiles 0 = none)
 };
 #ifndef FPTA_FUSED_MIX_CU_PCT
 #define FPTA_FUSED_MIX_CU_PCT 100  // CUs of k_grid_fused's grid while the next block's k_mix_mfma may co-run
 #endif
-constexpr int kFusedQueueWords = 9;  // 8 per-XCD item tickets + the count of finished workgroups
+constexpr int kFusedQueueWords = 10;  // 8 per-XCD item tickets, the count of finished workgroups, the mix tickets
+constexpr int kFusedMixWord = 9;
 #ifndef FPTA_FUSED_JOIN_SAFETY
 #define FPTA_FUSED_JOIN_SAFETY 1.5  // measured best of 0.5 .. 5 on C2 and C4 (profiles/round5/r5mn_*); variants may change it (make variant DEFS=-DFPTA_FUSED_JOIN_SAFETY=...)
 #endif

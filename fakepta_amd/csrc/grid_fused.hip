@@ -72,6 +72,95 @@ struct FusedOpsH {
   int row[2][NS];      // LDS grid row of band row 4 q + lg of half h
 };
 
+// One ticket of the successor block's mix (FusedMix): mode k, realizations 16 rg .. 16 rg + 15, pulsars
+// kFusedMixGroup pg .. (seven 16-pulsar tiles), both columns. Lane (lr, lg) draws realization 16 rg + lr at k-step row
+// q0 + lg: k_gen_mix's normals of (k, q, g) are the B operand; A = L^T[q][16 t + lr] of tile t, one MFMA per (tile,
+// column) while the tile's k-steps last (k_gen_mix's bound at 16-pulsar granularity: the steps it runs past them have
+// zero factors there). Two k-steps per trip: with an even first realization the lanes of a realization pair share
+// Philox counters, so each computes one of the two steps' Philox calls and they swap the halves the other needs (one
+// DPP exchange of two words); each lane then transforms its own half (normals4's operations: gp_normal2's values).
+__device__ __forceinline__ uint32_t dpp_u32_xor1(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xF, 0xF, false);
+}
+__device__ __forceinline__ void bm_half(uint32_t wl, uint32_t wa, double& zc, double& zs) {
+  double sn, cs;
+  const double r = bm_sqrt(-2.0 * bm_log_u32(wl));
+  bm_sincos2pi_u32(wa, sn, cs);
+  zc = r * cs;
+  zs = r * sn;
+}
+__device__ __forceinline__ void fused_mix_tile(const FusedMix& m, int k, int rg, int pg, int lane) {
+  constexpr int NT = kFusedMixGroup / 16;
+  const int lr = lane & 15, lg = lane >> 4;
+  const int r = 16 * rg + lr;
+  const bool rv = r < m.n_real;  // padding realizations: zero, as k_gen_mix writes them
+  const uint64_t g = (uint64_t)(m.real0 + r);
+  const int p0 = kFusedMixGroup * pg;
+  int qe[NT];
+  int qmax = 0;
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int pt = p0 + 16 * t;
+    qe[t] = pt < m.P ? min(m.lower ? min(m.P, pt + 16) : m.P, m.n_q) : 0;
+    qmax = max(qmax, qe[t]);
+  }
+  d4 acc[NT][2];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc[t][0] = acc[t][1] = d4{0.0, 0.0, 0.0, 0.0};
+  const double* __restrict__ lt = m.LT + p0 + lr;
+  const bool paired = (m.real0 & 1) == 0;  // lanes 2 i, 2 i + 1: realizations g, g + 1 of one Philox counter
+  const int e = lr & 1;
+  const uint32_t ctr3 = (uint32_t)(g >> 1);
+  // rows q0 + lg of k-steps q0 < qe[t] <= P only: up to 4 ceil(P / 4) - 1 < lt_rows (launch check), zero past P
+  for (int q0 = 0; q0 < qmax; q0 += 8) {
+    double a0[NT], a1[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      a0[t] = q0 < qe[t] ? ld_global(lt + (int64_t)(q0 + lg) * m.lt_ld + 16 * t) : 0.0;
+      a1[t] = q0 + 4 < qe[t] ? ld_global(lt + (int64_t)(q0 + 4 + lg) * m.lt_ld + 16 * t) : 0.0;
+    }
+    double zc0, zs0, zc1, zs1;
+    if (paired) {
+      const u32x4 v = philox4x32_10({(uint32_t)k, (uint32_t)(q0 + 4 * e + lg), (uint32_t)m.seg, ctr3}, m.k0, m.k1);
+      const uint32_t r0 = dpp_u32_xor1(e ? v.x : v.z), r1 = dpp_u32_xor1(e ? v.y : v.w);
+      bm_half(e ? r0 : v.x, e ? r1 : v.y, zc0, zs0);  // step q0: (x, y) of an even realization, (z, w) of an odd one
+      bm_half(e ? v.z : r0, e ? v.w : r1, zc1, zs1);  // step q0 + 4
+    } else {
+      gp_normal2((uint32_t)k, (uint32_t)(q0 + lg), (uint32_t)m.seg, g, m.k0, m.k1, zc0, zs0);
+      gp_normal2((uint32_t)k, (uint32_t)(q0 + 4 + lg), (uint32_t)m.seg, g, m.k0, m.k1, zc1, zs1);
+    }
+    const bool ok0 = rv && q0 + lg < m.n_q, ok1 = rv && q0 + 4 + lg < m.n_q;
+    zc0 = ok0 ? zc0 : 0.0;
+    zs0 = ok0 ? zs0 : 0.0;
+    zc1 = ok1 ? zc1 : 0.0;
+    zs1 = ok1 ? zs1 : 0.0;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+      if (q0 < qe[t]) {
+        acc[t][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0[t], zc0, acc[t][0], 0, 0, 0);
+        acc[t][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0[t], zs0, acc[t][1], 0, 0, 0);
+      }
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+      if (q0 + 4 < qe[t]) {
+        acc[t][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1[t], zc1, acc[t][0], 0, 0, 0);
+        acc[t][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1[t], zs1, acc[t][1], 0, 0, 0);
+      }
+  }
+  // D of tile t: lane (lr, lg) register gg = pulsar p0 + 16 t + lg + 4 gg, realization r; stored as amp * sum
+  // (k_gen_mix's rounding)
+  const double am = ld_global(m.amp + k);
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int gg = 0; gg < 4; ++gg) {
+        const int p = p0 + 16 * t + lg + 4 * gg;
+        if (p < m.P) m.coef[((int64_t)p * m.K + m.col0 + 2 * k + h) * m.R_pad + r] = am * acc[t][h][gg];
+      }
+}
+
 }  // namespace
 
 // NQ: band steps whose operands an interpolation wave holds (HALF: per half); ODD: the first realization is odd (GEN
@@ -118,7 +207,28 @@ __global__ __launch_bounds__(64 * (kFusedIW + kFusedDW), 1) void k_grid_fused(Sy
           __hip_atomic_store(f.queue + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   };
-  if (item_of(0) < 0) {  // the whole workgroup, before its first barrier
+  // The successor block's mix tickets (FusedMix), taken by every wave once it has nothing left of this block: the DFT
+  // waves from the last item's interpolation on, the interpolation waves after it (at the lowest issue priority: the
+  // last chunks go first). The launch's last workgroup zeroes the ticket counter with the queues (finish). (Tickets
+  // taken by interpolation waves waiting for a build, while enough of it was left, measured no faster, and one call
+  // site keeps the 112-pulsar accumulators within the registers.)
+  auto mix_tiles = [&]() {
+    if (f.mix.n_tiles <= 0) return;
+    __builtin_amdgcn_s_setprio(0);
+    // ticket t: pulsar group t % n_pg, then realization tile, then mode
+    const int n_pg = (f.mix.P + kFusedMixGroup - 1) / kFusedMixGroup, n_rg = f.mix.R_pad >> 4;
+    for (;;) {
+      int t = 0;
+      if (lane == 0)
+        t = (int)__hip_atomic_fetch_add(f.queue + kFusedMixWord, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      t = __builtin_amdgcn_readfirstlane(t);
+      if (t >= f.mix.n_tiles) break;
+      const int pg = t % n_pg, kr = t / n_pg;
+      const int k = kr / n_rg;
+      fused_mix_tile(f.mix, k, kr - k * n_rg, pg, lane);
+    }
+  };
+  if (item_of(0) < 0) {  // the whole workgroup, before its first barrier (the other workgroups take the mix tickets)
     finish();
     return;
   }
@@ -727,12 +837,7 @@ __global__ __launch_bounds__(64 * (kFusedIW + kFusedDW), 1) void k_grid_fused(Sy
       // by the waits before the ring syncs and barriers that follow
       if (dw == 0 && lane == 0) qitem[(k + 3) & 3] = item_of(k + 2) >= 0 ? queue.fetch() : -1;
       if (k >= 0) join(k);
-      if (!next) {  // the last item: no build, no grid write
-        if (k >= 0) barrier_a(k);
-        fused_wait_lgkm0();
-        fused_barrier();  // B(k)
-        break;
-      }
+      if (!next) break;  // the last item: no build, no grid write, no barriers (the roles meet after it, below)
       if (!(FPTA_FUSED_CUT & 1)) build(k + 1);  // build and write on one path: the accumulators die at the write
       if (k >= 0) barrier_a(k);
       write_grid();
@@ -741,9 +846,7 @@ __global__ __launch_bounds__(64 * (kFusedIW + kFusedDW), 1) void k_grid_fused(Sy
       pf.lap(4);
     }
     pf.flush(f.prof, wave);
-    return;
-  }
-
+  } else {
   // ------------------------------------------------------------------ interpolation waves
   Prof pf;  // interpolation waves: 0 next-chunk loads, 1 MFMA steps, 2 stores, 3 barriers, 4 wide-chunk steps, 5 chunks,
             // 6 ticket + stream
@@ -804,7 +907,8 @@ __global__ __launch_bounds__(64 * (kFusedIW + kFusedDW), 1) void k_grid_fused(Sy
       }
       step(o1, o0, kc);
     }
-    // no chunk of item k left for this wave: cross A(k), B(k)
+    // no chunk of item k left for this wave: cross A(k), B(k) (not after the last item: nothing follows it)
+    if (!g1.valid) break;
     fused_wait_lgkm0();  // every grid read of the item is done
     pf.lap(6);
     fused_barrier();  // A(k)
@@ -815,14 +919,17 @@ __global__ __launch_bounds__(64 * (kFusedIW + kFusedDW), 1) void k_grid_fused(Sy
     g1 = geo(k + 1);
     ex0 = ex1;
     ex1 = false;
-    if (!g0.valid) break;
     if (kc < 0) {
       const int cc = next(kc);
       load(cc >= 0 ? cc : g0.c0, o0, lane);
     }
   }
   pf.flush(f.prof, wave);
-  finish();  // thread 0 (an interpolation wave): after the last barrier, so after every fetch of the workgroup
+  }
+  // both roles: the successor's mix tickets, then the last barrier
+  mix_tiles();
+  fused_barrier();
+  if (wave < kFusedIW) finish();  // thread 0: after the last barrier, so after every fetch of the workgroup
 }
 
 hipError_t launch_grid_fused(hipStream_t st, const SynthArgs& a, const GridBand& band, const FusedArgs& f,
@@ -852,6 +959,15 @@ hipError_t launch_grid_fused(hipStream_t st, const SynthArgs& a, const GridBand&
     jobs += fs.n_rc;
   }
   if (jobs > kFusedDW) return hipErrorInvalidValue;
+  // the successor's mix: the L^T columns of its 16-pulsar tiles and rows of its k-steps, 16-realization tickets over
+  // its R_pad, its columns inside its coefficient rows
+  const FusedMix& m = f.mix;
+  if (m.n_tiles != 0 &&
+      (m.n_tiles < 0 || !m.LT || !m.amp || !m.coef || m.P <= 0 || m.P > kFusedMixMaxP || m.lt_ld < 16 * ((m.P + 15) / 16) ||
+       m.lt_rows < 4 * ((m.P + 3) / 4) || m.n_q <= 0 || m.n_q > m.P || m.nm <= 0 || m.R_pad <= 0 ||
+       m.R_pad % 16 != 0 || m.n_real <= 0 || m.n_real > m.R_pad || (int64_t)m.n_tiles != (int64_t)m.nm * (m.R_pad / 16) * ((m.P + kFusedMixGroup - 1) / kFusedMixGroup) ||
+       m.col0 < 0 || m.col0 + 2 * m.nm > m.K || m.real0 < 0 || m.real0 + m.n_real > ((int64_t)1 << 32)))
+    return hipErrorInvalidValue;
   const int32_t n_rb = a.R_pad / kFusedReal;
   const int64_t items = (int64_t)a.P * n_rb;
   if (items > 0x7FFFFFFF || items <= 0) return hipErrorInvalidValue;

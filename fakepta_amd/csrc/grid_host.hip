@@ -767,6 +767,9 @@ int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad, bool pipe) {
     // the DFT overwrites buffer gi: the interpolation that last read it (two blocks back) must be done
     if (c->gfree_set[gi]) HIPCHK(c, hipStreamWaitEvent(c->side, c->ev_gfree[gi], 0), "grid buffer wait");
   }
+  // a pipelined block whose draws and mixing queued nothing on the side stream (the previous block's kernel mixed its
+  // common signal, FPTA_OPT_FUSED_NEXT_MIX; its other signals drawn inside the kernel): no grid-ready event to wait for
+  bool gwait = pipe;
   if (psr || fused || fused_w) {
     GridSeg* gs = G.segs[0];
     GridSegDev& g = gsegs.s[0];
@@ -778,8 +781,9 @@ int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad, bool pipe) {
     g.tq = gs->tq.as<double>();
     g.ldq = gs->ldq;
     g.ntq = gs->ntq;
+    gwait = pipe && c->coef_queued;
+    if (gwait) HIPCHK(c, hipEventRecord(c->ev_gready, c->side), "event record");
     if (pipe) {
-      HIPCHK(c, hipEventRecord(c->ev_gready, c->side), "event record");
       c->coef_last_side = false;  // the interpolation on the ctx stream reads the coefficients
     } else {
       int rc = wait_coef_all(c);
@@ -918,7 +922,7 @@ int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad, bool pipe) {
     c->part_cur = pi;
     c->part_next = pi ^ 1;
   }
-  if (pipe) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_gready, 0), "grid ready wait");
+  if (gwait) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_gready, 0), "grid ready wait");
   if (pipe && c->s2done_set) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_gready2, 0), "grid ready wait");
   // the fused launch takes the timing events itself (no marker packets around it); the diagnostic options that take
   // another kernel for a fused layout time it with recorded events
@@ -1057,6 +1061,34 @@ int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad, bool pipe) {
       c->fused_q_ready = true;
     }
     f.queue = c->fused_q.as<uint32_t>();
+    // FPTA_OPT_FUSED_NEXT_MIX: the next block's common-signal mix (this seed and size from real0 + n_real) as spare-time
+    // tickets, into the coefficient buffer that block swaps in (c->coef2: this block's kernel and k_gen_mix's of the
+    // block before read it no more; grown already, so it is not reallocated under the kernel)
+    c->next_mix_made = false;
+    const int32_t nms = !fused_w && pipe && c->prev_psr ? next_mix_seg(c, L, R_pad) : -1;
+    const size_t coef_bytes = sizeof(double) * (size_t)L.P * std::max(L.K, 1) * R_pad;
+    if (nms >= 0 && c->coef2.cap >= coef_bytes && c->blk_real0 + 2 * (int64_t)a.n_real <= ((int64_t)1 << 32)) {
+      const SegDesc& d = L.segs[nms]->d;
+      FusedMix& m = f.mix;
+      m.LT = d.LT;
+      m.amp = d.amp;
+      m.coef = c->coef2.as<double>();
+      m.real0 = c->blk_real0 + a.n_real;
+      m.k0 = c->blk_k0;
+      m.k1 = c->blk_k1;
+      m.lt_ld = d.lt_ld;
+      m.lt_rows = d.lt_rows;
+      m.P = L.P;
+      m.K = a.K;
+      m.col0 = d.col0;
+      m.R_pad = R_pad;
+      m.n_real = a.n_real;
+      m.n_q = d.n_q;
+      m.lower = d.l_lower;
+      m.seg = nms;
+      m.nm = d.nm;
+      m.n_tiles = d.nm * (R_pad / 16) * ((L.P + kFusedMixGroup - 1) / kFusedMixGroup);
+    }
     hipEvent_t e0 = kt.start_ev();
     int ki = 0;
     if (fused_w) {
@@ -1067,6 +1099,19 @@ int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad, bool pipe) {
       HIPCHK(c, kt.checked(launch_grid_fused(c->stream, a, band, f, nq, G.fused_lds, e0, kt.stop_ev(), half, &ki)),
              "k_grid_fused launch");
       kind = kInterpKindFused0 + ki;  // fpta_batch_grid_info_n slot 15: the instance launched
+      if (f.mix.n_tiles > 0) {
+        fpta_ctx::NextMix& nx = c->next_mix;
+        nx.valid = true;
+        nx.layout = &L;
+        nx.version = L.version;
+        nx.seed = (uint64_t)c->blk_k0 | ((uint64_t)c->blk_k1 << 32);
+        nx.real0 = f.mix.real0;
+        nx.n_real = a.n_real;
+        nx.R_pad = R_pad;
+        nx.seg = nms;
+        nx.buf = c->coef2.p;
+        c->next_mix_made = true;
+      }
     }
     c->last_fma_interp = half ? G.fma_interp_half : G.fma_interp;
   } else if (psr) {

@@ -139,12 +139,17 @@ __device__ __forceinline__ void normals4(u32x4 v, double (&z)[4]) {
 
 // GP coefficient normals (oracle gp_normals): ctr = (mode, pulsar, signal, g >> 1); realization g takes normals
 // 2 (g & 1), 2 (g & 1) + 1 as (cos, sin). gp_pair2: both realizations g, g + 1 of an even g from one call.
+// (gp_normal2 transforms only the half of the Philox output realization g takes: normals4's operations on those two
+// words, so the same values as normals4's z[2 (g & 1)], z[2 (g & 1) + 1] for half the fp64 work)
 __device__ __forceinline__ void gp_normal2(uint32_t k, uint32_t p, uint32_t seg, uint64_t g, uint32_t k0, uint32_t k1,
                                            double& zc, double& zs) {
-  double z[4];
-  normals4(philox4x32_10({k, p, seg, (uint32_t)(g >> 1)}, k0, k1), z);
-  zc = (g & 1) ? z[2] : z[0];
-  zs = (g & 1) ? z[3] : z[1];
+  const u32x4 v = philox4x32_10({k, p, seg, (uint32_t)(g >> 1)}, k0, k1);
+  const bool odd = (g & 1) != 0;
+  double s, c;
+  const double r = bm_sqrt(-2.0 * bm_log_u32(odd ? v.z : v.x));
+  bm_sincos2pi_u32(odd ? v.w : v.y, s, c);
+  zc = r * c;
+  zs = r * s;
 }
 __device__ __forceinline__ void gp_pair2(uint32_t k, uint32_t p, uint32_t seg, uint64_t g_even, uint32_t k0,
                                          uint32_t k1, double (&z)[4]) {

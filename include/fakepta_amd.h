@@ -43,8 +43,9 @@ typedef struct fpta_ctx fpta_ctx;
  * or buffer size changes; the revision when a call's accepted values or reported codes change. 10100 (round 6):
  * FPTA_OPT_INTERP_WS 0/2/3, DFT_GEN 0, GEN_MIX 0/1/3, ASYNC_SUMS 1 and SIDE_SPLIT 0/1 are refused (FPTA_EINVAL) by
  * the product library (variant builds accept them); FPTA_OPT_INTERP_FUSED takes 0 .. 3; fpta_batch_grid_info_n slot
- * 15 names each k_grid_fused instance (kinds 11 .. 19) instead of kinds 8 / 9. */
-#define FPTA_VERSION 10100
+ * 15 names each k_grid_fused instance (kinds 11 .. 19) instead of kinds 8 / 9. 10200 (round 6): option
+ * FPTA_OPT_FUSED_NEXT_MIX; fpta_batch_grid_info_n slots 17 and 18 (FPTA_GRID_INFO_LEN 19). */
+#define FPTA_VERSION 10200
 int fpta_version(void);
 int fpta_create(int device, fpta_ctx** out);
 int fpta_destroy(fpta_ctx* ctx);
@@ -222,10 +223,13 @@ int fpta_batch_info(fpta_ctx* ctx, int64_t* info);
  * 11 .. 19 the k_grid_fused<NQ, ODD, GEN, HALF> instances (8 / 12 band steps' operands x no draws / draws / draws
  * from an odd realization, then half-chunk bands x the same three), 20 / 21 k_grid_fused_w (white / ECORR epilogue;
  * even / odd first realization); out[16] (FPTA_VERSION 10100) the interpolation MFMA FMAs per realization of the
- * last gridded block as its kernel ran them (half-chunk bands: both halves' steps; else out[4]).
+ * last gridded block as its kernel ran them (half-chunk bands: both halves' steps; else out[4]); out[17]
+ * (FPTA_VERSION 10200) 1 when the last block's k_grid_fused also made the next block's common-signal mix
+ * (FPTA_OPT_FUSED_NEXT_MIX), out[18] 1 when the last block took its common-signal mix from the previous block's kernel
+ * (no k_gen_mix launch).
  * fpta_batch_grid_info_n writes the first min(n_out, FPTA_GRID_INFO_LEN) values and returns FPTA_GRID_INFO_LEN
  * (negative on error); fpta_batch_grid_info keeps the round-1 contract: out[0..8], host double[9]. */
-#define FPTA_GRID_INFO_LEN 17
+#define FPTA_GRID_INFO_LEN 19
 int fpta_batch_grid_info_n(fpta_ctx* ctx, double* out, int32_t n_out);
 int fpta_batch_grid_info(fpta_ctx* ctx, double* out);
 /* Why the last batch did not take the gridded path (signal count, non-harmonic grid, error bound, cost,
@@ -392,6 +396,13 @@ int fpta_comm_gather(fpta_comm* comm, const double* send, int64_t count, double*
                                      epoch-major); 0 (default) the DFT + interpolation kernels (measured faster on C5:
                                      1.74 vs 2.05 ms per block). Sums agree to rounding (two summation
                                      chains per chunk), white / ECORR terms identical. */
+#define FPTA_OPT_FUSED_NEXT_MIX 25 /* (FPTA_VERSION 10200) pipelined gridded blocks on k_grid_fused (FPTA_OPT_OVERLAP 1)
+                                     with one ORF-mixed common signal of 64 .. 128 pulsars drawn by k_gen_mix (C2's
+                                     GWB): 1 (default) the kernel's waves with nothing left of their block draw and
+                                     mix that signal for the next block of the same seed and size (first realization
+                                     real0 + n_real) into the coefficient buffer that block reads; a batch_synth with
+                                     that key then launches no k_gen_mix, any other call first waits for the kernel.
+                                     0: every block runs k_gen_mix. Results are identical. */
 int fpta_set_option(fpta_ctx* ctx, int32_t key, int64_t value);
 /* Current value of option `key` (same keys as fpta_set_option). */
 int fpta_get_option(fpta_ctx* ctx, int32_t key, int64_t* value);

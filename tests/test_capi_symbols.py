@@ -41,7 +41,7 @@ def test_ctypes_binding_covers_header():
 
 def test_version_and_errors_without_gpu():
     from fakepta_amd import _capi
-    assert _capi._lib.fpta_version() == 10100  # FPTA_VERSION: ABI 1, behaviour revision 1
+    assert _capi._lib.fpta_version() == 10200  # FPTA_VERSION: ABI 1, behaviour revision 2
     # no device here: creation fails loudly with a message, never silently
     if _capi.device_count() == 0:
         with pytest.raises(_capi.FptaError):
