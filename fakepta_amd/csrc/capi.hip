@@ -317,12 +317,25 @@ int run_coefficients(fpta_ctx* c, Layout& L, uint64_t seed, int64_t real0, int32
   c->next_mix.valid = false;
   c->next_mix_used = false;
   int32_t nm_seg = -1;
+  // a miss: the side streams wait for that kernel (ctx-stream work is ordered after it anyway); a coefficient buffer
+  // that may be regrown below is not freed under it either (the whole ctx stream is waited for then)
+  const size_t coef_need = sizeof(double) * (size_t)P * std::max(L.K, 1) * R_pad;
+  auto next_mix_miss = [&]() -> int {
+    if (c->coef.cap < coef_need || c->coef2.cap < coef_need || !nmx.done) {
+      HIPCHK(c, hipStreamSynchronize(c->stream), "next mix sync");
+    } else {
+      if (c->side) HIPCHK(c, hipStreamWaitEvent(c->side, nmx.done, 0), "next mix wait");
+      if (c->side2) HIPCHK(c, hipStreamWaitEvent(c->side2, nmx.done, 0), "next mix wait");
+    }
+    nm_seg = -1;
+    return FPTA_OK;
+  };
   if (nmx.valid) {
     if (nmx.layout == &L && nmx.version == L.version && nmx.seed == seed && nmx.real0 == real0 && nmx.n_real == R &&
         nmx.R_pad == R_pad && pipe && side && merge && !zin && !x_out && !coef_host && nmx.seg == next_mix_seg(c, L, R_pad))
       nm_seg = nmx.seg;
-    else
-      HIPCHK(c, hipStreamSynchronize(c->stream), "next mix sync");
+    else if ((rc0 = next_mix_miss()))
+      return rc0;
   }
   hipStream_t st = c->stream;
   const bool use_side = side && (L.segs.size() > 1 || pipe);
@@ -336,10 +349,7 @@ int run_coefficients(fpta_ctx* c, Layout& L, uint64_t seed, int64_t real0, int32
     c->coef.swap(c->coef2);
     c->coef_slot = c->gbuf;
   }
-  if (nm_seg >= 0 && !(psr && c->coef.p == nmx.buf)) {
-    HIPCHK(c, hipStreamSynchronize(c->stream), "next mix sync");
-    nm_seg = -1;
-  }
+  if (nm_seg >= 0 && !(psr && c->coef.p == nmx.buf) && (rc0 = next_mix_miss())) return rc0;
   const size_t coef_bytes = sizeof(double) * (size_t)P * std::max(L.K, 1) * R_pad;
   if (c->side && c->coef.cap < coef_bytes) HIPCHK(c, hipStreamSynchronize(c->side), "side sync");  // before a regrow
   if (c->side2 && c->coef.cap < coef_bytes) HIPCHK(c, hipStreamSynchronize(c->side2), "side sync");
@@ -454,10 +464,7 @@ int run_coefficients(fpta_ctx* c, Layout& L, uint64_t seed, int64_t real0, int32
     const SegDesc& d = L.segs[i]->d;
     return d.kind == 1 && c->gen_mix && mfma_mix && !zin && !x_out && fuse_into[i] < 0 && P <= kGenMixMaxP;
   };
-  if (nm_seg >= 0 && !gen_mix_branch((size_t)nm_seg)) {
-    HIPCHK(c, hipStreamSynchronize(c->stream), "next mix sync");
-    nm_seg = -1;
-  }
+  if (nm_seg >= 0 && !gen_mix_branch((size_t)nm_seg) && (rc0 = next_mix_miss())) return rc0;
   for (size_t i = 0; i < L.segs.size(); ++i) {
     const SegDesc& d = L.segs[i]->d;
     hipStream_t si = stream_of(group_of[i]);  // side2 only for members of split_g (kind 0: no mixing below)
@@ -1484,6 +1491,7 @@ int batch_common(fpta_ctx* c, uint64_t seed, int64_t real0, int32_t n_real, cons
            "coef download");
   }
   if (out || coeffs_out || coeffs_host) HIPCHK(c, hipStreamSynchronize(c->stream), "batch sync");
+  c->last_blk = fpta_ctx::LastBlock{true, seed, real0, n_real};
   return FPTA_OK;
 }
 

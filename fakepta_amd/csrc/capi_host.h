@@ -273,7 +273,8 @@ struct fpta_ctx {
   bool prev_psr = false;
   // FPTA_OPT_FUSED_NEXT_MIX: the last k_grid_fused launch also made the mix of common signal `seg` for the block
   // (layout, version, seed, real0, n_real, R_pad) into buffer `buf` (c->coef2 then, c->coef once that block swaps).
-  // run_coefficients takes it when the next block has exactly that key, else waits for the ctx stream first.
+  // run_coefficients takes it when the next block has exactly that key; otherwise the side streams wait for that
+  // kernel (event `done`) before they write a coefficient buffer.
   int fused_next_mix = 1;
   struct NextMix {
     bool valid = false;
@@ -282,7 +283,16 @@ struct fpta_ctx {
     int64_t real0 = 0;
     int32_t n_real = 0, R_pad = 0, seg = -1;
     const void* buf = nullptr;
+    hipEvent_t done = nullptr;  // recorded on the ctx stream after that kernel (a miss makes the side streams wait for it)
   } next_mix;
+  // the last batch block (seed, first realization, size): the next block's first realization is predicted at this
+  // block's stride (simulate_sharded: the batch; bench.py on G ranks: G x R)
+  struct LastBlock {
+    bool valid = false;
+    uint64_t seed = 0;
+    int64_t real0 = 0;
+    int32_t n_real = 0;
+  } last_blk;
   bool next_mix_made = false, next_mix_used = false;  // fpta_batch_grid_info_n slots 17, 18 of the last block
   bool coef_queued = true;  // the last run_coefficients queued work (a pipelined block that queued none: no grid-ready wait)
   int async_sums = 0;    // streamed jobs: partial-checksum reductions on their own stream (FPTA_OPT_ASYNC_SUMS; measured

@@ -1064,16 +1064,24 @@ int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad, bool pipe) {
     // FPTA_OPT_FUSED_NEXT_MIX: the next block's common-signal mix (this seed and size from real0 + n_real) as spare-time
     // tickets, into the coefficient buffer that block swaps in (c->coef2: this block's kernel and k_gen_mix's of the
     // block before read it no more; grown already, so it is not reallocated under the kernel)
+    // (the next block's first realization: real0 + this block's stride from the last one of the same seed and size
+    // when that is a whole number of blocks (G ranks' interleaved blocks), else real0 + n_real)
     c->next_mix_made = false;
     const int32_t nms = !fused_w && pipe && c->prev_psr ? next_mix_seg(c, L, R_pad) : -1;
     const size_t coef_bytes = sizeof(double) * (size_t)L.P * std::max(L.K, 1) * R_pad;
-    if (nms >= 0 && c->coef2.cap >= coef_bytes && c->blk_real0 + 2 * (int64_t)a.n_real <= ((int64_t)1 << 32)) {
+    const uint64_t blk_seed = (uint64_t)c->blk_k0 | ((uint64_t)c->blk_k1 << 32);
+    const fpta_ctx::LastBlock& lb = c->last_blk;
+    const int64_t step = c->blk_real0 - lb.real0;
+    const int64_t stride =
+        lb.valid && lb.seed == blk_seed && lb.n_real == a.n_real && step >= a.n_real && step % a.n_real == 0 ? step
+                                                                                                         : a.n_real;
+    if (nms >= 0 && c->coef2.cap >= coef_bytes && c->blk_real0 + stride + a.n_real <= ((int64_t)1 << 32)) {
       const SegDesc& d = L.segs[nms]->d;
       FusedMix& m = f.mix;
       m.LT = d.LT;
       m.amp = d.amp;
       m.coef = c->coef2.as<double>();
-      m.real0 = c->blk_real0 + a.n_real;
+      m.real0 = c->blk_real0 + stride;
       m.k0 = c->blk_k0;
       m.k1 = c->blk_k1;
       m.lt_ld = d.lt_ld;
@@ -1104,12 +1112,13 @@ int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad, bool pipe) {
         nx.valid = true;
         nx.layout = &L;
         nx.version = L.version;
-        nx.seed = (uint64_t)c->blk_k0 | ((uint64_t)c->blk_k1 << 32);
+        nx.seed = blk_seed;
         nx.real0 = f.mix.real0;
         nx.n_real = a.n_real;
         nx.R_pad = R_pad;
         nx.seg = nms;
         nx.buf = c->coef2.p;
+        nx.done = nullptr;  // the event recorded after this launch (pipe: ev_gfree of this block's buffer index, below)
         c->next_mix_made = true;
       }
     }
@@ -1142,6 +1151,7 @@ int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad, bool pipe) {
   if (kind < kInterpKindFused0) c->last_fma_interp = G.fma_interp;
   if (pipe) {  // buffer gi is free once this interpolation is done; the next block's DFT writes the other one
     HIPCHK(c, hipEventRecord(c->ev_gfree[gi], c->stream), "event record");
+    if (c->next_mix_made) c->next_mix.done = c->ev_gfree[gi];  // the kernel that writes the next block's mix is done
     c->gfree_set[gi] = true;
     c->gbuf = gi ^ 1;
   }

@@ -33,3 +33,19 @@ def test_two_rank_c3_checksums_match_one_rank():
     assert one["n_gpus"] == 1 and two["n_gpus"] == 2
     assert one["n_checksums"] == two["n_checksums"] == 10000
     assert one["checksum"] == two["checksum"]
+
+
+def test_two_rank_c2_steps_match_one_rank():
+    """C2 on two ranks (gloo, one card): rank g's step s draws realizations ((W + s) 2 + g) R .. + R, so its blocks
+    advance at a stride of two blocks (the library's next-block mix follows that stride, FPTA_OPT_FUSED_NEXT_MIX);
+    the last step's realizations of both ranks, gathered in rank order, are one rank's last step at 2R realizations
+    per step: the same checksums, bit for bit."""
+    args = ["--steps", "4", "--warmup", "2", "--cpu-sample", "0", "--sub-configs", "0", "--exact-launches", "0",
+            "--dist-backend", "gloo"]
+    one = _line([sys.executable, "bench.py", "--real", "256"] + args)
+    two = _line([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                 "--master-addr", "127.0.0.1", "--master-port", "29533", "bench.py", "--gpus", "2", "--real", "128"]
+                + args)
+    assert one["n_gpus"] == 1 and two["n_gpus"] == 2
+    assert one["n_checksums"] == two["n_checksums"] == 256
+    assert one["checksum"] == two["checksum"]

@@ -1,5 +1,6 @@
 """FPTA_OPT_FUSED_NEXT_MIX: a pipelined k_grid_fused block also draws and ORF-mixes the common signal of the block
-that follows it (same seed and size, first realization real0 + n_real) as spare-time tickets of its waves
+that follows it (same seed and size, first realization real0 + the last stride when that is a whole number of
+blocks, else real0 + n_real) as spare-time tickets of its waves
 (fused_mix_tile), into the coefficient buffer that block swaps in; that block then launches no k_gen_mix.
 
 Checked against the same block sequences with the option off (every block runs k_gen_mix): bit for bit, since the
@@ -137,6 +138,29 @@ def test_next_mix_bitwise_vs_gen_mix(ctx, capi, shipped, P, factor):
         want = O.batch_synth(offs, toas, nu, segs, seed, real0, R)
         assert rel_err(got[i], want) <= GRID_TOL
         assert_parity(got[i], want, TOL)
+    finally:
+        ctx.batch_clear()
+        ctx.set_options(shipped)
+
+
+def test_next_mix_rank_strides(ctx, capi, shipped):
+    """Blocks at a stride of G blocks (rank g of G in bench.py: real0 = (s G + g) R): from the third block on the
+    prediction follows the stride (a whole number of blocks) and every block hits; a jump that is not a whole number
+    of blocks predicts real0 + n_real again. Bit for bit against the option off."""
+    rng = np.random.default_rng(751)
+    _layout(ctx, rng, 100, "cholesky")
+    R = 128
+    seq = [(11, (s * 4 + 1) * R, R, s % 2 == 1) for s in range(6)]                      # rank 1 of 4
+    seq += [(11, 5000, R, False), (11, 5000 + R, R, True), (11, 5000 + 2 * R, R, True)]  # a jump, then consecutive
+    try:
+        ctx.synchronize()
+        ref, _, _ = _run_seq(ctx, capi, 0, seq)
+        got, used, made = _run_seq(ctx, capi, 1, seq)
+        for i, (x, y) in enumerate(zip(ref, got)):
+            if x is not None:
+                np.testing.assert_array_equal(y, x, err_msg=f"block {i} {seq[i]}")
+        assert used == [False, False, True, True, True, True, False, True, True], used
+        assert all(made)
     finally:
         ctx.batch_clear()
         ctx.set_options(shipped)
