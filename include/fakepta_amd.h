@@ -400,8 +400,10 @@ int fpta_comm_gather(fpta_comm* comm, const double* send, int64_t count, double*
                                      with one ORF-mixed common signal of 64 .. 128 pulsars drawn by k_gen_mix (C2's
                                      GWB): 1 (default) the kernel's waves with nothing left of their block draw and
                                      mix that signal for the next block of the same seed and size (first realization
-                                     real0 + n_real) into the coefficient buffer that block reads; a batch_synth with
-                                     that key then launches no k_gen_mix, any other call first waits for the kernel.
+                                     real0 + the stride from the block before when that is a whole number of blocks,
+                                     else real0 + n_real) into the coefficient buffer that block reads; a batch_synth
+                                     with that key then launches no k_gen_mix; after any other call the side streams
+                                     wait for the kernel.
                                      0: every block runs k_gen_mix. Results are identical. */
 int fpta_set_option(fpta_ctx* ctx, int32_t key, int64_t value);
 /* Current value of option `key` (same keys as fpta_set_option). */
