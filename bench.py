@@ -278,6 +278,15 @@ def pmc_traffic(kernel, info, R, path_arg, layout=None):
     return None, None
 
 
+def next_mix_mfmas(P, nm, R_pad, lower=True, n_q=None):
+    """fp64 MFMAs k_grid_fused runs for the next block's common-signal mix (FPTA_OPT_FUSED_NEXT_MIX,
+    grid_fused.hip fused_mix_tile): per (mode, 16 realizations), two per k-step of each 16-pulsar tile, a lower-
+    triangular factor's steps stopping at the tile's diagonal."""
+    n_q = P if n_q is None else n_q
+    steps = sum(-(-min(min(P, pt + 16) if lower else P, n_q) // 4) for pt in range(0, P, 16))
+    return 2 * steps * nm * (R_pad // 16)
+
+
 def kernel_avg_s(ctx, which):
     n, ms = ctx.kernel_stats(which)
     return ms / max(n, 1) / 1e3
@@ -466,6 +475,8 @@ def main():
         dft_flops = 2.0 * gi["fma_dft"] * R_pad
         # grid signals with a per-pulsar member draw their coefficients inside the DFT (FPTA_OPT_DFT_GEN, C2)
         fused = kernel.startswith("k_grid_fused")
+        mix_flops = (2048.0 * next_mix_mfmas(info["n_psr"], 30, R_pad)
+                     if fused and args.config == "c2" and gi.get("next_mix_made") else 0.0)
         dft_kernel = ("inside " + kernel if fused else
                       "k_grid_dft_gen" if args.config == "c2" and ctx.get_option(_capi.OPT_DFT_GEN)
                       and gi["grid_mfma"] & 1 else GRID_DFT[bool(gi["grid_mfma"] & 1)])
@@ -479,10 +490,13 @@ def main():
                     "interp_fp64_TFLOPs": 2.0 * gi["fma_interp_run"] * R_pad / synth_avg_s / 1e12,
                     # k_grid_fused also runs the block's DFTs on the same fp64 pipe (one launch, no DFT kernel): its
                     # interpolation + DFT MFMA FLOPs against the 78.6 TF FP64 peak beside the HBM fraction
-                    "fp64_pipe": ({"flops_per_launch": 2.0 * (gi["fma_interp_run"] + gi["fma_dft"]) * R_pad,
-                                   "TFLOPs": 2.0 * (gi["fma_interp_run"] + gi["fma_dft"]) * R_pad / synth_avg_s / 1e12,
-                                   "frac": 2.0 * (gi["fma_interp_run"] + gi["fma_dft"]) * R_pad / synth_avg_s / 1e12
-                                   / FP64_PEAK_TFLOPS} if fused else None),
+                    # (+ the next block's GW mix when the launch made it: C2's HD GWB30, Cholesky factor)
+                    "fp64_pipe": ({"flops_per_launch": 2.0 * (gi["fma_interp_run"] + gi["fma_dft"]) * R_pad + mix_flops,
+                                   "next_mix_flops": mix_flops,
+                                   "TFLOPs": (2.0 * (gi["fma_interp_run"] + gi["fma_dft"]) * R_pad + mix_flops)
+                                   / synth_avg_s / 1e12,
+                                   "frac": (2.0 * (gi["fma_interp_run"] + gi["fma_dft"]) * R_pad + mix_flops)
+                                   / synth_avg_s / 1e12 / FP64_PEAK_TFLOPS} if fused else None),
                     "grid": {"width": gi["width"], "sigma": gi["sigma"], "err_bound": gi["err_bound"],
                              "signals": gi["signals"], "grid_signals": gi["grid_signals"],
                              "band_rows_per_chunk": gi["band_rows_per_chunk"]},
