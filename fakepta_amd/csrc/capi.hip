@@ -332,7 +332,8 @@ int run_coefficients(fpta_ctx* c, Layout& L, uint64_t seed, int64_t real0, int32
   };
   if (nmx.valid) {
     if (nmx.layout == &L && nmx.version == L.version && nmx.seed == seed && nmx.real0 == real0 && nmx.n_real == R &&
-        nmx.R_pad == R_pad && pipe && side && merge && !zin && !x_out && !coef_host && nmx.seg == next_mix_seg(c, L, R_pad))
+        nmx.R_pad == R_pad && pipe && side && merge && !zin && !x_out && !coef_host && nmx.done &&
+        nmx.seg == next_mix_seg(c, L, R_pad))
       nm_seg = nmx.seg;
     else if ((rc0 = next_mix_miss()))
       return rc0;
@@ -470,7 +471,11 @@ int run_coefficients(fpta_ctx* c, Layout& L, uint64_t seed, int64_t real0, int32
     hipStream_t si = stream_of(group_of[i]);  // side2 only for members of split_g (kind 0: no mixing below)
     if (in_fused[i] && d.kind == 0) continue;  // drawn inside its grid signal's DFT
     if ((int32_t)i == nm_seg) {
-      c->next_mix_used = true;  // made by the previous block's kernel into this buffer (ordered on the ctx stream)
+      // made by the previous block's kernel into this buffer: ordered before this block's ctx-stream work; a reader on
+      // a side stream (the two-kernel path's DFT of a white block) waits for that kernel
+      c->next_mix_used = true;
+      if (c->side) HIPCHK(c, hipStreamWaitEvent(c->side, nmx.done, 0), "next mix wait");
+      if (c->side2) HIPCHK(c, hipStreamWaitEvent(c->side2, nmx.done, 0), "next mix wait");
       continue;
     }
     ++n_launch;

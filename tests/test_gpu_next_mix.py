@@ -211,6 +211,38 @@ def test_next_mix_invalidated_by_changes(ctx, capi, shipped):
         ctx.set_options(shipped)
 
 
+def test_next_mix_taken_by_a_white_block(ctx, capi, shipped):
+    """A white / ECORR block whose mix the previous (plain) block's kernel made takes it (the key does not cover the
+    white noise) and runs the two-kernel white path, whose DFT reads the mixed columns on a side stream after that
+    kernel: equal to the option-off sequence bit for bit, queued without host syncs."""
+    rng = np.random.default_rng(757)
+    offs, toas, nu, segs = _layout(ctx, rng, 100, "cholesky")
+    n = int(offs[-1])
+    sigma = rng.uniform(0.5e-7, 2e-7, n)
+    blocks = [np.arange(i, min(i + 2, n)) for i in range(0, n - 1, 2)]
+    esig = rng.uniform(0.5e-7, 1.5e-7, len(blocks))
+    try:
+        def seq(on):
+            ctx.set_option(capi.OPT_FUSED_NEXT_MIX, on)
+            ctx.batch_set_white()
+            for real0 in (0, 256):
+                ctx.batch_synth(21, real0, 256, to_host=False)
+            ctx.batch_set_white(sigma, blocks, esig)
+            out = ctx.batch_synth(21, 512, 256)
+            gi = ctx.batch_grid_info()
+            ctx.batch_set_white()
+            return out, gi["next_mix_used"], gi["interp_kernel"]
+        ref, u0, _ = seq(0)
+        got, u1, k1 = seq(1)
+        assert not u0 and u1
+        assert not k1.startswith("k_grid_fused"), k1
+        np.testing.assert_array_equal(got, ref)
+    finally:
+        ctx.batch_set_white()
+        ctx.batch_clear()
+        ctx.set_options(shipped)
+
+
 def test_next_mix_not_made_outside_its_layouts(ctx, capi, shipped):
     """No successor mix for layouts k_gen_mix does not serve alone: fewer than 64 pulsars (k_mix path), more than
     256, two common signals; and none with the option off."""
