@@ -16,7 +16,7 @@
 namespace fpta {
 
 // k_grid_interp_mfma: 32 TOAs x 16 kInterpRW realizations per wave, kInterpWPC persistent workgroups per CU
-// (compile-time; tools/interp_variants.sh builds the alternatives it measures into build/diag)
+// (compile-time; archived tools/experiments_archive.sh interp_variants built the alternatives it measured)
 #ifndef FPTA_INTERP_RW
 #define FPTA_INTERP_RW 8
 #endif

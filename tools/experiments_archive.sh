@@ -1,5 +1,6 @@
 #!/bin/bash
-# Archive of the one-off GPU experiment command lines of rounds 2-4 (formerly tools/gpu_<name>.sh, one file each).
+# Archive of the one-off GPU experiment command lines of rounds 2-6 (formerly tools/gpu_<name>.sh or tools/<name>.sh,
+# one file each; exp_<name> without the gpu_ prefix).
 # Each is a function named after its old file (bodies unindented: some hold here-documents); the records they
 # produced are under profiles/ (the tags in the bodies). Kept for provenance only, NOT runnable: several bodies call
 # the tools/gpu_*.sh files this archive replaced (gpu_c3_trace.sh, gpu_c3_trace3.sh, gpu_c3_batch.sh, gpu_full.sh,
@@ -460,6 +461,217 @@ P4="WRITE_SIZE"
 bash tools/pmc_passes.sh ${o}_pmc "$P0" "$P1" "$P2" "$P3" "$P4" -- python bench.py --steps 4 --warmup 2 --cpu-sample 0 --exact-launches 0 --overlap 0 --sub-configs 0 --opt INTERP_WR=1 || { echo "pmc failed"; tail -20 ${o}_pmc/pass*.log; exit 1; }
 python tools/pmc_dispatch.py ${o}_pmc --match interp > ${o}_pmc_dispatch.txt 2>&1 || exit 1
 cat ${o}_pmc_dispatch.txt
+}
+
+exp_ab_kernel_events() {
+# (formerly tools/ab_kernel_events.sh)
+# C2 step with / without the bench's per-kernel HIP timing events, pipelined (OVERLAP 1) and one-stream (OVERLAP 0)
+# blocks, alternating, two repetitions; then kernel traces of the one-stream step with and without events.
+set -o pipefail
+tag=${1:-r5ev}
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest tests/test_gpu_fused.py tests/test_gpu_grid.py -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider -k "fused or gen_mix" > gpurun_out/${tag}_tests.log 2>&1 || { tail -30 gpurun_out/${tag}_tests.log; exit 1; }
+tail -n 1 gpurun_out/${tag}_tests.log
+out=gpurun_out/${tag}_ab.txt; : > $out
+for rep in 1 2; do
+  for ov in 1 0; do
+    for ev in on off; do
+      fl=""; [ $ev = off ] && fl="--no-kernel-events"
+      timeout -k 10 120 python bench.py --cpu-sample 0 --sub-configs 0 --steps 50 --warmup 30 --overlap $ov $fl > gpurun_out/${tag}_o${ov}_$ev.json || exit 1
+      python3 -c "import json; d=json.loads(open('gpurun_out/${tag}_o${ov}_$ev.json').read().strip().splitlines()[-1]); print('rep $rep overlap $ov events $ev', round(d['ms_per_step'],4), 'fused launch (events)', d['roofline'].get('avg_launch_ms'))" | tee -a $out
+    done
+  done
+done
+for ev in on off; do
+  fl=""; [ $ev = off ] && fl="--no-kernel-events"
+  timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/${tag}_tr0_$ev -o run -- python3 bench.py --cpu-sample 0 --sub-configs 0 --steps 20 --warmup 30 --overlap 0 $fl > gpurun_out/${tag}_tr0_$ev.log 2>&1 || exit 1
+done
+}
+
+exp_ab_overlap_fused() {
+# (formerly tools/ab_overlap_fused.sh)
+# C2 (k_grid_fused): pipelined (OVERLAP 1, k_gen_mix of the next block on the side stream) vs one-stream (OVERLAP 0)
+# blocks, alternating, four repetitions at W 30 / K 50 and at the driver's W 5 / K 20.
+set -o pipefail
+tag=${1:-r5ov}
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out
+out=gpurun_out/${tag}_ab.txt; : > $out
+for wk in "30 50" "5 20"; do
+  set -- $wk
+  for rep in 1 2 3 4; do
+    for ov in 1 0; do
+      timeout -k 10 120 python bench.py --cpu-sample 0 --sub-configs 0 --warmup $1 --steps $2 --overlap $ov > gpurun_out/${tag}_o$ov.json || exit 1
+      python3 -c "import json; d=json.loads(open('gpurun_out/${tag}_o$ov.json').read().strip().splitlines()[-1]); print('W $1 K $2 rep $rep overlap $ov', round(d['ms_per_step'],4), 'fused launch', round(d['roofline'].get('avg_launch_ms'),4))" | tee -a $out
+    done
+  done
+done
+}
+
+exp_evidence() {
+# (formerly tools/gpu_evidence.sh)
+# Evidence at HEAD in one GPU call: rocprofv3 kernel statistics of the default bench command (C2), HBM traffic
+# (FETCH_SIZE / WRITE_SIZE passes) of the C2 interpolation, per-dispatch PMC of the C2 and C5 kernels (one stream).
+#   bash tools/gpu_evidence.sh <tag> [traffic kernel]       (outputs under gpurun_out/<tag>_*)
+set -o pipefail
+tag=${1:-R5e}; kern=${2:-k_grid_fused}
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out
+o=gpurun_out/$tag
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d ${o}_prof -o run -- python bench.py --steps 20 --cpu-sample 0 --exact-launches 0 --sub-configs 0 > ${o}_prof.log 2>&1 || { tail -20 ${o}_prof.log; exit 1; }
+grep '^{' ${o}_prof.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('under rocprof', d['ms_per_step'], d['roofline']['avg_launch_ms'])"
+i=0
+for p in FETCH_SIZE WRITE_SIZE; do
+  timeout -s KILL 120 rocprofv3 --pmc $p --output-format csv -d ${o}_traffic/pass$i -o run -- python bench.py --steps 5 --warmup 2 --cpu-sample 0 --exact-launches 0 --sub-configs 0 > ${o}_traffic_$p.log 2>&1 || { tail -20 ${o}_traffic_$p.log; exit 1; }
+  i=$((i+1))
+done
+python tools/collect_traffic.py ${o}_traffic ${o}_grid_traffic.json 320 200000 1024 $kern band32c || exit 1
+P0="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE"
+P1="SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_F64 SQ_LDS_BANK_CONFLICT"
+P2="TCC_HIT_sum TCC_MISS_sum TCP_TCC_READ_REQ_sum TCP_PENDING_STALL_CYCLES_sum TA_TA_BUSY_sum TD_TD_BUSY_sum"
+P3="FETCH_SIZE"
+P4="WRITE_SIZE"
+run() {  # <name> <cmd...>
+  local name=$1; shift
+  bash tools/pmc_passes.sh ${o}_pmc_$name "$P0" "$P1" "$P2" "$P3" "$P4" -- "$@" || { echo "pmc $name failed"; tail -20 ${o}_pmc_$name/pass*.log; exit 1; }
+  python tools/pmc_dispatch.py ${o}_pmc_$name > ${o}_pmc_dispatch_$name.txt 2>&1 || python tools/pmc_summary.py ${o}_pmc_$name > ${o}_pmc_dispatch_$name.txt 2>&1 || exit 1
+}
+run c2 python bench.py --steps 4 --warmup 2 --cpu-sample 0 --exact-launches 0 --overlap 0 --sub-configs 0
+run c5 python tools/bench_configs.py c5
+find ${o}_prof -name "*kernel_stats.csv"
+}
+
+exp_interp_variants() {
+# (formerly tools/interp_variants.sh)
+# NOTE (round 4): the FPTA_INTERP_DIAG cuts below were removed from the product source; this
+# script reproduces the round-2/3 records only on a checkout of revision 059c9cc or earlier.
+# Build (build) or time (run) compile-time variants of k_grid_interp_mfma: realization tiles per wave (RW),
+# persistent workgroups per CU (WPC), diagnostic cuts (DIAG 1: grid loads from one L1-resident row; 2: no
+# stores; 3: non-temporal stores; 4: no band loop, the store stream alone; 5: every other workgroup starts
+# ~7 us late; 6: k_grid_interp_ws producers load nothing; 7: 1 and 2 together, the MFMA stream alone; 8: accumulators in AGPRs; 9: waves of a CU staggered by 0..7 x 3.4 us). WS selects FPTA_OPT_INTERP_WS values to time. VARIANTS entries are RW:WPC:DIAG. Throwaway libraries in build/diag, loaded by tools/interp_diag.py
+# through FAKEPTA_AMD_LIB; never the product or the bench. Results: profiles/r02_interp_diag*.txt (a single
+# operand set at 3 workgroups per CU measured 0.70 ms against 0.66 for the shipped 2-deep pipeline at 2).
+S=fakepta_amd/csrc
+D=build/diag
+VARIANTS=${VARIANTS:-"8:2:0 8:2:2 8:2:4 8:2:6"}
+if [ "$1" = build ]; then
+  mkdir -p $D
+  for v in $VARIANTS; do
+    IFS=: read rw wpc dg <<< "$v"
+    /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -Wall -Wno-unused-result -ffp-contract=fast \
+      -fno-gpu-rdc -DFPTA_INTERP_RW=$rw -DFPTA_INTERP_WPC=$wpc -DFPTA_INTERP_DIAG=$dg ${EXTRA:-} $S/kernels.hip $S/dense.hip $S/grid.hip \
+      $S/grid_mfma.hip $S/capi.hip -o $D/lib_rw${rw}_wpc${wpc}_d${dg}.so &
+  done
+  wait
+  exit 0
+fi
+set -o pipefail
+for v in $VARIANTS; do
+  IFS=: read rw wpc dg <<< "$v"
+  for ws in ${WS:-0 1}; do
+    FAKEPTA_AMD_LIB=$D/lib_rw${rw}_wpc${wpc}_d${dg}.so timeout -k 5 120 python tools/interp_diag.py --ws $ws --label "rw$rw-wpc$wpc-d$dg-ws$ws" || exit 1
+  done
+done
+}
+
+exp_fused_roles() {
+# (formerly tools/gpu_fused_roles.sh)
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out
+timeout -k 10 200 python -u -m pytest tests/test_gpu_fused.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/r5fx_tests.log 2>&1 || { tail -5 gpurun_out/r5fx_tests.log; exit 1; }
+tail -1 gpurun_out/r5fx_tests.log
+for v in "" cut1 cut2; do
+  lib=fakepta_amd/lib/libfakepta_amd.so; [ -n "$v" ] && lib=build/diag/lib_$v.so
+  FAKEPTA_AMD_LIB=$lib timeout -k 10 60 python -u bench.py --steps 30 --cpu-sample 0 --exact-launches 3 --sub-configs 0 > gpurun_out/r5fx_$v.log 2>&1 || { echo "$v failed"; tail -3 gpurun_out/r5fx_$v.log; exit 1; }
+  grep -h '^{' gpurun_out/r5fx_$v.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('$v', d['ms_per_step'], d['roofline']['isolated']['avg_launch_ms'])"
+done
+}
+
+exp_epoch_side_ab() {
+# (formerly tools/gpu_epoch_side_ab.sh)
+# C5: the ECORR epoch normals of pipelined blocks on a stream of their own (make variant NAME=zside
+# DEFS=-DFPTA_EPOCH_SIDE=1) vs the shipped library; the white / ECORR GPU tests on the variant first.
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out
+FAKEPTA_AMD_LIB=build/diag/lib_zside.so timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread -p no:cacheprovider -k "white or ecorr or c5 or pipelined" > gpurun_out/R6v_tests.log 2>&1 || { tail -30 gpurun_out/R6v_tests.log; exit 1; }
+tail -1 gpurun_out/R6v_tests.log
+bash tools/gpu_ab_cfg.sh R6v "" c5 "" "LIB=build/diag/lib_zside.so" || exit 1
+}
+
+exp_c5_white_wpc_ab() {
+# (formerly tools/gpu_c5_white_wpc_ab.sh)
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+bash tools/gpu_ab_cfg.sh R6t "" c5 "" "LIB=build/diag/lib_wwpc3.so" "LIB=build/diag/lib_wwpc4.so" || exit 1
+}
+
+exp_c4_half_ab() {
+# (formerly tools/gpu_c4_half_ab.sh)
+# C4: half-chunk bands forced (FPTA_OPT_INTERP_FUSED 3) vs the automatic choice (whole-chunk bands on C4); PMC of the
+# C4 fused kernel at HEAD.
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out
+bash tools/gpu_ab_cfg.sh R6w "" c4 "" "INTERP_FUSED=3" || exit 1
+P0="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE"
+P1="SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_F64 SQ_LDS_BANK_CONFLICT"
+P2="TCC_HIT_sum TCC_MISS_sum TCP_TCC_READ_REQ_sum TCP_PENDING_STALL_CYCLES_sum TA_TA_BUSY_sum TD_TD_BUSY_sum"
+bash tools/pmc_passes.sh gpurun_out/R6w_pmc_c4 "$P0" "$P1" "$P2" -- python tools/bench_configs.py c4 || exit 1
+python tools/pmc_dispatch.py gpurun_out/R6w_pmc_c4 > gpurun_out/R6w_pmc_dispatch_c4.txt 2>&1 || exit 1
+echo done
+}
+
+exp_events_ab() {
+# (formerly tools/gpu_events_ab.sh)
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out
+o=gpurun_out/R6k
+B="python bench.py --steps 20 --warmup 5 --cpu-sample 0 --sub-configs 0"
+for i in 1 2; do
+  timeout -k 10 300 $B > ${o}_ev$i.log 2>&1 || exit 1
+  timeout -k 10 300 $B --no-kernel-events > ${o}_noev$i.log 2>&1 || exit 1
+done
+timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d ${o}_tr_noev -o run -- python bench.py --steps 10 --cpu-sample 0 --exact-launches 0 --sub-configs 0 --no-kernel-events > ${o}_tr_noev.log 2>&1 || exit 1
+echo done
+}
+
+exp_next_mix_ab() {
+# (formerly tools/gpu_next_mix_ab.sh)
+# FPTA_OPT_FUSED_NEXT_MIX A/B on C2 (one box): the shipped library with the option on and off, and variant builds of
+# FusedMix::min_left (make variant NAME=ml<v> DEFS=-DFPTA_FUSED_MIX_MIN_LEFT=<v>), each twice in turn; then kernel
+# traces of on / off.
+#   bash tools/gpu_next_mix_ab.sh <tag> [variant names...]
+set -o pipefail
+tag=${1:-R6h}
+shift
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out
+o=gpurun_out/$tag
+timeout -k 10 420 python -u -m pytest -x -v --timeout 240 --timeout-method thread tests/test_gpu_next_mix.py tests/test_gpu_fused.py > ${o}_tests.log 2>&1 || exit 1
+B="python bench.py --steps 20 --warmup 5 --cpu-sample 0 --sub-configs 0"
+for i in 1 2; do
+  timeout -k 10 300 $B > ${o}_bench_on$i.log 2>&1 || exit 1
+  timeout -k 10 300 $B --opt fused_next_mix=0 > ${o}_bench_off$i.log 2>&1 || exit 1
+  for v in "$@"; do
+    FAKEPTA_AMD_LIB=build/diag/lib_$v.so timeout -k 10 300 $B > ${o}_bench_${v}_$i.log 2>&1 || exit 1
+  done
+done
+timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d ${o}_tr_on -o run -- python bench.py --steps 10 --cpu-sample 0 --exact-launches 0 --sub-configs 0 > ${o}_tr_on.log 2>&1 || exit 1
+echo done
+}
+
+exp_ab_prev_rev() {
+# (formerly tools/gpu_ab_prev_rev.sh)
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+bash tools/gpu_ab_cfg.sh R6m "" c4 "" "LIB=build/diag/lib_r6f.so" || exit 1
+bash tools/gpu_ab_cfg.sh R6m "" c5 "" "LIB=build/diag/lib_r6f.so" || exit 1
+bash tools/gpu_ab_cfg.sh R6n "" c3 "" "LIB=build/diag/lib_r6f.so" || exit 1
+bash tools/gpu_ab_cfg.sh R6o "" c2 "" "LIB=build/diag/lib_r6f.so" || exit 1
 }
 
 fn="exp_$1"
