@@ -267,3 +267,39 @@ def test_next_mix_not_made_outside_its_layouts(ctx, capi, shipped):
     finally:
         ctx.batch_clear()
         ctx.set_options(shipped)
+
+
+def test_next_mix_c2_full_size(ctx, capi, shipped):
+    """BASELINE configs[1] at full size (100 psr x 2000 TOAs, RN30 + DM100 + HD30, R = 1024), blocks streamed as
+    bench.py runs them: the third block takes the mix the second block's kernel made (no k_gen_mix), equals the
+    option-off block bit for bit, and its realizations 0, 1, 511, 1023 match the oracle's own batch semantics."""
+    from fakepta import correlated_noises as cn
+    from fakepta import fake_pta as fp
+    from fakepta_amd.batch import BatchSimulator
+    from tests.helpers import oracle_segments
+    np.random.seed(0)
+    psrs = fp.make_fake_array(npsrs=100, Tobs=10, ntoas=2000, gaps=False, isotropic=True, toaerr=1e-7,
+                              backends="NUPPI.1400", custom_model={"RN": 30, "DM": 100, "Sv": None})
+    cn.add_common_correlated_noise(psrs, orf="hd", log10_A=-15, gamma=13 / 3)
+    sim = BatchSimulator(psrs, white=False, ctx=ctx)
+    try:
+        ctx.set_option(capi.OPT_SYNTH_PATH, 4)
+        outs = {}
+        for on in (0, 1):
+            ctx.set_option(capi.OPT_FUSED_NEXT_MIX, on)
+            for real0 in (0, 1024):
+                sim.synth(1024, seed=1234, real0=real0, to_host=False)
+            ctx.debug_fill_out(np.nan)
+            outs[on] = sim.synth(1024, seed=1234, real0=2048)
+            gi = ctx.batch_grid_info()
+            assert gi["interp_kernel"] == "k_grid_fused<8, false, true, true>", gi["interp_kernel"]
+            assert gi["next_mix_used"] == bool(on)
+        assert np.all(np.isfinite(outs[1]))
+        np.testing.assert_array_equal(outs[1], outs[0])
+        segs = oracle_segments(sim)
+        for r in (0, 1, 511, 1023):
+            want = O.batch_synth(sim.offs, sim.toas, sim.freqs, segs, 1234, 2048 + r, 1)[0]
+            assert_parity(outs[1][r], want, TOL)
+    finally:
+        ctx.batch_clear()
+        ctx.set_options(shipped)
