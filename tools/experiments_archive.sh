@@ -674,6 +674,15 @@ bash tools/gpu_ab_cfg.sh R6n "" c3 "" "LIB=build/diag/lib_r6f.so" || exit 1
 bash tools/gpu_ab_cfg.sh R6o "" c2 "" "LIB=build/diag/lib_r6f.so" || exit 1
 }
 
+exp_mix_early_ab() {
+# (formerly tools/gpu_mix_early_ab.sh; the variant switch FPTA_FUSED_MIX_EARLY was removed)
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+FAKEPTA_AMD_LIB=build/diag/lib_early3.so timeout -k 10 300 python -u -m pytest -x -q --timeout 240 --timeout-method thread tests/test_gpu_next_mix.py > gpurun_out/R6bb_tests.log 2>&1 || { tail -20 gpurun_out/R6bb_tests.log; exit 1; }
+tail -1 gpurun_out/R6bb_tests.log
+bash tools/gpu_ab_cfg.sh R6bb "" c2 "" "LIB=build/diag/lib_early3.so" "LIB=build/diag/lib_early5.so" || exit 1
+}
+
 fn="exp_$1"
 if ! declare -F "$fn" > /dev/null; then echo "unknown experiment: $fn" >&2; exit 2; fi
 echo "# archived experiment (provenance only, not runnable: it may call removed scripts):" >&2
