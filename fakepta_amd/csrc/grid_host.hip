@@ -1061,11 +1061,11 @@ int grid_run(fpta_ctx* c, Layout& L, SynthArgs& a, int32_t R_pad, bool pipe) {
       c->fused_q_ready = true;
     }
     f.queue = c->fused_q.as<uint32_t>();
-    // FPTA_OPT_FUSED_NEXT_MIX: the next block's common-signal mix (this seed and size from real0 + n_real) as spare-time
-    // tickets, into the coefficient buffer that block swaps in (c->coef2: this block's kernel and k_gen_mix's of the
-    // block before read it no more; grown already, so it is not reallocated under the kernel)
-    // (the next block's first realization: real0 + this block's stride from the last one of the same seed and size
-    // when that is a whole number of blocks (G ranks' interleaved blocks), else real0 + n_real)
+    // FPTA_OPT_FUSED_NEXT_MIX: the next block's common-signal mix (this seed and size) as spare-time tickets, into the
+    // coefficient buffer that block swaps in (c->coef2: this block's kernel and k_gen_mix's of the block before read
+    // it no more; grown already, so it is not reallocated under the kernel). The next block's first realization:
+    // real0 + this block's stride from the last one of the same seed and size when that is a whole number of blocks
+    // (G ranks' interleaved blocks), else real0 + n_real.
     c->next_mix_made = false;
     const int32_t nms = !fused_w && pipe && c->prev_psr ? next_mix_seg(c, L, R_pad) : -1;
     const size_t coef_bytes = sizeof(double) * (size_t)L.P * std::max(L.K, 1) * R_pad;
